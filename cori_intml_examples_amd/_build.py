@@ -1,0 +1,121 @@
+"""Native build driver: hipcc (gfx950) for the HIP kernels, g++ for the host-only C++.
+
+    python -m cori_intml_examples_amd._build          # incremental
+    python -m cori_intml_examples_amd._build --clean
+
+Outputs live IN-TREE next to this file (``_kernels*.so``, ``_h5lite*.so``) so they travel
+with the repository snapshot to the GPU box.  No hipify, no torch JIT cache.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "build")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ARCH = os.environ.get("INTML_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+HDF5_ROOT = os.environ.get("INTML_HDF5_ROOT", "/opt/conda")
+
+
+def _py_includes():
+    import pybind11
+    return ["-I" + sysconfig.get_paths()["include"], "-I" + pybind11.get_include()]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed: %s\n%s\n%s" % (" ".join(cmd), r.stdout, r.stderr))
+    return r
+
+
+def kernels_so_path():
+    return os.path.join(HERE, "_kernels" + EXT)
+
+
+def h5_so_path():
+    return os.path.join(HERE, "_h5lite" + EXT)
+
+
+def build_kernels(verbose=False, jobs=8):
+    kdir = os.path.join(CSRC, "kernels")
+    headers = glob.glob(os.path.join(kdir, "*.h"))
+    srcs = sorted(glob.glob(os.path.join(kdir, "*.hip"))) + [os.path.join(kdir, "bindings.cpp")]
+    os.makedirs(BUILD, exist_ok=True)
+    flags = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-I" + kdir,
+             "-Wno-unused-result", "-munsafe-fp-atomics"]
+    objs, jobs_list = [], []
+    for src in srcs:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if _newer(obj, [src] + headers):
+            extra = _py_includes() if src.endswith(".cpp") else []
+            lang = ["-x", "hip"] if src.endswith(".hip") else []
+            jobs_list.append([HIPCC] + flags + extra + lang + ["-c", src, "-o", obj])
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(lambda c: _run(c, verbose), jobs_list))
+    out = kernels_so_path()
+    if jobs_list or _newer(out, objs):
+        _run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", out] + objs, verbose)
+    return out
+
+
+def build_h5(verbose=False):
+    src = os.path.join(CSRC, "io", "h5lite.cpp")
+    out = h5_so_path()
+    if not os.path.exists(src):
+        return None
+    inc, lib = os.path.join(HDF5_ROOT, "include"), os.path.join(HDF5_ROOT, "lib")
+    if not os.path.exists(os.path.join(inc, "hdf5.h")):
+        if verbose:
+            print("libhdf5 headers not found under %s; skipping _h5lite" % HDF5_ROOT)
+        return None
+    if _newer(out, [src]):
+        cxx = shutil.which("g++") or "c++"
+        _run([cxx, "-O2", "-shared", "-fPIC", "-std=c++17", src, "-o", out, "-I" + inc] + _py_includes()
+             + ["-L" + lib, "-Wl,-rpath," + lib, "-lhdf5"], verbose)
+    return out
+
+
+def build_all(verbose=False):
+    outs = [build_kernels(verbose)]
+    h5 = build_h5(verbose)
+    if h5:
+        outs.append(h5)
+    return outs
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    if a.clean:
+        shutil.rmtree(BUILD, ignore_errors=True)
+        for p in (kernels_so_path(), h5_so_path()):
+            if os.path.exists(p):
+                os.remove(p)
+    for o in build_all(a.verbose):
+        print("built", o)
+
+
+if __name__ == "__main__":
+    main()

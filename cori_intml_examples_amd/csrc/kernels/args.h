@@ -1,0 +1,160 @@
+// Kernel argument structs (shared by the .hip translation units and the pybind11 bindings).
+// Pointers are device pointers; Python fills the structs once per (plan, batch size) and
+// re-launches them every step (eagerly or under HIP-graph capture).
+#pragma once
+#include "common.h"
+
+// "Backward through the previous stage": turn dL/d(prev stage output) into dL/d(prev
+// pre-activation) = apply the previous stage's dropout mask (regenerated), ReLU mask
+// (from its saved output) and 2x2 max-pool routing (from its saved argmax code), writing
+// the full-resolution gradient the previous layer's wgrad/dgrad consume.
+struct BwdThrough {
+  const bf16* prev_out = nullptr;     // saved output of the previous stage [.., pCs]
+  const uint8_t* prev_code = nullptr; // saved pool argmax codes
+  int prev_relu = 0, prev_pool = 0;
+  int pH = 1, pW = 1, pC = 0, pCs = 0;  // previous stage output geometry (post-pool)
+  int cH = 1, cW = 1;                   // previous conv's full-resolution grid
+  uint32_t drop_thr = 0;
+  float drop_scale = 1.f;
+  uint32_t seed = 0, stream_id = 0;
+  bf16* dy = nullptr;                   // output [B, cH, cW, pCs] (or [B, pH, pW, pCs])
+};
+
+// Implicit-GEMM convolution / 1x1 "dense as conv" (fwd, dgrad, dense-dX).
+struct ConvMMArgs {
+  const bf16* x = nullptr;       // input activations [B, H, W, Cs_in]
+  int B = 0, H = 0, W = 0, Cs_in = 0;
+  int Ho = 0, Wo = 0;            // GEMM row space = conv output grid
+  int KH = 1, KW = 1, stride = 1, pad_t = 0, pad_l = 0, in_dil = 1;
+  int KS = 0;                    // number of 32-wide k-steps
+  const bf16* wpk = nullptr;     // fragment-major pack
+  int NT = 0;                    // n-tiles in the pack
+  const float* bias = nullptr;   // fp32 bias (fwd) or null
+  int N = 0;                     // valid output channels (fwd)
+  int mode = 0;                  // 0: forward epilogue, 1: backward-through-previous-stage
+  int flat_out = 0;              // mode 1: GEMM columns are flattened (y, x, c) of prev output
+  // forward epilogue
+  int relu = 0, pool = 0;
+  bf16* out = nullptr;
+  int Cs_out = 0, Hp = 0, Wp = 0;
+  uint8_t* code = nullptr;
+  uint32_t drop_thr = 0;         // 0 = no dropout
+  float drop_scale = 1.f;
+  uint32_t seed = 0, stream_id = 0;
+  const StepState* st = nullptr;
+  // backward-through epilogue (mode 1)
+  BwdThrough bt;
+};
+
+// Weight gradient: dW[k][n] = sum_pixels im2col(x)[p][k] * dY[p][n]  (split over pixels)
+struct WgradArgs {
+  const bf16* x = nullptr;
+  int B = 0, H = 0, W = 0, Cs_in = 0;
+  int Ho = 0, Wo = 0, KH = 1, KW = 1, stride = 1, pad_t = 0, pad_l = 0;
+  int Ktiles = 0;                // 16-wide k tiles over k = tap*Cs_in + ci
+  const bf16* dy = nullptr;
+  int Cs_dy = 0;
+  int NT = 0;                    // 16-wide n tiles
+  int P = 0;                     // pixels (B*Ho*Wo)
+  int px_per_split = 0;          // multiple of 32
+  int KT = 0;                    // k tiles per workgroup (grid.y groups)
+  float* slab = nullptr;         // [S][Ktiles*16][NT*16]
+  float* bslab = nullptr;        // [S][NT*16] or null
+};
+
+// Dense forward, split-K partial products: part[s][m][n]
+struct DenseFwdArgs {
+  const bf16* x = nullptr;
+  int M = 0, Ks = 0;             // x is [M][Ks]
+  const bf16* wpk = nullptr;
+  int NT = 0, KS = 0;            // pack geometry
+  int splits = 1, ks_per_split = 0;
+  float* part = nullptr;         // [splits][M][NT*16]
+};
+
+// Split-K reduction + bias + activation + dropout -> bf16 [M][Ns]
+struct DenseEpiArgs {
+  const float* part = nullptr;
+  int splits = 1, M = 0, N = 0, Ns = 0, ldp = 0;
+  const float* bias = nullptr;
+  int relu = 0;
+  bf16* out = nullptr;
+  uint32_t drop_thr = 0;
+  float drop_scale = 1.f;
+  uint32_t seed = 0, stream_id = 0;
+  const StepState* st = nullptr;
+};
+
+// Fused output head: logits = h @ W + b, activation, loss, metrics, and (training)
+// dz, dW/db partial slabs and dh_prev (through the previous dense's relu/dropout).
+struct HeadArgs {
+  const bf16* h = nullptr;       // [M][Ks]
+  int M = 0, K = 0, Ks = 0, N = 0;
+  int flat_C = 0, flat_Cs = 0;   // flatten mapping of h's columns (keras k -> padded)
+  const float* w = nullptr;      // fp32 master kernel [K][N] (keras layout)
+  const float* bias = nullptr;
+  const float* y = nullptr;      // targets [M][N]
+  int act = 0;                   // 0 linear(mse), 1 sigmoid(bce), 2 softmax(cce)
+  int training = 0;
+  float inv_bs = 1.f;
+  StepState* st = nullptr;       // metrics accumulation
+  float* probs = nullptr;        // predict mode: [M][N]
+  float* wslab = nullptr;        // [nblocks][K][N]
+  float* bslab = nullptr;        // [nblocks][N]
+  // gradient wrt the previous stage (hidden dense or flattened conv); bt.dy == null: skip
+  BwdThrough bt;
+};
+
+struct GatherArgs {
+  const bf16* xs = nullptr;      // dataset [Nd][R] bf16
+  const float* ys = nullptr;     // [Nd][C]
+  const int* perm = nullptr;     // or null (identity / eval)
+  const StepState* st = nullptr;
+  int bs = 0, R = 0, C = 0, Nd = 0;
+  bf16* xb = nullptr;
+  float* yb = nullptr;
+};
+
+struct StepBeginArgs {
+  StepState* st = nullptr;
+  int training = 1;
+  int bs = 0;
+  int opt_kind = 0;
+  float beta1 = 0.9f, beta2 = 0.999f, decay = 0.f, schedule_decay = 0.004f;
+};
+
+struct OptimArgs {
+  float* p = nullptr;
+  const float* g = nullptr;
+  float* s0 = nullptr;
+  float* s1 = nullptr;
+  int n = 0;
+  const StepState* st = nullptr;
+  int kind = 0;
+  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-7f, rho = 0.95f, momentum = 0.f;
+  int nesterov = 0;
+  float grad_scale = 1.f;
+  int pack_only = 0;
+  bf16* arena = nullptr;
+};
+
+// Slab reduction descriptors: sum split-partials into the flat fp32 grad buffer in
+// Keras layout.
+enum RedType { RED_CONVW = 0, RED_BIAS = 1, RED_FLATW = 2 };
+
+struct RedDesc {
+  const float* slab;
+  long long stride_s;  // elements between consecutive splits
+  int S;
+  int ld;              // row stride (n) of the slab
+  int dst_off, numel, type;
+  int KH, KW, Cin, Cout, Cs;   // conv: k = tap*Cs + ci ; flat: C=Cin (channels), Cs
+  int pad_;
+};
+
+#define MAX_RED 16
+struct RedTable {
+  int n;
+  int pad_[3];
+  RedDesc d[MAX_RED];
+};

@@ -1,0 +1,149 @@
+// pybind11 bindings for the gfx950 kernels.  Argument structs are exposed as Python
+// classes (pointer fields take integer device addresses, e.g. tensor.data_ptr()); the
+// launch_* functions take the HIP stream as an integer (torch stream.cuda_stream), so
+// every launch is capturable into a HIP graph by torch.cuda.graph.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "args.h"
+
+namespace py = pybind11;
+
+void launch_conv_mm(const ConvMMArgs& a, int ntc, int gx, hipStream_t s);
+size_t conv_mm_lds_bytes(const ConvMMArgs& a, int ntc, bool cs4);
+void launch_wgrad(const WgradArgs& a, int ktw, int ntt, int splits, hipStream_t s);
+size_t wgrad_lds_bytes(int KT, int NTT);
+void launch_dense_fwd(const DenseFwdArgs& a, hipStream_t s);
+void launch_dense_epi(const DenseEpiArgs& a, hipStream_t s);
+void launch_head(const HeadArgs& a, hipStream_t s);
+void launch_step_begin(const StepBeginArgs& a, hipStream_t s);
+void launch_gather(const GatherArgs& a, hipStream_t s);
+void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s);
+void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s);
+
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+#define RW(cls, f) .def_readwrite(#f, &cls::f)
+#define PTR(cls, f)                                                                   \
+  .def_property(                                                                      \
+      #f, [](const cls& o) { return reinterpret_cast<uintptr_t>(o.f); },              \
+      [](cls& o, uintptr_t v) { o.f = reinterpret_cast<decltype(o.f)>(v); })
+
+static void check_last(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_kernels, m) {
+  m.doc() = "cori_intml_examples_amd gfx950 HIP kernels";
+
+  py::class_<BwdThrough>(m, "BwdThrough")
+      .def(py::init<>())
+      PTR(BwdThrough, prev_out) PTR(BwdThrough, prev_code) RW(BwdThrough, prev_relu)
+      RW(BwdThrough, prev_pool) RW(BwdThrough, pH) RW(BwdThrough, pW) RW(BwdThrough, pC)
+      RW(BwdThrough, pCs) RW(BwdThrough, cH) RW(BwdThrough, cW) RW(BwdThrough, drop_thr)
+      RW(BwdThrough, drop_scale) RW(BwdThrough, seed) RW(BwdThrough, stream_id) PTR(BwdThrough, dy);
+
+  py::class_<ConvMMArgs>(m, "ConvMMArgs")
+      .def(py::init<>())
+      PTR(ConvMMArgs, x) RW(ConvMMArgs, B) RW(ConvMMArgs, H) RW(ConvMMArgs, W) RW(ConvMMArgs, Cs_in)
+      RW(ConvMMArgs, Ho) RW(ConvMMArgs, Wo) RW(ConvMMArgs, KH) RW(ConvMMArgs, KW) RW(ConvMMArgs, stride)
+      RW(ConvMMArgs, pad_t) RW(ConvMMArgs, pad_l) RW(ConvMMArgs, in_dil) RW(ConvMMArgs, KS)
+      PTR(ConvMMArgs, wpk) RW(ConvMMArgs, NT) PTR(ConvMMArgs, bias) RW(ConvMMArgs, N) RW(ConvMMArgs, mode)
+      RW(ConvMMArgs, flat_out) RW(ConvMMArgs, relu) RW(ConvMMArgs, pool) PTR(ConvMMArgs, out)
+      RW(ConvMMArgs, Cs_out) RW(ConvMMArgs, Hp) RW(ConvMMArgs, Wp) PTR(ConvMMArgs, code)
+      RW(ConvMMArgs, drop_thr) RW(ConvMMArgs, drop_scale) RW(ConvMMArgs, seed) RW(ConvMMArgs, stream_id)
+      PTR(ConvMMArgs, st) RW(ConvMMArgs, bt);
+
+  py::class_<WgradArgs>(m, "WgradArgs")
+      .def(py::init<>())
+      PTR(WgradArgs, x) RW(WgradArgs, B) RW(WgradArgs, H) RW(WgradArgs, W) RW(WgradArgs, Cs_in)
+      RW(WgradArgs, Ho) RW(WgradArgs, Wo) RW(WgradArgs, KH) RW(WgradArgs, KW) RW(WgradArgs, stride)
+      RW(WgradArgs, pad_t) RW(WgradArgs, pad_l) RW(WgradArgs, Ktiles) PTR(WgradArgs, dy)
+      RW(WgradArgs, Cs_dy) RW(WgradArgs, NT) RW(WgradArgs, P) RW(WgradArgs, px_per_split)
+      RW(WgradArgs, KT) PTR(WgradArgs, slab) PTR(WgradArgs, bslab);
+
+  py::class_<DenseFwdArgs>(m, "DenseFwdArgs")
+      .def(py::init<>())
+      PTR(DenseFwdArgs, x) RW(DenseFwdArgs, M) RW(DenseFwdArgs, Ks) PTR(DenseFwdArgs, wpk)
+      RW(DenseFwdArgs, NT) RW(DenseFwdArgs, KS) RW(DenseFwdArgs, splits) RW(DenseFwdArgs, ks_per_split)
+      PTR(DenseFwdArgs, part);
+
+  py::class_<DenseEpiArgs>(m, "DenseEpiArgs")
+      .def(py::init<>())
+      PTR(DenseEpiArgs, part) RW(DenseEpiArgs, splits) RW(DenseEpiArgs, M) RW(DenseEpiArgs, N)
+      RW(DenseEpiArgs, Ns) RW(DenseEpiArgs, ldp) PTR(DenseEpiArgs, bias) RW(DenseEpiArgs, relu)
+      PTR(DenseEpiArgs, out) RW(DenseEpiArgs, drop_thr) RW(DenseEpiArgs, drop_scale)
+      RW(DenseEpiArgs, seed) RW(DenseEpiArgs, stream_id) PTR(DenseEpiArgs, st);
+
+  py::class_<HeadArgs>(m, "HeadArgs")
+      .def(py::init<>())
+      PTR(HeadArgs, h) RW(HeadArgs, M) RW(HeadArgs, K) RW(HeadArgs, Ks) RW(HeadArgs, N)
+      RW(HeadArgs, flat_C) RW(HeadArgs, flat_Cs) PTR(HeadArgs, w) PTR(HeadArgs, bias) PTR(HeadArgs, y)
+      RW(HeadArgs, act) RW(HeadArgs, training) RW(HeadArgs, inv_bs) PTR(HeadArgs, st) PTR(HeadArgs, probs)
+      PTR(HeadArgs, wslab) PTR(HeadArgs, bslab) RW(HeadArgs, bt);
+
+  py::class_<GatherArgs>(m, "GatherArgs")
+      .def(py::init<>())
+      PTR(GatherArgs, xs) PTR(GatherArgs, ys) PTR(GatherArgs, perm) PTR(GatherArgs, st)
+      RW(GatherArgs, bs) RW(GatherArgs, R) RW(GatherArgs, C) RW(GatherArgs, Nd) PTR(GatherArgs, xb)
+      PTR(GatherArgs, yb);
+
+  py::class_<StepBeginArgs>(m, "StepBeginArgs")
+      .def(py::init<>())
+      PTR(StepBeginArgs, st) RW(StepBeginArgs, training) RW(StepBeginArgs, bs) RW(StepBeginArgs, opt_kind)
+      RW(StepBeginArgs, beta1) RW(StepBeginArgs, beta2) RW(StepBeginArgs, decay)
+      RW(StepBeginArgs, schedule_decay);
+
+  py::class_<OptimArgs>(m, "OptimArgs")
+      .def(py::init<>())
+      PTR(OptimArgs, p) PTR(OptimArgs, g) PTR(OptimArgs, s0) PTR(OptimArgs, s1) RW(OptimArgs, n)
+      PTR(OptimArgs, st) RW(OptimArgs, kind) RW(OptimArgs, beta1) RW(OptimArgs, beta2) RW(OptimArgs, eps)
+      RW(OptimArgs, rho) RW(OptimArgs, momentum) RW(OptimArgs, nesterov) RW(OptimArgs, grad_scale)
+      RW(OptimArgs, pack_only) PTR(OptimArgs, arena);
+
+  py::class_<PackTable>(m, "PackTable")
+      .def(py::init([]() { PackTable t; memset(&t, 0, sizeof(t)); return t; }))
+      .def_readonly("n", &PackTable::n)
+      .def("add", [](PackTable& t, int src_off, int numel, int type, int KH, int KW, int Cin, int Cout,
+                      int Cs, int NT, long long dst_off) {
+        if (t.n >= MAX_PACK) throw std::runtime_error("PackTable full");
+        PackDesc& d = t.d[t.n++];
+        d.src_off = src_off; d.numel = numel; d.type = type; d.KH = KH; d.KW = KW; d.Cin = Cin;
+        d.Cout = Cout; d.Cs = Cs; d.NT = NT; d.pad_ = 0; d.dst_off = dst_off;
+      });
+
+  py::class_<RedTable>(m, "RedTable")
+      .def(py::init([]() { RedTable t; memset(&t, 0, sizeof(t)); return t; }))
+      .def_readonly("n", &RedTable::n)
+      .def("add", [](RedTable& t, uintptr_t slab, long long stride_s, int S, int ld, int dst_off, int numel,
+                      int type, int KH, int KW, int Cin, int Cout, int Cs) {
+        if (t.n >= MAX_RED) throw std::runtime_error("RedTable full");
+        RedDesc& d = t.d[t.n++];
+        d.slab = reinterpret_cast<const float*>(slab); d.stride_s = stride_s; d.S = S; d.ld = ld;
+        d.dst_off = dst_off; d.numel = numel; d.type = type; d.KH = KH; d.KW = KW; d.Cin = Cin;
+        d.Cout = Cout; d.Cs = Cs; d.pad_ = 0;
+      });
+
+  m.attr("STEP_STATE_BYTES") = (int)sizeof(StepState);
+  m.attr("STEP_STATE_METRICS_OFFSET") = (int)offsetof(StepState, metrics);
+  m.attr("STEP_STATE_MSCHED_OFFSET") = (int)offsetof(StepState, m_schedule);
+  m.attr("STEP_STATE_LR_OFFSET") = (int)offsetof(StepState, lr);
+  m.attr("STEP_STATE_DATA_OFFSET") = (int)offsetof(StepState, data_x);
+  m.attr("STEP_STATE_DATAN_OFFSET") = (int)offsetof(StepState, data_n);
+
+  m.def("conv_mm_lds_bytes", [](const ConvMMArgs& a, int ntc) { return conv_mm_lds_bytes(a, ntc, a.Cs_in == 4); });
+  m.def("wgrad_lds_bytes", &wgrad_lds_bytes);
+  m.def("conv_mm", [](const ConvMMArgs& a, int ntc, int gx, uintptr_t s) {
+    launch_conv_mm(a, ntc, gx, S(s)); check_last("conv_mm"); });
+  m.def("wgrad", [](const WgradArgs& a, int ktw, int ntt, int splits, uintptr_t s) {
+    launch_wgrad(a, ktw, ntt, splits, S(s)); check_last("wgrad"); });
+  m.def("dense_fwd", [](const DenseFwdArgs& a, uintptr_t s) { launch_dense_fwd(a, S(s)); check_last("dense_fwd"); });
+  m.def("dense_epi", [](const DenseEpiArgs& a, uintptr_t s) { launch_dense_epi(a, S(s)); check_last("dense_epi"); });
+  m.def("head", [](const HeadArgs& a, uintptr_t s) { launch_head(a, S(s)); check_last("head"); });
+  m.def("step_begin", [](const StepBeginArgs& a, uintptr_t s) { launch_step_begin(a, S(s)); check_last("step_begin"); });
+  m.def("gather", [](const GatherArgs& a, uintptr_t s) { launch_gather(a, S(s)); check_last("gather"); });
+  m.def("slab_reduce", [](uintptr_t grad, int lo, int hi, const RedTable& t, uintptr_t s) {
+    launch_slab_reduce(reinterpret_cast<float*>(grad), lo, hi, t, S(s)); check_last("slab_reduce"); });
+  m.def("optim", [](const OptimArgs& a, const PackTable& t, uintptr_t s) { launch_optim(a, t, S(s)); check_last("optim"); });
+}

@@ -1,0 +1,126 @@
+// Shared definitions for the gfx950 (CDNA4 / MI355X) kernels of cori_intml_examples_amd.
+//
+// Conventions (see models/plan.py and models/executor_hip.py):
+//   * activations are bf16 NHWC with a padded channel stride Cs (multiple of 8; the
+//     network input uses Cs = 4): padded channels hold exact zeros;
+//   * weights used by MFMA kernels are bf16 "fragment-major" packs produced by the
+//     fused optimizer from the fp32 master copy:
+//       pack[((ks * NT + nt) * 64 + lane) * 8 + j] = B[k = 32 ks + 8 (lane >> 4) + j]
+//                                                     [n = 16 nt + (lane & 15)]
+//     i.e. exactly the B-operand fragment of v_mfma_f32_16x16x32_bf16, so a wave
+//     loads a whole fragment with one 16-byte access per lane;
+//   * all waves are 64 lanes; workgroups are 256 threads (4 waves).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 zero_bf16x8() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.0f;
+  return z;
+}
+
+__device__ __forceinline__ bf16x8 load_bf16x8(const bf16* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+
+__device__ __forceinline__ bf16x4 load_bf16x4(const bf16* p) {
+  return *reinterpret_cast<const bf16x4*>(p);
+}
+
+__device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
+__device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
+
+// ---------------------------------------------------------------------------------------
+// Counter-based RNG (bit-identical twin of ops/rng.py)
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t rng_u32(uint32_t idx, uint32_t seed, uint32_t stream, uint32_t step) {
+  uint32_t x = idx ^ (step * 0x9E3779B9u);
+  x = fmix32(x ^ seed);
+  x = fmix32(x + stream * 0x85EBCA6Bu);
+  return x;
+}
+
+// keep iff (u >> 8) >= thr ; scale = 1/(1-rate)
+__device__ __forceinline__ bool dropout_keep(uint32_t idx, uint32_t seed, uint32_t stream, uint32_t step,
+                                             uint32_t thr) {
+  return (rng_u32(idx, seed, stream, step) >> 8) >= thr;
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-step device state, advanced by step_begin<<<1,64>>> at the head of each captured
+// training step (race-free scalar bookkeeping: iteration counter, data cursor, LR and
+// optimizer bias-correction scalars).
+struct StepState {
+  int t;          // optimizer iterations completed (Keras `iterations`)
+  int pos;        // next data cursor
+  int cur_pos;    // cursor of the step in flight
+  int eval_pos;   // cursor for eval / predict steps
+  float lr;       // base learning rate (host-written)
+  float lr_eff;   // lr after Keras `decay`
+  float s[6];     // optimizer scalars for this step (meaning depends on optimizer kind)
+  double m_schedule;  // Nadam running product
+  double metrics[4];  // loss_sum, correct_sum, count, spare
+  // bound dataset (host-written when the executor switches datasets, so captured graphs
+  // are dataset-independent): x rows [n][R] bf16, targets [n][C] fp32, epoch permutation
+  unsigned long long data_x, data_y, perm;
+  int data_n, data_R, data_C, use_perm;
+};
+
+enum OptKind { OPT_SGD = 0, OPT_RMSPROP = 1, OPT_ADADELTA = 2, OPT_ADAM = 3, OPT_NADAM = 4 };
+
+// ---------------------------------------------------------------------------------------
+// Pack / unpack descriptors (fp32 master <-> bf16 fragment packs, grad slabs -> master layout)
+enum PackType {
+  PACK_CONV_FWD = 0,   // B[k=(tap,ci)][n=co] = W[ky][kx][ci][co]
+  PACK_CONV_DGRAD = 1, // B[k=(tap',co)][n=ci] = W[KH-1-ky'][KW-1-kx'][ci][co]
+  PACK_DENSE_FWD = 2,  // B[k=padded flat][n] = W[k_keras][n]
+  PACK_DENSE_BWD = 3,  // B[k=n_dense][n=padded flat] = W[k_keras][k]
+};
+
+struct PackDesc {
+  int src_off;   // offset of the tensor in the flat master buffer
+  int numel;
+  int type;
+  int KH, KW, Cin, Cout;  // conv dims; dense: KH=Hf, KW=Wf (flatten source), Cin=Cf, Cout=N
+  int Cs;        // padded channel stride of the relevant activation (fwd: input; dgrad: output)
+  int NT;        // n-tiles of the pack
+  int pad_;
+  long long dst_off;  // element offset in the bf16 pack arena
+};
+
+#define MAX_PACK 24
+
+struct PackTable {
+  int n;
+  int pad_[3];
+  PackDesc d[MAX_PACK];
+};
+
+// Dense flatten mapping: keras flat index (h,w,c) over C channels -> padded index over Cs.
+__device__ __forceinline__ int flat_keras_to_padded(int k, int C, int Cs) {
+  int hw = k / C;
+  int c = k - hw * C;
+  return hw * Cs + c;
+}

@@ -1,0 +1,771 @@
+"""HIP / gfx950 backend: executes a Plan with the hand-written CDNA4 kernels.
+
+One training step is a fixed sequence of ~15-20 launches (SURVEY.md §2.7 "fused op
+boundaries"), captured once per batch size into a HIP graph and replayed:
+
+  step_begin -> gather -> conv_mm(fwd) x C -> [dense split-K + epilogue] x D -> head
+  -> [wgrad(dense) + conv_mm(dX, bwd-through)] x D -> [wgrad(conv) + conv_mm(dgrad,
+  bwd-through)] x C -> slab_reduce (per DP bucket) -> [RCCL all-reduce] -> optim(+pack)
+
+Activations are bf16 NHWC with channel strides padded to 8 (input: 4); weights live in
+ONE fp32 master buffer (Keras layout) and are mirrored into bf16 fragment-major packs by
+the optimizer kernel; gradients land in ONE flat fp32 buffer via deterministic slab
+reductions.  Metrics accumulate on the device; the host syncs once per epoch.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..ops.hip import kernels
+from ..ops.rng import keep_threshold
+from ..utils.env import env_flag
+from .executor_base import DeviceData, Executor, prepare_targets
+from .plan import Plan
+
+BF16 = torch.bfloat16
+OPT_KIND = {"sgd": 0, "rmsprop": 1, "adadelta": 2, "adam": 3, "nadam": 4}
+PACK_CONV_FWD, PACK_CONV_DGRAD, PACK_DENSE_FWD, PACK_DENSE_BWD = 0, 1, 2, 3
+RED_CONVW, RED_BIAS, RED_FLATW = 0, 1, 2
+
+
+def cdiv(a, b):
+    return -(-a // b)
+
+
+def r8(x):
+    return cdiv(x, 8) * 8
+
+
+def _pow2_le(x, cap):
+    v = 1
+    while v * 2 <= min(x, cap):
+        v *= 2
+    return v
+
+
+@dataclass
+class Src:
+    """An activation buffer feeding the next stage (for flatten mapping / bwd-through)."""
+    kind: str            # 'input' | 'conv' | 'dense'
+    idx: int
+    C: int               # logical channels (flatten mapping)
+    Cs: int              # padded channel stride
+    H: int = 1
+    W: int = 1
+
+    @property
+    def width(self):
+        return self.H * self.W * self.Cs
+
+
+@dataclass
+class ConvGeo:
+    i: int
+    H: int
+    W: int
+    Cin: int
+    Cs_in: int
+    Ho: int
+    Wo: int
+    Cout: int
+    Cs_out: int
+    Hp: int
+    Wp: int
+    KH: int
+    KW: int
+    stride: int
+    pad_t: int
+    pad_l: int
+    pool: bool
+    relu: bool
+    rate: float
+    stream: int
+    KS: int = 0
+    NT: int = 0
+    KSd: int = 0
+    NTd: int = 0
+    pack_fwd: int = 0
+    pack_dgrad: int = -1
+
+
+@dataclass
+class DenseGeo:
+    j: int
+    src: Src
+    K: int
+    N: int
+    Ns: int
+    relu: bool
+    rate: float
+    stream: int
+    KS: int = 0
+    NT: int = 0
+    KSb: int = 0
+    NTb: int = 0
+    pack_fwd: int = 0
+    pack_bwd: int = -1
+
+
+class HipExecutor(Executor):
+    def __init__(self, plan: Plan, store, optimizer, seed: int):
+        super().__init__(plan, store, optimizer, seed)
+        self.K = kernels()
+        self.device = store.device
+        if self.device.type != "cuda":
+            raise RuntimeError("HipExecutor needs a GPU device")
+        torch.cuda.set_device(self.device)
+        self.use_graphs = env_flag("INTML_GRAPHS", True)
+        self.state = torch.zeros(self.K.STEP_STATE_BYTES, dtype=torch.uint8, device=self.device)
+        self._st_i32 = self.state.view(torch.int32)
+        self._st_f32 = self.state.view(torch.float32)
+        self._st_f64 = self.state.view(torch.float64)
+        self._st_i64 = self.state.view(torch.int64)
+        self._st_f64[self.K.STEP_STATE_MSCHED_OFFSET // 8] = 1.0
+        base = getattr(optimizer, "_base_optimizer", optimizer)
+        self.opt = base
+        n_slots = getattr(base, "n_slots", 0)
+        self.slots = [torch.zeros(store.capacity, dtype=torch.float32, device=self.device) for _ in range(n_slots)]
+        self._build_geometry()
+        self._build_packs()
+        self._plans: Dict[Tuple[int, str], "BatchPlan"] = {}
+        self._lr_host = None
+        self._expected_pos = None
+        self._bound_data = None
+        self._bound_ref = None
+        self._perm_obj = None
+        self._perm_buf = None
+        self._metrics_prev = (0.0, 0.0, 0.0)
+        self.grad_scale = 1.0
+        self.params_changed()
+
+    # ------------------------------------------------------------------ geometry
+    def _build_geometry(self):
+        p = self.plan
+        H0, W0, C0 = (p.input_shape + (1, 1))[:3] if len(p.input_shape) == 3 else (1, 1, p.input_shape[0])
+        if len(p.input_shape) == 1:
+            H0, W0, C0 = 1, 1, p.input_shape[0]
+        self.in_C = C0
+        self.in_Cs = 4 if C0 <= 4 else r8(C0)
+        self.in_H, self.in_W = H0, W0
+        self.convs: List[ConvGeo] = []
+        src = Src("input", 0, C0, self.in_Cs, H0, W0)
+        H, W, Cin, Cs_in = H0, W0, C0, self.in_Cs
+        for i, cs in enumerate(p.convs):
+            Ho, Wo, Cout = cs.conv_shape
+            Hp, Wp, _ = cs.out_shape
+            pt, _, pl, _ = cs.pads
+            kh, kw = cs.conv.kernel_size
+            g = ConvGeo(i, H, W, Cin, Cs_in, Ho, Wo, Cout, r8(Cout), Hp, Wp, kh, kw, cs.stride, pt, pl,
+                        cs.pool is not None, cs.relu, cs.rate, cs.stream)
+            g.KS = cdiv(kh * kw * Cs_in, 32)
+            g.NT = cdiv(Cout, 16)
+            if i > 0:
+                g.KSd = cdiv(kh * kw * g.Cs_out, 32)
+                g.NTd = cdiv(Cin, 16)
+            self.convs.append(g)
+            H, W, Cin, Cs_in = Hp, Wp, Cout, g.Cs_out
+            src = Src("conv", i, Cout, g.Cs_out, Hp, Wp)
+        self.denses: List[DenseGeo] = []
+        for j, ds in enumerate(p.denses):
+            g = DenseGeo(j, src, ds.K, ds.N, r8(ds.N), ds.relu, ds.rate, ds.stream)
+            if g.K != src.H * src.W * src.C:
+                raise ValueError("dense %d input width mismatch" % j)
+            g.KS = cdiv(src.width, 32)
+            g.NT = cdiv(ds.N, 16)
+            if j > 0 or self.convs:
+                g.KSb = cdiv(g.Ns, 32)
+                g.NTb = cdiv(src.width, 16)
+            self.denses.append(g)
+            src = Src("dense", j, ds.N, g.Ns)
+        self.head_src = src
+        hd = p.head
+        if hd.K != src.H * src.W * src.C:
+            raise ValueError("head input width mismatch")
+        if hd.N > 16:
+            raise NotImplementedError("output layers wider than 16 units")
+        self.head_act = {None: 0, "sigmoid": 1, "softmax": 2}[hd.activation]
+
+    def _build_packs(self):
+        K = self.K
+        st = self.store
+        tab = K.PackTable()
+        off = 0
+
+        def alloc(ks, nt):
+            nonlocal off
+            o = off
+            off += ks * nt * 64 * 8
+            return o
+
+        for g, cs in zip(self.convs, self.plan.convs):
+            sp = st.spec(cs.conv, "kernel")
+            g.pack_fwd = alloc(g.KS, g.NT)
+            tab.add(sp.offset, sp.numel, PACK_CONV_FWD, g.KH, g.KW, g.Cin, g.Cout, g.Cs_in, g.NT, g.pack_fwd)
+            if g.i > 0:
+                g.pack_dgrad = alloc(g.KSd, g.NTd)
+                tab.add(sp.offset, sp.numel, PACK_CONV_DGRAD, g.KH, g.KW, g.Cin, g.Cout, g.Cs_out, g.NTd,
+                        g.pack_dgrad)
+        for g, ds in zip(self.denses, self.plan.denses):
+            sp = st.spec(ds.dense, "kernel")
+            g.pack_fwd = alloc(g.KS, g.NT)
+            tab.add(sp.offset, sp.numel, PACK_DENSE_FWD, 0, 0, g.src.C, g.N, g.src.Cs, g.NT, g.pack_fwd)
+            if g.KSb:
+                g.pack_bwd = alloc(g.KSb, g.NTb)
+                tab.add(sp.offset, sp.numel, PACK_DENSE_BWD, 0, 0, g.src.C, g.N, g.src.Cs, g.NTb, g.pack_bwd)
+        self.pack_table = tab
+        self.arena = torch.zeros(max(off, 8), dtype=BF16, device=self.device)
+
+    # ------------------------------------------------------------------ params / optimizer
+    def _optim_args(self, pack_only: bool):
+        K = self.K
+        a = K.OptimArgs()
+        a.p = self.store.master.data_ptr()
+        a.g = self.store.grad.data_ptr()
+        if self.slots:
+            a.s0 = self.slots[0].data_ptr()
+        if len(self.slots) > 1:
+            a.s1 = self.slots[1].data_ptr()
+        a.n = self.store.numel
+        a.st = self.state.data_ptr()
+        o = self.opt
+        a.kind = OPT_KIND[o.kind]
+        a.beta1 = getattr(o, "beta_1", 0.9)
+        a.beta2 = getattr(o, "beta_2", 0.999)
+        a.eps = getattr(o, "epsilon", 1e-7)
+        a.rho = getattr(o, "rho", 0.95)
+        a.momentum = getattr(o, "momentum", 0.0)
+        a.nesterov = int(getattr(o, "nesterov", False))
+        a.grad_scale = self.grad_scale
+        a.pack_only = int(pack_only)
+        a.arena = self.arena.data_ptr()
+        return a
+
+    def params_changed(self):
+        self.K.optim(self._optim_args(True), self.pack_table, torch.cuda.current_stream().cuda_stream)
+
+    def optimizer_state(self):
+        return [s[:self.store.numel] for s in self.slots]
+
+    def set_optimizer_state(self, iterations, slots):
+        self.opt.iterations = int(iterations)
+        self._st_i32[0] = int(iterations)
+        for dst, src in zip(self.slots, slots):
+            dst[:self.store.numel].copy_(torch.as_tensor(src, device=self.device).reshape(-1))
+
+    def _sync_lr(self):
+        lr = float(self.opt.lr)
+        if lr != self._lr_host:
+            self._st_f32[self.K.STEP_STATE_LR_OFFSET // 4] = lr
+            self._lr_host = lr
+
+    # ------------------------------------------------------------------ data
+    def upload(self, x, y):
+        if x is None:
+            return None
+        x = np.asarray(x)
+        if tuple(x.shape[1:]) != tuple(self.plan.input_shape):
+            raise ValueError("input shape %s != model input %s" % (x.shape[1:], self.plan.input_shape))
+        n = x.shape[0]
+        xt = torch.as_tensor(np.ascontiguousarray(x, dtype=np.float32)).to(self.device, non_blocking=False)
+        xt = xt.reshape(n, self.in_H, self.in_W, self.in_C)
+        xs = torch.zeros(n, self.in_H, self.in_W, self.in_Cs, dtype=BF16, device=self.device)
+        xs[..., :self.in_C] = xt.to(BF16)
+        del xt
+        yt = None
+        if y is not None:
+            yt = torch.as_tensor(prepare_targets(y, self.plan)).to(self.device)
+        else:
+            yt = torch.zeros(n, self.plan.head.N, dtype=torch.float32, device=self.device)
+        return DeviceData(xs.reshape(n, -1), yt, n)
+
+    def _bind_data(self, data: DeviceData, perm: Optional[torch.Tensor]):
+        K = self.K
+        key = (id(data), data.x.data_ptr(), data.y.data_ptr())
+        if self._bound_data != key or self._bound_ref is not data:
+            self._bound_ref = data     # keep alive: its id / memory must not be recycled while bound
+            o = K.STEP_STATE_DATA_OFFSET // 8
+            self._st_i64[o] = data.x.data_ptr()
+            self._st_i64[o + 1] = data.y.data_ptr()
+            on = K.STEP_STATE_DATAN_OFFSET // 4
+            self._st_i32[on] = data.n
+            self._st_i32[on + 1] = data.x.shape[1]
+            self._st_i32[on + 2] = data.y.shape[1]
+            self._bound_data = key
+            self._perm_obj = None
+        if perm is not None and perm is not self._perm_obj:
+            if self._perm_buf is None or self._perm_buf.numel() < data.n:
+                self._perm_buf = torch.empty(max(data.n, 1), dtype=torch.int32, device=self.device)
+            self._perm_buf[:data.n].copy_(perm.to(device=self.device, dtype=torch.int32))
+            self._st_i64[K.STEP_STATE_DATA_OFFSET // 8 + 2] = self._perm_buf.data_ptr()
+            self._perm_obj = perm
+        self._st_i32[K.STEP_STATE_DATAN_OFFSET // 4 + 3] = 1 if perm is not None else 0
+
+    # ------------------------------------------------------------------ steps
+    def _plan_for(self, bs: int, mode: str) -> "BatchPlan":
+        key = (bs, mode)
+        bp = self._plans.get(key)
+        if bp is None:
+            bp = BatchPlan(self, bs, mode)
+            self._plans[key] = bp
+        return bp
+
+    def train_step(self, data, perm, pos, bs):
+        self._sync_lr()
+        self._bind_data(data, perm)
+        if self._expected_pos != pos:
+            self._st_i32[1] = pos
+        bp = self._plan_for(bs, "train")
+        bp.run()
+        self._expected_pos = pos + bs
+        self.opt.iterations += 1
+
+    def eval_step(self, data, pos, bs):
+        self._bind_data(data, None)
+        self._st_i32[3] = pos
+        self._plan_for(bs, "eval").run()
+        self._expected_pos = None
+
+    def predict_step(self, data, pos, bs):
+        self._bind_data(data, None)
+        self._st_i32[3] = pos
+        bp = self._plan_for(bs, "predict")
+        bp.run()
+        out = bp.probs.clone()
+        return out
+
+    # ------------------------------------------------------------------ metrics
+    def _metrics(self):
+        o = self.K.STEP_STATE_METRICS_OFFSET // 8
+        v = self._st_f64[o:o + 3].tolist()
+        return v
+
+    def reset_metrics(self):
+        o = self.K.STEP_STATE_METRICS_OFFSET // 8
+        self._st_f64[o:o + 4].zero_()
+        self._metrics_prev = (0.0, 0.0, 0.0)
+
+    def read_metrics(self):
+        ls, cs, n = self._metrics()
+        self._metrics_prev = (ls, cs, n)
+        n1 = max(n, 1.0)
+        return ls / n1, cs / n1, int(n)
+
+    def last_batch_metrics(self):
+        ls, cs, n = self._metrics()
+        pl, pc, pn = self._metrics_prev
+        self._metrics_prev = (ls, cs, n)
+        dn = max(n - pn, 1.0)
+        return (ls - pl) / dn, (cs - pc) / dn
+
+    def synchronize(self):
+        torch.cuda.synchronize(self.device)
+
+
+class BatchPlan:
+    """Buffers + prepared kernel argument structs for one (batch size, mode); records the
+    launch sequence and replays it from a HIP graph."""
+
+    def __init__(self, ex: HipExecutor, bs: int, mode: str):
+        self.ex, self.bs, self.mode = ex, bs, mode
+        self.training = mode == "train"
+        K = ex.K
+        dev = ex.device
+        self.graph = None
+        self.graph_pre = None
+        self.graph_post = None
+        z = lambda *s, dt=BF16: torch.zeros(*s, dtype=dt, device=dev)
+        self.xb = z(bs, ex.in_H * ex.in_W * ex.in_Cs)
+        self.yb = z(bs, ex.plan.head.N, dt=torch.float32)
+        self.conv_out, self.conv_code, self.conv_dy = [], [], []
+        for g in ex.convs:
+            self.conv_out.append(z(bs, g.Hp, g.Wp, g.Cs_out))
+            self.conv_code.append(z(bs, g.Hp, g.Wp, g.Cs_out, dt=torch.uint8) if g.pool else None)
+            self.conv_dy.append(z(bs, g.Ho, g.Wo, g.Cs_out) if self.training else None)
+        self.dense_out, self.dense_part, self.dense_dh = [], [], []
+        self.dense_splits = []
+        for g in ex.denses:
+            self.dense_out.append(z(bs, g.Ns))
+            mt = cdiv(bs, 16)
+            splits = max(1, min(g.KS, 2048 // max(1, mt * g.NT)))
+            kps = cdiv(g.KS, splits)
+            splits = cdiv(g.KS, kps)
+            self.dense_splits.append((splits, kps))
+            self.dense_part.append(z(splits, bs, g.NT * 16, dt=torch.float32))
+            self.dense_dh.append(z(bs, g.Ns) if self.training else None)
+        hd = ex.plan.head
+        self.head_blocks = cdiv(bs, 16)
+        self.probs = z(bs, hd.N, dt=torch.float32) if mode == "predict" else None
+        if self.training:
+            self.head_wslab = z(self.head_blocks, hd.K, hd.N, dt=torch.float32)
+            self.head_bslab = z(self.head_blocks, hd.N, dt=torch.float32)
+        self._build_args()
+
+    # ---------------------------------------------------------------- helpers
+    def _src_buf(self, src: Src):
+        if src.kind == "input":
+            return self.xb
+        if src.kind == "conv":
+            return self.conv_out[src.idx]
+        return self.dense_out[src.idx]
+
+    def _bt_for(self, src: Src):
+        """BwdThrough args routing a gradient wrt ``src``'s output back into its layer."""
+        K, ex = self.ex.K, self.ex
+        bt = K.BwdThrough()
+        if src.kind == "input":
+            return None
+        if src.kind == "conv":
+            g = ex.convs[src.idx]
+            bt.prev_out = self.conv_out[g.i].data_ptr()
+            if g.pool:
+                bt.prev_code = self.conv_code[g.i].data_ptr()
+            bt.prev_relu, bt.prev_pool = int(g.relu), int(g.pool)
+            bt.pH, bt.pW, bt.pC, bt.pCs = g.Hp, g.Wp, g.Cout, g.Cs_out
+            bt.cH, bt.cW = g.Ho, g.Wo
+            rate, stream = g.rate, g.stream
+            bt.dy = self.conv_dy[g.i].data_ptr()
+        else:
+            g = ex.denses[src.idx]
+            bt.prev_out = self.dense_out[g.j].data_ptr()
+            bt.prev_relu, bt.prev_pool = int(g.relu), 0
+            bt.pH, bt.pW, bt.pC, bt.pCs = 1, 1, g.N, g.Ns
+            bt.cH, bt.cW = 1, 1
+            rate, stream = g.rate, g.stream
+            bt.dy = self.dense_dh[g.j].data_ptr()
+        if rate > 0:
+            bt.drop_thr = keep_threshold(rate)
+            bt.drop_scale = 1.0 / (1.0 - rate)
+        bt.seed, bt.stream_id = ex.seed, stream
+        return bt
+
+    def _build_args(self):
+        ex, K, bs = self.ex, self.ex.K, self.bs
+        st_ptr = ex.state.data_ptr()
+        store = ex.store
+        training = self.training
+        self.launches = []          # list of (name, callable(stream))
+
+        # step begin
+        sb = K.StepBeginArgs()
+        sb.st = st_ptr
+        sb.training = int(training)
+        sb.bs = bs
+        o = ex.opt
+        sb.opt_kind = OPT_KIND[o.kind]
+        sb.beta1 = getattr(o, "beta_1", 0.9)
+        sb.beta2 = getattr(o, "beta_2", 0.999)
+        sb.decay = getattr(o, "initial_decay", 0.0)
+        sb.schedule_decay = getattr(o, "schedule_decay", 0.004)
+        self.launches.append(("step_begin", lambda s, a=sb: K.step_begin(a, s)))
+
+        ga = K.GatherArgs()
+        ga.st = st_ptr
+        ga.bs = bs
+        ga.R = self.xb.shape[1]
+        ga.xb = self.xb.data_ptr()
+        ga.yb = self.yb.data_ptr()
+        self.launches.append(("gather", lambda s, a=ga: K.gather(a, s)))
+
+        # ---------------- forward convs
+        x_buf, H, W, Cs = self.xb, ex.in_H, ex.in_W, ex.in_Cs
+        for g, cs in zip(ex.convs, ex.plan.convs):
+            a = K.ConvMMArgs()
+            a.x = x_buf.data_ptr()
+            a.B, a.H, a.W, a.Cs_in = bs, g.H, g.W, g.Cs_in
+            a.Ho, a.Wo = g.Ho, g.Wo
+            a.KH, a.KW, a.stride, a.pad_t, a.pad_l, a.in_dil = g.KH, g.KW, g.stride, g.pad_t, g.pad_l, 1
+            a.KS = g.KS
+            a.wpk = ex.arena.data_ptr() + 2 * g.pack_fwd
+            a.NT = g.NT
+            a.bias = store.view(cs.conv, "bias").data_ptr() if cs.conv.use_bias else 0
+            a.N = g.Cout
+            a.mode = 0
+            a.relu, a.pool = int(g.relu), int(g.pool)
+            a.out = self.conv_out[g.i].data_ptr()
+            a.Cs_out, a.Hp, a.Wp = g.Cs_out, g.Hp, g.Wp
+            if g.pool:
+                a.code = self.conv_code[g.i].data_ptr()
+            if training and g.rate > 0:
+                a.drop_thr = keep_threshold(g.rate)
+                a.drop_scale = 1.0 / (1.0 - g.rate)
+            a.seed, a.stream_id, a.st = ex.seed, g.stream, st_ptr
+            ntc, gx = self._conv_launch_cfg(a, g.NT, g.pool)
+            self.launches.append(("conv_fwd%d" % g.i, lambda s, a=a, n=ntc, gx=gx: K.conv_mm(a, n, gx, s)))
+            x_buf = self.conv_out[g.i]
+
+        # ---------------- forward denses
+        for g, ds in zip(ex.denses, ex.plan.denses):
+            splits, kps = self.dense_splits[g.j]
+            a = K.DenseFwdArgs()
+            a.x = self._src_buf(g.src).data_ptr()
+            a.M, a.Ks = bs, g.src.width
+            a.wpk = ex.arena.data_ptr() + 2 * g.pack_fwd
+            a.NT, a.KS = g.NT, g.KS
+            a.splits, a.ks_per_split = splits, kps
+            a.part = self.dense_part[g.j].data_ptr()
+            self.launches.append(("dense_fwd%d" % g.j, lambda s, a=a: K.dense_fwd(a, s)))
+            e = K.DenseEpiArgs()
+            e.part = a.part
+            e.splits, e.M, e.N, e.Ns, e.ldp = splits, bs, g.N, g.Ns, g.NT * 16
+            e.bias = store.view(ds.dense, "bias").data_ptr() if ds.dense.use_bias else 0
+            e.relu = int(g.relu)
+            e.out = self.dense_out[g.j].data_ptr()
+            if training and g.rate > 0:
+                e.drop_thr = keep_threshold(g.rate)
+                e.drop_scale = 1.0 / (1.0 - g.rate)
+            e.seed, e.stream_id, e.st = ex.seed, g.stream, st_ptr
+            self.launches.append(("dense_epi%d" % g.j, lambda s, e=e: K.dense_epi(e, s)))
+
+        # ---------------- head
+        hd = ex.plan.head
+        h = K.HeadArgs()
+        src = ex.head_src
+        h.h = self._src_buf(src).data_ptr()
+        h.M, h.K, h.Ks, h.N = bs, hd.K, src.width, hd.N
+        h.flat_C, h.flat_Cs = src.C, src.Cs
+        h.w = store.view(hd.dense, "kernel").data_ptr()
+        h.bias = store.view(hd.dense, "bias").data_ptr() if hd.dense.use_bias else 0
+        h.y = self.yb.data_ptr() if self.mode != "predict" else 0
+        h.act = ex.head_act
+        h.training = int(training)
+        h.inv_bs = 1.0 / bs
+        h.st = st_ptr
+        if self.probs is not None:
+            h.probs = self.probs.data_ptr()
+        if training:
+            h.wslab = self.head_wslab.data_ptr()
+            h.bslab = self.head_bslab.data_ptr()
+            bt = self._bt_for(src)
+            if bt is not None:
+                h.bt = bt
+        self.launches.append(("head", lambda s, a=h: K.head(a, s)))
+        if not training:
+            return
+
+        # ---------------- backward
+        self.red_groups = []       # (lo, hi, [desc tuples]) in backward order
+        hw = store.spec(hd.dense, "kernel")
+        descs = [(self.head_wslab.data_ptr(), hd.K * hd.N, self.head_blocks, hd.N, hw.offset, hw.numel,
+                  RED_BIAS, 0, 0, 0, 0, 0)]
+        lo, hi = hw.offset, hw.offset + hw.numel
+        if hd.dense.use_bias:
+            hb = store.spec(hd.dense, "bias")
+            descs.append((self.head_bslab.data_ptr(), hd.N, self.head_blocks, hd.N, hb.offset, hb.numel,
+                          RED_BIAS, 0, 0, 0, 0, 0))
+            hi = max(hi, hb.offset + hb.numel)
+        self.red_groups.append((lo, hi, descs))
+        self.wgrad_slabs = []
+
+        for g, ds in reversed(list(zip(ex.denses, ex.plan.denses))):
+            xin = self._src_buf(g.src)
+            wa, cfg, slab, bslab = self._wgrad_args(xin, 1, 1, g.src.width, 1, 1, 1, 1, 1, 0, 0,
+                                                    self.dense_dh[g.j], g.Ns, g.N, bs, ds.dense.use_bias)
+            self.launches.append(("wgrad_dense%d" % g.j, lambda s, a=wa, c=cfg: K.wgrad(a, c[0], c[1], c[2], s)))
+            sp = store.spec(ds.dense, "kernel")
+            S, ld = cfg[2], g.NT * 16
+            descs = [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel, RED_FLATW,
+                      0, 0, g.src.C, g.N, g.src.Cs)]
+            lo, hi = sp.offset, sp.offset + sp.numel
+            if ds.dense.use_bias:
+                bp_ = store.spec(ds.dense, "bias")
+                descs.append((bslab.data_ptr(), ld, S, ld, bp_.offset, bp_.numel, RED_BIAS, 0, 0, 0, 0, 0))
+                hi = max(hi, bp_.offset + bp_.numel)
+            self.red_groups.append((lo, hi, descs))
+            if g.KSb:
+                a = K.ConvMMArgs()
+                a.x = self.dense_dh[g.j].data_ptr()
+                a.B, a.H, a.W, a.Cs_in = bs, 1, 1, g.Ns
+                a.Ho, a.Wo = 1, 1
+                a.KS = g.KSb
+                a.wpk = ex.arena.data_ptr() + 2 * g.pack_bwd
+                a.NT = g.NTb
+                a.mode, a.flat_out = 1, 1
+                a.st = st_ptr
+                a.bt = self._bt_for(g.src)
+                ntc, gx = self._conv_launch_cfg(a, g.NTb, False)
+                pre = self._zero_if_needed(g.src)
+                self.launches.append(("dense_dx%d" % g.j,
+                                      lambda s, a=a, n=ntc, gx=gx, pre=pre: (pre(), K.conv_mm(a, n, gx, s))))
+
+        for g, cs in reversed(list(zip(ex.convs, ex.plan.convs))):
+            xin = self.xb if g.i == 0 else self.conv_out[g.i - 1]
+            wa, cfg, slab, bslab = self._wgrad_args(xin, g.H, g.W, g.Cs_in, g.Ho, g.Wo, g.KH, g.KW, g.stride,
+                                                    g.pad_t, g.pad_l, self.conv_dy[g.i], g.Cs_out, g.Cout,
+                                                    bs, cs.conv.use_bias)
+            self.launches.append(("wgrad_conv%d" % g.i, lambda s, a=wa, c=cfg: K.wgrad(a, c[0], c[1], c[2], s)))
+            sp = store.spec(cs.conv, "kernel")
+            S, ld = cfg[2], g.NT * 16
+            descs = [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel, RED_CONVW,
+                      g.KH, g.KW, g.Cin, g.Cout, g.Cs_in)]
+            lo, hi = sp.offset, sp.offset + sp.numel
+            if cs.conv.use_bias:
+                bp_ = store.spec(cs.conv, "bias")
+                descs.append((bslab.data_ptr(), ld, S, ld, bp_.offset, bp_.numel, RED_BIAS, 0, 0, 0, 0, 0))
+                hi = max(hi, bp_.offset + bp_.numel)
+            self.red_groups.append((lo, hi, descs))
+            if g.i > 0:
+                prev = ex.convs[g.i - 1]
+                a = K.ConvMMArgs()
+                a.x = self.conv_dy[g.i].data_ptr()
+                a.B, a.H, a.W, a.Cs_in = bs, g.Ho, g.Wo, g.Cs_out
+                a.Ho, a.Wo = g.H, g.W            # == prev stage output grid
+                a.KH, a.KW, a.stride = g.KH, g.KW, 1
+                a.pad_t, a.pad_l, a.in_dil = g.KH - 1 - g.pad_t, g.KW - 1 - g.pad_l, g.stride
+                a.KS = g.KSd
+                a.wpk = ex.arena.data_ptr() + 2 * g.pack_dgrad
+                a.NT = g.NTd
+                a.mode, a.flat_out = 1, 0
+                a.st = st_ptr
+                a.bt = self._bt_for(Src("conv", prev.i, prev.Cout, prev.Cs_out, prev.Hp, prev.Wp))
+                ntc, gx = self._conv_launch_cfg(a, g.NTd, False)
+                pre = self._zero_if_needed(Src("conv", prev.i, prev.Cout, prev.Cs_out, prev.Hp, prev.Wp))
+                self.launches.append(("dgrad_conv%d" % g.i,
+                                      lambda s, a=a, n=ntc, gx=gx, pre=pre: (pre(), K.conv_mm(a, n, gx, s))))
+        self._build_reduce()
+
+    def _zero_if_needed(self, src: Src):
+        """Full-res dY of a pooled conv whose grid is odd is not fully covered by the
+        pool-routing scatter: clear it first (captured as a memset node)."""
+        if src.kind == "conv":
+            g = self.ex.convs[src.idx]
+            if g.pool and (g.Ho % 2 or g.Wo % 2):
+                t = self.conv_dy[g.i]
+                return lambda t=t: t.zero_()
+        return lambda: None
+
+    def _conv_launch_cfg(self, a, NT, pool):
+        KS = a.KS
+        ntc = 8
+        while ntc > 1 and (ntc > NT or KS * ntc > 64):
+            ntc //= 2
+        if KS * ntc > 150:
+            raise NotImplementedError("conv K too large for the LDS weight stage (KS=%d)" % KS)
+        gy = cdiv(NT, ntc)
+        rows = a.B * (a.Hp * a.Wp if pool else a.Ho * a.Wo)
+        ntiles = cdiv(rows, 4) if pool else cdiv(rows, 16)
+        gx = max(1, min(cdiv(ntiles, 4), max(1, 512 // gy)))
+        return ntc, gx
+
+    def _wgrad_args(self, xin, H, W, Cs_in, Ho, Wo, KH, KW, stride, pad_t, pad_l, dy, Cs_dy, N, bs, bias):
+        K, dev = self.ex.K, self.ex.device
+        a = K.WgradArgs()
+        a.x = xin.data_ptr()
+        a.B, a.H, a.W, a.Cs_in = bs, H, W, Cs_in
+        a.Ho, a.Wo, a.KH, a.KW, a.stride, a.pad_t, a.pad_l = Ho, Wo, KH, KW, stride, pad_t, pad_l
+        if not (Cs_in == 4 or Cs_in % 8 == 0):
+            raise NotImplementedError("wgrad needs Cs_in == 4 or a multiple of 8 (got %d)" % Cs_in)
+        a.Ktiles = cdiv(KH * KW * Cs_in, 16)
+        a.dy = dy.data_ptr()
+        a.Cs_dy = Cs_dy
+        NT = cdiv(N, 16)
+        a.NT = NT
+        P = bs * Ho * Wo
+        a.P = P
+        ntt = _pow2_le(NT, 8)
+        ktw = 4 if ntt <= 4 else 2
+        while ktw > 1 and 4 * (ktw // 2) >= a.Ktiles:
+            ktw //= 2
+        if ntt == 8 and ktw == 4:
+            ktw = 2
+        a.KT = 4 * ktw
+        gy = cdiv(a.Ktiles, a.KT)
+        gz = cdiv(NT, ntt)
+        per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
+        s_budget = max(1, (4 << 20) // per_split_bytes)
+        S = max(1, min(512 // max(1, gy * gz), s_budget, cdiv(P, 32)))
+        pps = cdiv(cdiv(P, S), 32) * 32
+        S = cdiv(P, pps)
+        a.px_per_split = pps
+        slab = torch.zeros(S, a.Ktiles * 16, NT * 16, dtype=torch.float32, device=dev)
+        bslab = torch.zeros(S, NT * 16, dtype=torch.float32, device=dev) if bias else None
+        a.slab = slab.data_ptr()
+        a.bslab = bslab.data_ptr() if bslab is not None else 0
+        self.wgrad_slabs.append((slab, bslab))
+        return a, (ktw, ntt, S), slab, bslab
+
+    def _build_reduce(self):
+        """Group per-layer slab reductions into data-parallel buckets (backward order)."""
+        ex, K = self.ex, self.ex.K
+        groups = [(lo, hi) for lo, hi, _ in self.red_groups]
+        reducer = ex.reducer
+        if reducer is not None:
+            bucket_groups = reducer.configure(groups)
+        else:
+            bucket_groups = [list(range(len(groups)))]
+        self.bucket_tables = []
+        for bg in bucket_groups:
+            tab = K.RedTable()
+            lo = min(self.red_groups[i][0] for i in bg)
+            hi = max(self.red_groups[i][1] for i in bg)
+            for i in bg:
+                for d in self.red_groups[i][2]:
+                    tab.add(*d)
+            self.bucket_tables.append((lo, hi, tab))
+
+    # ---------------------------------------------------------------- execution
+    def _run_seq(self, names_filter=None):
+        s = torch.cuda.current_stream().cuda_stream
+        for name, fn in self.launches:
+            fn(s)
+
+    def _launch_reduce(self, i):
+        lo, hi, tab = self.bucket_tables[i]
+        self.ex.K.slab_reduce(self.ex.store.grad.data_ptr(), lo, hi, tab,
+                              torch.cuda.current_stream().cuda_stream)
+
+    def _launch_optim(self):
+        ex = self.ex
+        ex.K.optim(ex._optim_args(False), ex.pack_table, torch.cuda.current_stream().cuda_stream)
+
+    def _body(self, with_optim: bool):
+        self._run_seq()
+        if self.training:
+            for i in range(len(self.bucket_tables)):
+                self._launch_reduce(i)
+            if with_optim:
+                self._launch_optim()
+
+    def run(self):
+        ex = self.ex
+        dp = self.training and ex.reducer is not None and ex.reducer.size > 1
+        if dp:
+            ex.grad_scale = 1.0 / ex.reducer.size
+        if not ex.use_graphs:
+            self._body(with_optim=not dp)
+            if dp:
+                self._dp_tail()
+            return
+        if dp:
+            if self.graph_pre is None:
+                self.graph_pre = self._capture(lambda: self._body(with_optim=False))
+                self.graph_post = self._capture(self._launch_optim)
+            self.graph_pre.replay()
+            for i in range(len(self.bucket_tables)):
+                ex.reducer.start(i, ex.store.grad)
+            ex.reducer.finish()
+            self.graph_post.replay()
+            return
+        if self.graph is None:
+            self.graph = self._capture(lambda: self._body(with_optim=True))
+        self.graph.replay()
+
+    def _dp_tail(self):
+        ex = self.ex
+        for i in range(len(self.bucket_tables)):
+            ex.reducer.start(i, ex.store.grad)
+        ex.reducer.finish()
+        self._launch_optim()
+
+    def _capture(self, fn):
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=self.ex.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.graph(g, stream=s):
+            fn()
+        torch.cuda.current_stream().wait_stream(s)
+        return g

@@ -1,0 +1,284 @@
+"""Horovod-shaped data-parallel runtime over torch.distributed (RCCL on ROCm).
+
+API parity with the calls the reference makes:
+  ``hvd.init()``                    train_rpv.py:37, DistTrain_mnist.ipynb:148
+  ``hvd.rank()/local_rank()/size()``train_rpv.py:38-39,56,65
+  ``hvd.DistributedOptimizer(opt)`` rpv.py:65, DistTrain_mnist.ipynb:310
+  ``hvd.callbacks.*``               rpv.py:83-93, DistTrain_mnist.ipynb:494
+
+MI355X design (not a translation of Horovod's coordinator/fusion-buffer core):
+  * one process per GPU, ``torch.distributed`` backend ``nccl`` (= RCCL over xGMI);
+  * the flat gradient buffer is split into size-capped buckets in *backward order*
+    (head/dense grads first), so the first bucket's all-reduce is in flight on
+    RCCL's stream while the conv backward kernels still run;
+  * averaging (1/size) is folded into the fused optimizer kernel, no extra pass;
+  * initial state broadcast happens BEFORE step 0 (the reference's Horovod
+    broadcasts after batch 0);
+  * epoch metrics are averaged with ONE packed all-reduce.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+
+from . import state as S
+
+
+# ------------------------------------------------------------------------------ bootstrap
+def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
+         bucket_bytes: Optional[int] = None) -> S.DPState:
+    """Initialise the data-parallel group from torchrun-style env vars
+    (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  Without them this
+    is a size-1 group (no process group is created)."""
+    st = S.current()
+    if st is not None:
+        if shard_data is not None:
+            st.shard_data = shard_data
+        return st
+    env_shard = os.environ.get("INTML_DP_SHARD")
+    if shard_data is None:
+        shard_data = True if env_shard is None else env_shard not in ("0", "false", "False")
+    bucket_bytes = bucket_bytes or int(os.environ.get("INTML_BUCKET_BYTES", 4 << 20))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    local_size = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    owns = False
+    if tdist.is_available() and tdist.is_initialized():
+        world, rank = tdist.get_world_size(), tdist.get_rank()
+        be = tdist.get_backend()
+    elif world > 1:
+        use_gpu = torch.cuda.is_available() and os.environ.get("INTML_DEVICE", "cuda").startswith("cuda")
+        be = backend or ("nccl" if use_gpu else "gloo")
+        if use_gpu:
+            torch.cuda.set_device(local_rank % torch.cuda.device_count())
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        tdist.init_process_group(backend=be, rank=rank, world_size=world)
+        owns = True
+    else:
+        be = backend or "none"
+    st = S.DPState(rank=rank, size=world, local_rank=local_rank, local_size=local_size,
+                   backend=be, shard_data=shard_data, bucket_bytes=bucket_bytes, owns_pg=owns)
+    S.set_state(st)
+    return st
+
+
+def shutdown() -> None:
+    st = S.current()
+    if st is not None and st.owns_pg and tdist.is_initialized():
+        tdist.destroy_process_group()
+    S.set_state(None)
+
+
+def _st() -> S.DPState:
+    st = S.current()
+    if st is None:
+        raise ValueError("Horovod-style API used before init()")
+    return st
+
+
+def rank() -> int: return _st().rank
+def size() -> int: return _st().size
+def local_rank() -> int: return _st().local_rank
+def local_size() -> int: return _st().local_size
+def is_initialized() -> bool: return S.current() is not None
+
+
+def _active() -> bool:
+    st = S.current()
+    return st is not None and st.size > 1 and tdist.is_initialized()
+
+
+# ------------------------------------------------------------------------------ collectives
+def allreduce(value, average: bool = True, name: Optional[str] = None):
+    """All-reduce a tensor / numpy array / python scalar (returns the same kind)."""
+    if not _active():
+        return value
+    is_t = isinstance(value, torch.Tensor)
+    dev = _comm_device()
+    t = value if is_t else torch.as_tensor(np.asarray(value, dtype=np.float64))
+    src = t
+    t = t.to(dev, dtype=torch.float64 if not is_t else t.dtype).clone()
+    tdist.all_reduce(t)
+    if average:
+        t = t / size()
+    if is_t:
+        return t.to(src.device)
+    out = t.cpu().numpy()
+    return out.item() if np.ndim(value) == 0 else out
+
+
+def allgather(value) -> list:
+    if not _active():
+        return [value]
+    out = [None] * size()
+    tdist.all_gather_object(out, value)
+    return out
+
+
+def broadcast(tensor: torch.Tensor, root_rank: int = 0) -> torch.Tensor:
+    if _active():
+        dev = _comm_device()
+        if tensor.device == dev:
+            tdist.broadcast(tensor, src=root_rank)
+        else:
+            tmp = tensor.to(dev)
+            tdist.broadcast(tmp, src=root_rank)
+            tensor.copy_(tmp.to(tensor.device))
+    return tensor
+
+
+def broadcast_object(obj, root_rank: int = 0):
+    if not _active():
+        return obj
+    box = [obj]
+    tdist.broadcast_object_list(box, src=root_rank)
+    return box[0]
+
+
+def barrier() -> None:
+    if _active():
+        if _st().backend == "nccl":
+            tdist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            tdist.barrier()
+
+
+def _comm_device() -> torch.device:
+    if _st().backend == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def broadcast_model_state(model, root_rank: int = 0) -> None:
+    """R2: one broadcast of the flat master buffer + each optimizer slot + step."""
+    if not _active():
+        return
+    ex = model._executor
+    broadcast(model.store.master, root_rank)
+    if ex is not None:
+        for slot in ex.optimizer_state():
+            broadcast(slot, root_rank)
+        base = getattr(model.optimizer, "_base_optimizer", model.optimizer)
+        it = broadcast_object(int(base.iterations), root_rank)
+        ex.set_optimizer_state(it, ex.optimizer_state())
+        ex.params_changed()
+
+
+# ------------------------------------------------------------------------------ optimizer wrap
+class _DistributedOptimizer:
+    """Wraps a Keras optimizer; the executor all-reduces gradients in buckets."""
+
+    def __init__(self, optimizer, compression=None, bucket_bytes=None):
+        from ..optim import get
+        object.__setattr__(self, "_base_optimizer", get(optimizer))
+        object.__setattr__(self, "distributed", True)
+        object.__setattr__(self, "compression", compression)
+        object.__setattr__(self, "bucket_bytes", bucket_bytes)
+
+    def __getattr__(self, item):
+        return getattr(self._base_optimizer, item)
+
+    def __setattr__(self, key, value):
+        setattr(self._base_optimizer, key, value)
+
+    def get_config(self):
+        return self._base_optimizer.get_config()
+
+    @property
+    def __class__(self):   # serialises / isinstance-checks as the wrapped class
+        return type(self._base_optimizer)
+
+
+def DistributedOptimizer(optimizer, name=None, device_dense="", device_sparse="", compression=None,
+                         sparse_as_dense=False, bucket_bytes=None):
+    if not is_initialized():
+        init()
+    return _DistributedOptimizer(optimizer, compression=compression, bucket_bytes=bucket_bytes)
+
+
+class Compression:
+    """``hvd.Compression.none`` / ``.fp16``; on MI355X the 16-bit wire format is bf16."""
+    none = None
+    fp16 = "bf16"
+    bf16 = "bf16"
+
+
+# ------------------------------------------------------------------------------ grad reducer
+class GradReducer:
+    """Bucketed gradient all-reduce over the flat grad buffer.
+
+    ``groups`` are (lo, hi) flat ranges in the order their gradients become final
+    during backward.  Consecutive groups are merged until ``bucket_bytes``; each
+    bucket is ONE RCCL all-reduce (async, on RCCL's stream) over a contiguous view.
+    """
+
+    def __init__(self, store, compression=None, bucket_bytes: int = 4 << 20):
+        self.store = store
+        self.compression = compression
+        self.bucket_bytes = bucket_bytes
+        self.size = size()
+        self.buckets: List[Tuple[int, int]] = [(0, store.numel)]
+        self.bucket_groups: List[List[int]] = [[0]]
+        self._pending = []
+
+    def configure(self, groups: Sequence[Tuple[int, int]]) -> List[List[int]]:
+        """Merge backward-ordered groups into buckets; returns group indices per bucket."""
+        buckets, cur, cur_bytes = [], [], 0
+        for gi, (lo, hi) in enumerate(groups):
+            cur.append(gi)
+            cur_bytes += (hi - lo) * 4
+            if cur_bytes >= self.bucket_bytes:
+                buckets.append(cur)
+                cur, cur_bytes = [], 0
+        if cur:
+            buckets.append(cur)
+        self.bucket_groups = buckets
+        self.buckets = []
+        for b in buckets:
+            lo = min(groups[g][0] for g in b)
+            hi = max(groups[g][1] for g in b)
+            self.buckets.append((lo, hi))
+        return buckets
+
+    def start(self, bucket: int, grad: torch.Tensor):
+        """Launch the all-reduce of one bucket asynchronously (stream-ordered after the
+        producing kernels on the current stream)."""
+        if not _active():
+            return
+        lo, hi = self.buckets[bucket]
+        view = grad[lo:hi]
+        if self.compression == "bf16":
+            buf = view.to(torch.bfloat16)
+            work = tdist.all_reduce(buf, async_op=True)
+            self._pending.append((work, buf, view))
+        else:
+            work = tdist.all_reduce(view, async_op=True)
+            self._pending.append((work, None, None))
+
+    def finish(self) -> None:
+        """Make the current stream wait for every in-flight bucket."""
+        for work, buf, view in self._pending:
+            work.wait()
+            if buf is not None:
+                view.copy_(buf.to(torch.float32))
+        self._pending.clear()
+
+    def reduce_all(self, grad: torch.Tensor, average: bool = True) -> None:
+        for i in range(len(self.buckets)):
+            self.start(i, grad)
+        self.finish()
+        if average and _active():
+            grad[: self.store.numel].div_(self.size)
+
+
+def make_reducer(executor, optimizer) -> GradReducer:
+    if not is_initialized():
+        init()
+    st = _st()
+    bb = getattr(optimizer, "bucket_bytes", None) or st.bucket_bytes
+    return GradReducer(executor.store, getattr(optimizer, "compression", None), bb)

@@ -1,0 +1,29 @@
+"""Process-level data-parallel state (one process per GPU)."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+
+@dataclass
+class DPState:
+    rank: int
+    size: int
+    local_rank: int
+    local_size: int
+    backend: str
+    shard_data: bool = True
+    bucket_bytes: int = 4 << 20
+    owns_pg: bool = False
+
+
+_STATE: Optional[DPState] = None
+
+
+def current() -> Optional[DPState]:
+    return _STATE
+
+
+def set_state(s: Optional[DPState]) -> None:
+    global _STATE
+    _STATE = s

@@ -1,0 +1,118 @@
+"""``Model.fit`` driver (Keras 2.2 ``fit_loop`` semantics, GPU-friendly).
+
+Differences from a naive port: the dataset is uploaded to the device once, the
+per-epoch shuffle is a device permutation, the per-batch step is one HIP-graph
+replay on GPU, and epoch metrics accumulate on the device (one D2H per epoch).
+Per-batch host syncs happen only when a callback actually consumes batch logs.
+
+Reference behaviour reproduced: ``validation_split`` takes the *last* fraction
+before shuffling (``DistHPO_mnist.ipynb:188,293``: 60000 -> 49800/10200), the final
+partial batch is processed, ``Train on N samples, validate on M samples`` banner,
+History keys ``loss, acc, val_loss, val_acc`` (+ ``lr`` from ReduceLROnPlateau).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import callbacks as cbks
+
+
+def _split_validation(x, y, validation_split, validation_data):
+    if validation_data is not None:
+        if len(validation_data) == 3:
+            vx, vy, vw = validation_data
+            if vw is not None:
+                raise NotImplementedError("validation sample weights")
+        else:
+            vx, vy = validation_data
+        return x, y, vx, vy
+    if validation_split and 0.0 < validation_split < 1.0:
+        n = len(x)
+        split_at = int(n * (1.0 - validation_split))
+        return x[:split_at], y[:split_at], x[split_at:], y[split_at:]
+    return x, y, None, None
+
+
+def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_split, validation_data,
+             shuffle, initial_epoch):
+    from ..parallel import state as dp_state
+    ex = model._executor
+    x, y, vx, vy = _split_validation(x, y, validation_split, validation_data)
+
+    # data-parallel sharding (default) or the reference's replicated semantics
+    dp = dp_state.current()
+    if dp is not None and dp.size > 1 and dp.shard_data and getattr(model.optimizer, "distributed", False):
+        n = len(x)
+        per = n // dp.size
+        x = x[dp.rank * per:(dp.rank + 1) * per]
+        y = y[dp.rank * per:(dp.rank + 1) * per]
+
+    train = ex.upload(x, y)
+    val = ex.upload(vx, vy) if vx is not None else None
+    do_val = val is not None
+
+    model.history = cbks.History()
+    progbar = cbks.ProgbarLogger() if verbose else None
+    cb_list = ([progbar] if progbar else []) + list(callbacks or []) + [model.history]
+    cb = cbks.CallbackList(cb_list)
+    out_labels = model.metrics_names
+    metrics = list(out_labels) + (["val_" + n for n in out_labels] if do_val else [])
+    cb.set_model(model)
+    cb.set_params({"batch_size": batch_size, "epochs": epochs, "steps": None,
+                   "samples": train.n, "verbose": verbose, "do_validation": do_val,
+                   "metrics": metrics})
+    for c in cb:
+        c.validation_data = (vx, vy) if do_val else None
+    model.stop_training = False
+    need_batch_logs = cb.batch_logs_needed
+    need_batch_begin = cb.batch_begin_needed
+
+    if do_val and verbose:
+        print("Train on %d samples, validate on %d samples" % (train.n, val.n))
+    elif verbose:
+        print("Train on %d samples" % train.n)
+
+    gen = torch.Generator(device="cpu")
+    gen.manual_seed((model._seed + 7919 * (dp.rank if dp is not None else 0)) & 0x7FFFFFFF)
+    cb.on_train_begin()
+    for epoch in range(initial_epoch, epochs):
+        cb.on_epoch_begin(epoch, {})
+        if shuffle:
+            perm = torch.randperm(train.n, generator=gen).to(ex.device)
+        else:
+            perm = torch.arange(train.n, device=ex.device)
+        ex.reset_metrics()
+        nb = (train.n + batch_size - 1) // batch_size
+        for b in range(nb):
+            pos = b * batch_size
+            bs = min(batch_size, train.n - pos)
+            if need_batch_begin:
+                cb.on_batch_begin(b, {"batch": b, "size": bs})
+            ex.train_step(train, perm, pos, bs)
+            if need_batch_logs:
+                l, a = ex.last_batch_metrics()
+                logs = {"batch": b, "size": bs, "loss": l}
+                if model.metrics:
+                    logs["acc"] = a
+                cb.on_batch_end(b, logs)
+            if progbar is not None and verbose == 1:
+                if need_batch_logs or b == nb - 1 or b % 50 == 0:
+                    progbar.progress(pos + bs, [])
+            if model.stop_training:
+                break
+        loss, acc, _ = ex.read_metrics()
+        epoch_logs = {"loss": loss}
+        if model.metrics:
+            epoch_logs["acc"] = acc
+        if do_val:
+            model._run_eval(val, batch_size)
+            vloss, vacc, _ = ex.read_metrics()
+            epoch_logs["val_loss"] = vloss
+            if model.metrics:
+                epoch_logs["val_acc"] = vacc
+        cb.on_epoch_end(epoch, epoch_logs)
+        if model.stop_training:
+            break
+    cb.on_train_end()
+    return model.history
