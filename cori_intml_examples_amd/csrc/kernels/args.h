@@ -44,6 +44,12 @@ struct ConvMMArgs {
   const StepState* st = nullptr;
   // backward-through epilogue (mode 1)
   BwdThrough bt;
+  // halo-staged spatial kernel: R output rows per workgroup block; input given as a
+  // pooled gradient dP [B, in_pH, in_pW, Cs_in] + argmax codes (unpool on load)
+  int R = 1;
+  const uint8_t* in_code = nullptr;
+  int in_pH = 0, in_pW = 0;
+  int dbg = 0;   // ablation (timing only, wrong results): 1 skip staging, 2 skip MFMA, 4 skip stores
 };
 
 // Weight gradient: dW[k][n] = sum_pixels im2col(x)[p][k] * dY[p][n]  (split over pixels)
@@ -60,6 +66,12 @@ struct WgradArgs {
   int KT = 0;                    // k tiles per workgroup (grid.y groups)
   float* slab = nullptr;         // [S][Ktiles*16][NT*16]
   float* bslab = nullptr;        // [S][NT*16] or null
+  // halo-staged spatial variant: R output rows per block, blocks_per_split blocks per WG;
+  // dY given as pooled gradient dP [B, dHp, dWp, Cs_dy] + codes when dy_code != null
+  int R = 1, blocks_per_split = 1;
+  const uint8_t* dy_code = nullptr;
+  int dHp = 0, dWp = 0;
+  int dbg = 0;   // ablation (timing only): 1 skip staging, 2 skip MFMA, 4 skip slab stores
 };
 
 // Dense forward, split-K partial products: part[s][m][n]
@@ -70,6 +82,11 @@ struct DenseFwdArgs {
   int NT = 0, KS = 0;            // pack geometry
   int splits = 1, ks_per_split = 0;
   float* part = nullptr;         // [splits][M][NT*16]
+  // mode 1 (dense backward dX = dH W^T, splits == 1): route each output element (row m,
+  // flattened column n over the previous stage's padded output) through bwd_through_store
+  int mode = 0;
+  const StepState* st = nullptr;
+  BwdThrough bt;
 };
 
 // Split-K reduction + bias + activation + dropout -> bf16 [M][Ns]
@@ -149,12 +166,15 @@ struct RedDesc {
   int ld;              // row stride (n) of the slab
   int dst_off, numel, type;
   int KH, KW, Cin, Cout, Cs;   // conv: k = tap*Cs + ci ; flat: C=Cin (channels), Cs
+  int tpe;             // threads per element (1..64, power of 2): lanes split the S partials
+  int blk0;            // first workgroup of this descriptor in the launch
   int pad_;
 };
 
 #define MAX_RED 16
 struct RedTable {
   int n;
-  int pad_[3];
+  int nblocks;         // total workgroups of the launch
+  int pad_[2];
   RedDesc d[MAX_RED];
 };

@@ -9,8 +9,11 @@
 
 namespace py = pybind11;
 
-void launch_conv_mm(const ConvMMArgs& a, int ntc, int gx, hipStream_t s);
-size_t conv_mm_lds_bytes(const ConvMMArgs& a, int ntc, bool cs4);
+void launch_conv_halo(const ConvMMArgs& a, int ntc, hipStream_t s);
+size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc);
+void launch_wgrad_halo(const WgradArgs& a, int MT, int NTT, int splits, hipStream_t s);
+size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT);
+int head_rows_per_block();
 void launch_wgrad(const WgradArgs& a, int ktw, int ntt, int splits, hipStream_t s);
 size_t wgrad_lds_bytes(int KT, int NTT);
 void launch_dense_fwd(const DenseFwdArgs& a, hipStream_t s);
@@ -53,7 +56,8 @@ PYBIND11_MODULE(_kernels, m) {
       RW(ConvMMArgs, flat_out) RW(ConvMMArgs, relu) RW(ConvMMArgs, pool) PTR(ConvMMArgs, out)
       RW(ConvMMArgs, Cs_out) RW(ConvMMArgs, Hp) RW(ConvMMArgs, Wp) PTR(ConvMMArgs, code)
       RW(ConvMMArgs, drop_thr) RW(ConvMMArgs, drop_scale) RW(ConvMMArgs, seed) RW(ConvMMArgs, stream_id)
-      PTR(ConvMMArgs, st) RW(ConvMMArgs, bt);
+      PTR(ConvMMArgs, st) RW(ConvMMArgs, bt) RW(ConvMMArgs, R) PTR(ConvMMArgs, in_code)
+      RW(ConvMMArgs, in_pH) RW(ConvMMArgs, in_pW) RW(ConvMMArgs, dbg);
 
   py::class_<WgradArgs>(m, "WgradArgs")
       .def(py::init<>())
@@ -61,13 +65,15 @@ PYBIND11_MODULE(_kernels, m) {
       RW(WgradArgs, Ho) RW(WgradArgs, Wo) RW(WgradArgs, KH) RW(WgradArgs, KW) RW(WgradArgs, stride)
       RW(WgradArgs, pad_t) RW(WgradArgs, pad_l) RW(WgradArgs, Ktiles) PTR(WgradArgs, dy)
       RW(WgradArgs, Cs_dy) RW(WgradArgs, NT) RW(WgradArgs, P) RW(WgradArgs, px_per_split)
-      RW(WgradArgs, KT) PTR(WgradArgs, slab) PTR(WgradArgs, bslab);
+      RW(WgradArgs, KT) PTR(WgradArgs, slab) PTR(WgradArgs, bslab) RW(WgradArgs, R)
+      RW(WgradArgs, blocks_per_split) PTR(WgradArgs, dy_code) RW(WgradArgs, dHp) RW(WgradArgs, dWp)
+      RW(WgradArgs, dbg);
 
   py::class_<DenseFwdArgs>(m, "DenseFwdArgs")
       .def(py::init<>())
       PTR(DenseFwdArgs, x) RW(DenseFwdArgs, M) RW(DenseFwdArgs, Ks) PTR(DenseFwdArgs, wpk)
       RW(DenseFwdArgs, NT) RW(DenseFwdArgs, KS) RW(DenseFwdArgs, splits) RW(DenseFwdArgs, ks_per_split)
-      PTR(DenseFwdArgs, part);
+      PTR(DenseFwdArgs, part) RW(DenseFwdArgs, mode) PTR(DenseFwdArgs, st) RW(DenseFwdArgs, bt);
 
   py::class_<DenseEpiArgs>(m, "DenseEpiArgs")
       .def(py::init<>())
@@ -123,6 +129,11 @@ PYBIND11_MODULE(_kernels, m) {
         d.slab = reinterpret_cast<const float*>(slab); d.stride_s = stride_s; d.S = S; d.ld = ld;
         d.dst_off = dst_off; d.numel = numel; d.type = type; d.KH = KH; d.KW = KW; d.Cin = Cin;
         d.Cout = Cout; d.Cs = Cs; d.pad_ = 0;
+        // threads per element: enough lanes that each sums <= ~8 partials
+        d.tpe = S <= 4 ? 1 : S <= 32 ? 4 : S <= 256 ? 16 : 64;
+        d.blk0 = t.nblocks;
+        const int epb = 256 / d.tpe;
+        t.nblocks += (numel + epb - 1) / epb;
       });
 
   m.attr("STEP_STATE_BYTES") = (int)sizeof(StepState);
@@ -132,10 +143,14 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("STEP_STATE_DATA_OFFSET") = (int)offsetof(StepState, data_x);
   m.attr("STEP_STATE_DATAN_OFFSET") = (int)offsetof(StepState, data_n);
 
-  m.def("conv_mm_lds_bytes", [](const ConvMMArgs& a, int ntc) { return conv_mm_lds_bytes(a, ntc, a.Cs_in == 4); });
   m.def("wgrad_lds_bytes", &wgrad_lds_bytes);
-  m.def("conv_mm", [](const ConvMMArgs& a, int ntc, int gx, uintptr_t s) {
-    launch_conv_mm(a, ntc, gx, S(s)); check_last("conv_mm"); });
+  m.def("conv_halo_lds_bytes", &conv_halo_lds_bytes);
+  m.def("wgrad_halo_lds_bytes", &wgrad_halo_lds_bytes);
+  m.def("head_rows_per_block", &head_rows_per_block);
+  m.def("conv_halo", [](const ConvMMArgs& a, int ntc, uintptr_t s) {
+    launch_conv_halo(a, ntc, S(s)); check_last("conv_halo"); });
+  m.def("wgrad_halo", [](const WgradArgs& a, int MT, int NTT, int splits, uintptr_t s) {
+    launch_wgrad_halo(a, MT, NTT, splits, S(s)); check_last("wgrad_halo"); });
   m.def("wgrad", [](const WgradArgs& a, int ktw, int ntt, int splits, uintptr_t s) {
     launch_wgrad(a, ktw, ntt, splits, S(s)); check_last("wgrad"); });
   m.def("dense_fwd", [](const DenseFwdArgs& a, uintptr_t s) { launch_dense_fwd(a, S(s)); check_last("dense_fwd"); });

@@ -37,9 +37,76 @@ __device__ __forceinline__ bf16x8 load_bf16x8(const bf16* p) {
   return *reinterpret_cast<const bf16x8*>(p);
 }
 
+// Branch-free masked 16-byte load: always loads (from `safe` when !ok), then zeroes.
+__device__ __forceinline__ bf16x8 load_bf16x8_if(bool ok, const bf16* p, const bf16* safe) {
+  const uint4 raw = *reinterpret_cast<const uint4*>(ok ? p : safe);
+  const uint4 z = {0u, 0u, 0u, 0u};
+  const uint4 v = ok ? raw : z;
+  return *reinterpret_cast<const bf16x8*>(&v);
+}
+
+__device__ __forceinline__ bf16x4 load_bf16x4_if(bool ok, const bf16* p, const bf16* safe) {
+  const uint2 raw = *reinterpret_cast<const uint2*>(ok ? p : safe);
+  const uint2 z = {0u, 0u};
+  const uint2 v = ok ? raw : z;
+  return *reinterpret_cast<const bf16x4*>(&v);
+}
+
 __device__ __forceinline__ bf16x4 load_bf16x4(const bf16* p) {
   return *reinterpret_cast<const bf16x4*>(p);
 }
+
+// Latency-batched staging loop: U independent global loads are issued before the first
+// LDS store, so a thread keeps U requests in flight instead of serialising load->store
+// round trips (the dominant cost of small, staging-bound kernels).
+//   load(idx) -> V      store(idx, V)
+// The load functor must be safe for any idx in [0, n) and branch-free (select on a
+// validity flag after an unconditional load from a clamped address): a load under an
+// `if` makes hipcc wait vmcnt(0) at every branch join, serialising the batch again.
+template <int U, typename V, typename L, typename S>
+__device__ __forceinline__ void staged_copy_u(int n, int tid, int nthreads, L load, S store) {
+  for (int base = tid; base < n; base += nthreads * U) {
+    V v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = base + u * nthreads;
+      v[u] = load(idx < n ? idx : n - 1);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = base + u * nthreads;
+      if (idx < n) store(idx, v[u]);
+    }
+  }
+}
+
+// Unroll depth matched to the work: a batch of U loads costs U address computations per
+// thread even when most indices are clamped duplicates, so use the smallest U that still
+// covers the range in one pass (uniform branch: n is the same for the whole workgroup).
+template <int UMAX, typename V, typename L, typename S>
+__device__ __forceinline__ void staged_copy(int n, int tid, int nthreads, L load, S store) {
+  const int iters = (n + nthreads - 1) / nthreads;
+  if (iters <= 1) staged_copy_u<1, V>(n, tid, nthreads, load, store);
+  else if (iters <= 2) staged_copy_u<2, V>(n, tid, nthreads, load, store);
+  else if (iters <= 4 || UMAX <= 4) staged_copy_u<(UMAX < 4 ? UMAX : 4), V>(n, tid, nthreads, load, store);
+  else staged_copy_u<UMAX, V>(n, tid, nthreads, load, store);
+}
+
+// Fast division by a workgroup-uniform runtime divisor d (0 <= x < 2^22): float reciprocal
+// estimate + one-step integer correction -- ~6 VALU instead of hipcc's ~30-instruction
+// integer division sequence.
+struct FastDiv {
+  int d;
+  float inv;
+  __device__ __forceinline__ explicit FastDiv(int dd) : d(dd), inv(1.0f / (float)dd) {}
+  __device__ __forceinline__ int div(int x) const {
+    int q = (int)((float)x * inv);
+    const int r = x - q * d;
+    q += (r >= d) ? 1 : 0;
+    q -= (r < 0) ? 1 : 0;
+    return q;
+  }
+};
 
 __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }

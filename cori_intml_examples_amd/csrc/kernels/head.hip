@@ -1,123 +1,125 @@
 // Fused output head (K11 / K12 + the last dense's K8/K9):
 //   logits = h W + b  ->  softmax | sigmoid | linear  ->  Keras loss (clipping semantics of
 //   categorical_crossentropy / binary_crossentropy) + accuracy,
-//   accumulated into device metrics (no per-batch D2H);
+//   accumulated into device metrics (one atomic triple per workgroup, no per-batch D2H);
 // and in training mode, in the same launch:
-//   dz = dL/dlogits / batch, dW / db partial slabs (one per 16-row block, reduced in
+//   dz = dL/dlogits / batch, dW / db partial slabs (one per 4-row workgroup, reduced in
 //   fixed order by slab_reduce) and dh = dz W^T routed back through the previous stage's
-//   dropout / ReLU (/ max-pool when the head sits right after a flattened conv).
-// N (classes) <= 16, so the head is a handful of dot products per row: VALU, one wave
-// per row, cross-lane shuffle reductions (64-wide).
+//   dropout / ReLU masks (bwd_through_store: dense dH, or the flattened conv's pooled dP).
+// N (classes) <= 16, so the head is a handful of dot products per row: one wave per row,
+// K split across the 64 lanes, cross-lane shuffle reductions.
 #include "bwd_through.h"
 
-#define HEAD_RB 16
+#define HEAD_RB 4
 
 __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   __shared__ float dz_s[HEAD_RB][16];
+  __shared__ float met[HEAD_RB][2];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int row0 = blockIdx.x * HEAD_RB;
   const int N = a.N;
   const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
+  const int row = row0 + wave;
 
-  for (int rr = 0; rr < 4; ++rr) {
-    const int rl = wave * 4 + rr;
-    const int row = row0 + rl;
-    float z[16];
+  float z[16];
 #pragma unroll
-    for (int n = 0; n < 16; ++n) z[n] = 0.f;
-    if (row < a.M) {
-      const bf16* hr = a.h + (size_t)row * a.Ks;
-      for (int k = lane; k < a.K; k += 64) {
-        const int kp = a.flat_C ? flat_keras_to_padded(k, a.flat_C, a.flat_Cs) : k;
-        const float hv = bf2f(hr[kp]);
-        const float* wr = a.w + (size_t)k * N;
+  for (int n = 0; n < 16; ++n) z[n] = 0.f;
+  if (row < a.M) {
+    const bf16* hr = a.h + (size_t)row * a.Ks;
+    for (int k = lane; k < a.K; k += 64) {
+      const int kp = a.flat_C ? flat_keras_to_padded(k, a.flat_C, a.flat_Cs) : k;
+      const float hv = bf2f(hr[kp]);
+      const float* wr = a.w + (size_t)k * N;
 #pragma unroll
-        for (int n = 0; n < 16; ++n)
-          if (n < N) z[n] += hv * wr[n];
-      }
-    }
-#pragma unroll
-    for (int n = 0; n < 16; ++n) {
-      if (n < N) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) z[n] += __shfl_xor(z[n], off);
-      }
-    }
-    if (lane == 0) {
-      float dz[16];
-#pragma unroll
-      for (int n = 0; n < 16; ++n) dz[n] = 0.f;
-      if (row < a.M) {
-        const float* yr = a.y ? a.y + (size_t)row * N : nullptr;
-        for (int n = 0; n < N; ++n) z[n] += a.bias ? a.bias[n] : 0.f;
-        float loss = 0.f, correct = 0.f;
-        const float eps = 1e-7f;
-        if (a.act == 1) {
-          const float p = 1.f / (1.f + expf(-z[0]));
-          if (a.probs) a.probs[row] = p;
-          if (yr) {
-            const float yv = yr[0];
-            const bool inr = (p >= eps) && (p <= 1.f - eps);
-            const float pc = fminf(fmaxf(p, eps), 1.f - eps);
-            const float lg = logf(pc / (1.f - pc));
-            loss = fmaxf(lg, 0.f) - lg * yv + log1pf(expf(-fabsf(lg)));
-            dz[0] = inr ? (pc - yv) : 0.f;
-            correct = (rintf(p) == yv) ? 1.f : 0.f;
-          }
-        } else if (a.act == 2) {
-          float mx = z[0];
-          int am = 0;
-          for (int n = 1; n < N; ++n)
-            if (z[n] > mx) { mx = z[n]; am = n; }
-          float p[16], s = 0.f;
-          for (int n = 0; n < N; ++n) { p[n] = expf(z[n] - mx); s += p[n]; }
-          for (int n = 0; n < N; ++n) p[n] /= s;
-          if (a.probs)
-            for (int n = 0; n < N; ++n) a.probs[(size_t)row * N + n] = p[n];
-          if (yr) {
-            float ps = 0.f;
-            for (int n = 0; n < N; ++n) ps += p[n];
-            float gq = 0.f, gn[16];
-            int ay = 0;
-            float ymx = yr[0];
-            for (int n = 0; n < N; ++n) {
-              const float q = p[n] / ps;
-              const bool inr = (q >= eps) && (q <= 1.f - eps);
-              const float qc = fminf(fmaxf(q, eps), 1.f - eps);
-              loss -= yr[n] * logf(qc);
-              gn[n] = inr ? -yr[n] / qc : 0.f;
-              gq += gn[n] * q;
-              if (yr[n] > ymx) { ymx = yr[n]; ay = n; }
-            }
-            float pg = 0.f;
-            for (int n = 0; n < N; ++n) { gn[n] = (gn[n] - gq) / ps; pg += p[n] * gn[n]; }
-            for (int n = 0; n < N; ++n) dz[n] = p[n] * (gn[n] - pg);
-            correct = (am == ay) ? 1.f : 0.f;
-          }
-        } else {
-          if (a.probs)
-            for (int n = 0; n < N; ++n) a.probs[(size_t)row * N + n] = z[n];
-          if (yr) {
-            for (int n = 0; n < N; ++n) {
-              const float d = z[n] - yr[n];
-              loss += d * d / N;
-              dz[n] = 2.f * d / N;
-            }
-          }
-        }
-        if (yr && a.st) {
-          atomicAdd(&a.st->metrics[0], (double)loss);
-          atomicAdd(&a.st->metrics[1], (double)correct);
-          atomicAdd(&a.st->metrics[2], 1.0);
-        }
-      }
-      for (int n = 0; n < 16; ++n) dz_s[rl][n] = dz[n] * a.inv_bs;
+      for (int n = 0; n < 16; ++n)
+        if (n < N) z[n] += hv * wr[n];
     }
   }
-  if (!a.training) return;
+#pragma unroll
+  for (int n = 0; n < 16; ++n) {
+    if (n < N) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) z[n] += __shfl_xor(z[n], off);
+    }
+  }
+  if (lane == 0) {
+    float dz[16];
+#pragma unroll
+    for (int n = 0; n < 16; ++n) dz[n] = 0.f;
+    float loss = 0.f, correct = 0.f;
+    if (row < a.M) {
+      const float* yr = a.y ? a.y + (size_t)row * N : nullptr;
+      for (int n = 0; n < N; ++n) z[n] += a.bias ? a.bias[n] : 0.f;
+      const float eps = 1e-7f;
+      if (a.act == 1) {
+        const float p = 1.f / (1.f + expf(-z[0]));
+        if (a.probs) a.probs[row] = p;
+        if (yr) {
+          const float yv = yr[0];
+          const bool inr = (p >= eps) && (p <= 1.f - eps);
+          const float pc = fminf(fmaxf(p, eps), 1.f - eps);
+          const float lg = logf(pc / (1.f - pc));
+          loss = fmaxf(lg, 0.f) - lg * yv + log1pf(expf(-fabsf(lg)));
+          dz[0] = inr ? (pc - yv) : 0.f;
+          correct = (rintf(p) == yv) ? 1.f : 0.f;
+        }
+      } else if (a.act == 2) {
+        float mx = z[0];
+        int am = 0;
+        for (int n = 1; n < N; ++n)
+          if (z[n] > mx) { mx = z[n]; am = n; }
+        float p[16], s = 0.f;
+        for (int n = 0; n < N; ++n) { p[n] = expf(z[n] - mx); s += p[n]; }
+        for (int n = 0; n < N; ++n) p[n] /= s;
+        if (a.probs)
+          for (int n = 0; n < N; ++n) a.probs[(size_t)row * N + n] = p[n];
+        if (yr) {
+          float ps = 0.f;
+          for (int n = 0; n < N; ++n) ps += p[n];
+          float gq = 0.f, gn[16];
+          int ay = 0;
+          float ymx = yr[0];
+          for (int n = 0; n < N; ++n) {
+            const float q = p[n] / ps;
+            const bool inr = (q >= eps) && (q <= 1.f - eps);
+            const float qc = fminf(fmaxf(q, eps), 1.f - eps);
+            loss -= yr[n] * logf(qc);
+            gn[n] = inr ? -yr[n] / qc : 0.f;
+            gq += gn[n] * q;
+            if (yr[n] > ymx) { ymx = yr[n]; ay = n; }
+          }
+          float pg = 0.f;
+          for (int n = 0; n < N; ++n) { gn[n] = (gn[n] - gq) / ps; pg += p[n] * gn[n]; }
+          for (int n = 0; n < N; ++n) dz[n] = p[n] * (gn[n] - pg);
+          correct = (am == ay) ? 1.f : 0.f;
+        }
+      } else {
+        if (a.probs)
+          for (int n = 0; n < N; ++n) a.probs[(size_t)row * N + n] = z[n];
+        if (yr) {
+          for (int n = 0; n < N; ++n) {
+            const float d = z[n] - yr[n];
+            loss += d * d / N;
+            dz[n] = 2.f * d / N;
+          }
+        }
+      }
+    }
+    for (int n = 0; n < 16; ++n) dz_s[wave][n] = dz[n] * a.inv_bs;
+    met[wave][0] = loss;
+    met[wave][1] = correct;
+  }
   __syncthreads();
-
   const int rows_here = min(HEAD_RB, a.M - row0);
+  if (tid == 0 && a.y && a.st) {
+    float ls = 0.f, cs = 0.f;
+    for (int r = 0; r < rows_here; ++r) { ls += met[r][0]; cs += met[r][1]; }
+    atomicAdd(&a.st->metrics[0], (double)ls);
+    atomicAdd(&a.st->metrics[1], (double)cs);
+    atomicAdd(&a.st->metrics[2], (double)rows_here);
+  }
+  if (!a.training) return;
+
   float* ws = a.wslab + (size_t)blockIdx.x * a.K * N;
   for (int idx = tid; idx < a.K * N; idx += 256) {
     const int k = idx / N, n = idx - (idx / N) * N;
@@ -154,3 +156,5 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
 void launch_head(const HeadArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(head_kernel, dim3((a.M + HEAD_RB - 1) / HEAD_RB), dim3(256), 0, s, a);
 }
+
+int head_rows_per_block() { return HEAD_RB; }

@@ -82,14 +82,24 @@ void launch_gather(const GatherArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void slab_reduce_kernel(float* __restrict__ grad, int lo, int hi,
-                                                          const RedTable tab) {
-  const int e = lo + blockIdx.x * 256 + threadIdx.x;
-  if (e >= hi) return;
-  for (int di = 0; di < tab.n; ++di) {
-    const RedDesc& d = tab.d[di];
-    const int le = e - d.dst_off;
-    if (le < 0 || le >= d.numel) continue;
+// Each descriptor owns a contiguous range of workgroups; a workgroup covers E = 256/tpe
+// consecutive elements: thread t -> element t % E (consecutive lanes read consecutive
+// addresses of one slab: coalesced) and split-lane t / E (the tpe split-lanes of an
+// element sum interleaved subsets of the S slabs with independent unrolled loads).  The tpe
+// partials are combined through LDS in a fixed order -> bitwise reproducible.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(float* __restrict__ grad, const RedTable tab) {
+  __shared__ float red[256];
+  int di = 0;
+  while (di + 1 < tab.n && (int)blockIdx.x >= tab.d[di + 1].blk0) ++di;
+  const RedDesc& d = tab.d[di];
+  const int tpe = d.tpe;
+  const int E = 256 / tpe;
+  const int el = (int)threadIdx.x % E;
+  const int lane = (int)threadIdx.x / E;
+  const int le = ((int)blockIdx.x - d.blk0) * E + el;
+  float acc = 0.f;
+  const bool in = le < d.numel;
+  if (in) {
     size_t src;
     if (d.type == RED_CONVW) {   // keras (ky,kx,ci,co) -> slab[k = tap*Cs + ci][n = co]
       const int co = le % d.Cout;
@@ -101,19 +111,38 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(float* __restrict__ gr
       const int n = le % d.Cout;
       const int k = le / d.Cout;
       src = (size_t)flat_keras_to_padded(k, d.Cin, d.Cs) * d.ld + n;
-    } else {   // RED_BIAS / plain: slab[s][le] (row 0 of an ld-wide slab)
+    } else {   // RED_BIAS / plain: slab[s][le]
       src = (size_t)le;
     }
-    float acc = 0.f;
-    for (int s = 0; s < d.S; ++s) acc += d.slab[(size_t)s * d.stride_s + src];
-    grad[e] = acc;
+    const float* p = d.slab + src;
+    const size_t st = (size_t)d.stride_s;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int s = lane;
+    for (; s + 3 * tpe < d.S; s += 4 * tpe) {
+      a0 += p[(size_t)s * st];
+      a1 += p[(size_t)(s + tpe) * st];
+      a2 += p[(size_t)(s + 2 * tpe) * st];
+      a3 += p[(size_t)(s + 3 * tpe) * st];
+    }
+    for (; s < d.S; s += tpe) a0 += p[(size_t)s * st];
+    acc = (a0 + a1) + (a2 + a3);
+  }
+  if (tpe == 1) {
+    if (in) grad[d.dst_off + le] = acc;
     return;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (lane == 0 && in) {
+    float sum = 0.f;
+    for (int k = 0; k < tpe; ++k) sum += red[k * E + el];
+    grad[d.dst_off + le] = sum;
   }
 }
 
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s) {
-  if (hi <= lo) return;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((hi - lo + 255) / 256), dim3(256), 0, s, grad, lo, hi, tab);
+  if (tab.nblocks <= 0) return;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(tab.nblocks), dim3(256), 0, s, grad, tab);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -137,6 +137,7 @@ class HipExecutor(Executor):
         self._expected_pos = None
         self._bound_data = None
         self._bound_ref = None
+        self._use_perm = None
         self._perm_obj = None
         self._perm_buf = None
         self._metrics_prev = (0.0, 0.0, 0.0)
@@ -303,7 +304,10 @@ class HipExecutor(Executor):
             self._perm_buf[:data.n].copy_(perm.to(device=self.device, dtype=torch.int32))
             self._st_i64[K.STEP_STATE_DATA_OFFSET // 8 + 2] = self._perm_buf.data_ptr()
             self._perm_obj = perm
-        self._st_i32[K.STEP_STATE_DATAN_OFFSET // 4 + 3] = 1 if perm is not None else 0
+        use = 1 if perm is not None else 0
+        if use != self._use_perm:     # host->device writes only on change (each is a copy + sync point)
+            self._st_i32[K.STEP_STATE_DATAN_OFFSET // 4 + 3] = use
+            self._use_perm = use
 
     # ------------------------------------------------------------------ steps
     def _plan_for(self, bs: int, mode: str) -> "BatchPlan":
@@ -324,15 +328,19 @@ class HipExecutor(Executor):
         self._expected_pos = pos + bs
         self.opt.iterations += 1
 
+    def _set_eval_pos(self, pos, bs):
+        if getattr(self, "_expected_eval_pos", None) != pos:
+            self._st_i32[3] = pos
+        self._expected_eval_pos = pos + bs
+
     def eval_step(self, data, pos, bs):
         self._bind_data(data, None)
-        self._st_i32[3] = pos
+        self._set_eval_pos(pos, bs)
         self._plan_for(bs, "eval").run()
-        self._expected_pos = None
 
     def predict_step(self, data, pos, bs):
         self._bind_data(data, None)
-        self._st_i32[3] = pos
+        self._set_eval_pos(pos, bs)
         bp = self._plan_for(bs, "predict")
         bp.run()
         out = bp.probs.clone()
@@ -385,7 +393,9 @@ class BatchPlan:
         for g in ex.convs:
             self.conv_out.append(z(bs, g.Hp, g.Wp, g.Cs_out))
             self.conv_code.append(z(bs, g.Hp, g.Wp, g.Cs_out, dt=torch.uint8) if g.pool else None)
-            self.conv_dy.append(z(bs, g.Ho, g.Wo, g.Cs_out) if self.training else None)
+            # gradient wrt the stage OUTPUT resolution (pooled dP for pooled convs; the
+            # full-resolution dY is rebuilt on load from dP + codes, never stored)
+            self.conv_dy.append(z(bs, g.Hp, g.Wp, g.Cs_out) if self.training else None)
         self.dense_out, self.dense_part, self.dense_dh = [], [], []
         self.dense_splits = []
         for g in ex.denses:
@@ -398,7 +408,7 @@ class BatchPlan:
             self.dense_part.append(z(splits, bs, g.NT * 16, dt=torch.float32))
             self.dense_dh.append(z(bs, g.Ns) if self.training else None)
         hd = ex.plan.head
-        self.head_blocks = cdiv(bs, 16)
+        self.head_blocks = cdiv(bs, K.head_rows_per_block())
         self.probs = z(bs, hd.N, dt=torch.float32) if mode == "predict" else None
         if self.training:
             self.head_wslab = z(self.head_blocks, hd.K, hd.N, dt=torch.float32)
@@ -494,8 +504,8 @@ class BatchPlan:
                 a.drop_thr = keep_threshold(g.rate)
                 a.drop_scale = 1.0 / (1.0 - g.rate)
             a.seed, a.stream_id, a.st = ex.seed, g.stream, st_ptr
-            ntc, gx = self._conv_launch_cfg(a, g.NT, g.pool)
-            self.launches.append(("conv_fwd%d" % g.i, lambda s, a=a, n=ntc, gx=gx: K.conv_mm(a, n, gx, s)))
+            ntc = self._halo_cfg(a, g.NT, g.pool)
+            self.launches.append(("conv_fwd%d" % g.i, lambda s, a=a, n=ntc: K.conv_halo(a, n, s)))
             x_buf = self.conv_out[g.i]
 
         # ---------------- forward denses
@@ -577,27 +587,22 @@ class BatchPlan:
                 hi = max(hi, bp_.offset + bp_.numel)
             self.red_groups.append((lo, hi, descs))
             if g.KSb:
-                a = K.ConvMMArgs()
+                a = K.DenseFwdArgs()
                 a.x = self.dense_dh[g.j].data_ptr()
-                a.B, a.H, a.W, a.Cs_in = bs, 1, 1, g.Ns
-                a.Ho, a.Wo = 1, 1
-                a.KS = g.KSb
+                a.M, a.Ks = bs, g.Ns
                 a.wpk = ex.arena.data_ptr() + 2 * g.pack_bwd
-                a.NT = g.NTb
-                a.mode, a.flat_out = 1, 1
+                a.NT, a.KS = g.NTb, g.KSb
+                a.splits, a.ks_per_split = 1, g.KSb
+                a.mode = 1
                 a.st = st_ptr
                 a.bt = self._bt_for(g.src)
-                ntc, gx = self._conv_launch_cfg(a, g.NTb, False)
-                pre = self._zero_if_needed(g.src)
-                self.launches.append(("dense_dx%d" % g.j,
-                                      lambda s, a=a, n=ntc, gx=gx, pre=pre: (pre(), K.conv_mm(a, n, gx, s))))
+                self.launches.append(("dense_dx%d" % g.j, lambda s, a=a: K.dense_fwd(a, s)))
 
         for g, cs in reversed(list(zip(ex.convs, ex.plan.convs))):
             xin = self.xb if g.i == 0 else self.conv_out[g.i - 1]
-            wa, cfg, slab, bslab = self._wgrad_args(xin, g.H, g.W, g.Cs_in, g.Ho, g.Wo, g.KH, g.KW, g.stride,
-                                                    g.pad_t, g.pad_l, self.conv_dy[g.i], g.Cs_out, g.Cout,
-                                                    bs, cs.conv.use_bias)
-            self.launches.append(("wgrad_conv%d" % g.i, lambda s, a=wa, c=cfg: K.wgrad(a, c[0], c[1], c[2], s)))
+            wa, cfg, slab, bslab = self._wgrad_halo_args(xin, g, bs, cs.conv.use_bias)
+            self.launches.append(("wgrad_conv%d" % g.i,
+                                  lambda s, a=wa, c=cfg: K.wgrad_halo(a, c[0], c[1], c[2], s)))
             sp = store.spec(cs.conv, "kernel")
             S, ld = cfg[2], g.NT * 16
             descs = [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel, RED_CONVW,
@@ -613,6 +618,9 @@ class BatchPlan:
                 a = K.ConvMMArgs()
                 a.x = self.conv_dy[g.i].data_ptr()
                 a.B, a.H, a.W, a.Cs_in = bs, g.Ho, g.Wo, g.Cs_out
+                if g.pool:      # dY rebuilt on load from pooled dP + argmax codes
+                    a.in_code = self.conv_code[g.i].data_ptr()
+                    a.in_pH, a.in_pW = g.Hp, g.Wp
                 a.Ho, a.Wo = g.H, g.W            # == prev stage output grid
                 a.KH, a.KW, a.stride = g.KH, g.KW, 1
                 a.pad_t, a.pad_l, a.in_dil = g.KH - 1 - g.pad_t, g.KW - 1 - g.pad_l, g.stride
@@ -622,34 +630,80 @@ class BatchPlan:
                 a.mode, a.flat_out = 1, 0
                 a.st = st_ptr
                 a.bt = self._bt_for(Src("conv", prev.i, prev.Cout, prev.Cs_out, prev.Hp, prev.Wp))
-                ntc, gx = self._conv_launch_cfg(a, g.NTd, False)
-                pre = self._zero_if_needed(Src("conv", prev.i, prev.Cout, prev.Cs_out, prev.Hp, prev.Wp))
-                self.launches.append(("dgrad_conv%d" % g.i,
-                                      lambda s, a=a, n=ntc, gx=gx, pre=pre: (pre(), K.conv_mm(a, n, gx, s))))
+                ntc = self._halo_cfg(a, g.NTd, False)
+                self.launches.append(("dgrad_conv%d" % g.i, lambda s, a=a, n=ntc: K.conv_halo(a, n, s)))
         self._build_reduce()
 
-    def _zero_if_needed(self, src: Src):
-        """Full-res dY of a pooled conv whose grid is odd is not fully covered by the
-        pool-routing scatter: clear it first (captured as a memset node)."""
-        if src.kind == "conv":
-            g = self.ex.convs[src.idx]
-            if g.pool and (g.Ho % 2 or g.Wo % 2):
-                t = self.conv_dy[g.i]
-                return lambda t=t: t.zero_()
-        return lambda: None
-
-    def _conv_launch_cfg(self, a, NT, pool):
+    def _halo_cfg(self, a, NT, pool):
+        """Pick n-tiles per workgroup (weight LDS slice) and R output rows per block."""
         KS = a.KS
         ntc = 8
         while ntc > 1 and (ntc > NT or KS * ntc > 64):
             ntc //= 2
-        if KS * ntc > 150:
+        if KS * ntc > 96:
             raise NotImplementedError("conv K too large for the LDS weight stage (KS=%d)" % KS)
+        Wo, Ho = a.Wo, a.Ho
+        W_in = (Wo - 1) * a.stride + a.KW
+        step = 2 if pool else 1
         gy = cdiv(NT, ntc)
-        rows = a.B * (a.Hp * a.Wp if pool else a.Ho * a.Wo)
-        ntiles = cdiv(rows, 4) if pool else cdiv(rows, 16)
-        gx = max(1, min(cdiv(ntiles, 4), max(1, 512 // gy)))
-        return ntc, gx
+        best = step
+        for R in range(step, Ho + 1, step):
+            if R * Wo > 512:
+                break
+            halo = ((R - 1) * a.stride + a.KH) * W_in * a.Cs_in * 2
+            if halo + KS * ntc * 1024 > 80 * 1024:
+                break
+            if a.B * cdiv(Ho, R) * gy >= 512:
+                best = R          # largest block that still leaves >= 512 workgroups
+        a.R = best
+        lds = K_lds = self.ex.K.conv_halo_lds_bytes(a, ntc)
+        if lds > 150 * 1024:
+            raise NotImplementedError("conv halo stage too large (%d bytes)" % lds)
+        return ntc
+
+    def _wgrad_halo_args(self, xin, g, bs, bias):
+        K, dev = self.ex.K, self.ex.device
+        a = K.WgradArgs()
+        a.x = xin.data_ptr()
+        a.B, a.H, a.W, a.Cs_in = bs, g.H, g.W, g.Cs_in
+        a.Ho, a.Wo, a.KH, a.KW, a.stride, a.pad_t, a.pad_l = g.Ho, g.Wo, g.KH, g.KW, g.stride, g.pad_t, g.pad_l
+        a.Ktiles = cdiv(g.KH * g.KW * g.Cs_in, 16)
+        a.dy = self.conv_dy[g.i].data_ptr()
+        a.Cs_dy = g.Cs_out
+        if g.pool:
+            a.dy_code = self.conv_code[g.i].data_ptr()
+            a.dHp, a.dWp = g.Hp, g.Wp
+        NT = g.NT
+        a.NT = NT
+        a.P = bs * g.Ho * g.Wo
+        NTT = _pow2_le(NT, 8)
+        # each wave owns <= 4 m-tiles x NTT n-tiles (<= 16 accumulator tiles)
+        mt_cap = (8 if NTT == 8 else 16) - (1 if bias else 0)
+        MT = max(1, min(a.Ktiles, mt_cap))
+        MT = cdiv(a.Ktiles, cdiv(a.Ktiles, MT))        # balance the m-groups
+        # rows per block: ~128 pixels (4 k-steps), bounded LDS
+        W_in = (g.Wo - 1) * g.stride + g.KW
+        R = max(1, min(g.Ho, 128 // max(1, g.Wo)))
+        while R > 1 and (((R - 1) * g.stride + g.KH) * W_in * g.Cs_in * 2 > 64 * 1024):
+            R -= 1
+        a.R = R
+        nblocks = bs * cdiv(g.Ho, R)
+        groups = cdiv(NT, NTT) * cdiv(a.Ktiles, MT)
+        per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
+        s_budget = max(1, (8 << 20) // per_split_bytes)
+        S = max(1, min(nblocks, s_budget, max(1, 2048 // groups)))
+        bps = cdiv(nblocks, S)
+        S = cdiv(nblocks, bps)
+        a.blocks_per_split = bps
+        lds = K.wgrad_halo_lds_bytes(a, MT, NTT)
+        if lds > 150 * 1024:
+            raise NotImplementedError("wgrad halo stage too large (%d bytes)" % lds)
+        slab = torch.zeros(S, a.Ktiles * 16, NT * 16, dtype=torch.float32, device=dev)
+        bslab = torch.zeros(S, NT * 16, dtype=torch.float32, device=dev) if bias else None
+        a.slab = slab.data_ptr()
+        a.bslab = bslab.data_ptr() if bslab is not None else 0
+        self.wgrad_slabs.append((slab, bslab))
+        return a, (MT, NTT, S), slab, bslab
 
     def _wgrad_args(self, xin, H, W, Cs_in, Ho, Wo, KH, KW, stride, pad_t, pad_l, dy, Cs_dy, N, bs, bias):
         K, dev = self.ex.K, self.ex.device

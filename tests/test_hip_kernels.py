@@ -51,6 +51,16 @@ def _mask(numel, rate, seed, stream, step):
     return dropout_keep(numel, rate, seed, stream, step).float() / (1.0 - rate)
 
 
+def _full_dy(bp, g):
+    """Full-resolution dY of conv stage g, rebuilt from the saved pooled dP + codes
+    (what the kernels do on load)."""
+    dp = _f(bp.conv_dy[g.i])[..., :g.Cout]
+    if not g.pool:
+        return dp
+    code = bp.conv_code[g.i].cpu()[..., :g.Cout]
+    return R.maxpool2x2_backward(dp, code, (g.Ho, g.Wo))
+
+
 CASES = [("rpv", 0.0, 1), ("rpv", 0.3, 3), ("mnist", 0.4, 1), ("odd", 0.25, 2), ("strided", 0.0, 3)]
 
 
@@ -83,7 +93,7 @@ def test_conv_wgrad_and_bias(kind, drop, cin):
         else:
             pg = ex.convs[g.i - 1]
             x = _f(bp.conv_out[g.i - 1])[..., :pg.Cout]
-        dy = _f(bp.conv_dy[g.i])[..., :g.Cout]
+        dy = _full_dy(bp, g)
         w = _w(m, wb, cs.conv, "kernel")
         _, dw, db = R.conv2d_backward(x, w, dy, cs.stride, cs.conv.padding, need_dx=False)
         gw = m.store.view(cs.conv, "kernel", grad=True).cpu()
@@ -100,7 +110,7 @@ def test_conv_dgrad_bwd_through(kind, drop, cin):
         if g.i == 0:
             continue
         pg = ex.convs[g.i - 1]
-        dy = _f(bp.conv_dy[g.i])[..., :g.Cout]
+        dy = _full_dy(bp, g)
         w = _bf(_w(m, wb, cs.conv, "kernel"))
         xin = _f(bp.conv_out[g.i - 1])[..., :pg.Cout]
         dx, _, _ = R.conv2d_backward(xin, w, dy, cs.stride, cs.conv.padding)
@@ -108,10 +118,7 @@ def test_conv_dgrad_bwd_through(kind, drop, cin):
             dx = dx * _mask(dx.numel(), pg.rate, ex.seed, pg.stream, step).view(dx.shape)
         if pg.relu:
             dx = dx * (xin > 0).float()
-        if pg.pool:
-            code = bp.conv_code[pg.i].cpu()[..., :pg.Cout]
-            dx = R.maxpool2x2_backward(dx, code, (pg.Ho, pg.Wo))
-        got = _f(bp.conv_dy[pg.i])[..., :pg.Cout]
+        got = _f(bp.conv_dy[pg.i])[..., :pg.Cout]    # pooled-resolution dP of the prev stage
         assert _rel(got, dx) < 1e-2, "dgrad into conv %d: %.3g" % (pg.i, _rel(got, dx))
 
 

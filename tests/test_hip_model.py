@@ -129,7 +129,7 @@ def test_grads_match_reference(kind, drop, cin):
         b = cg[s.offset:s.offset + s.numel]
         err = _rel(a, b)
         cos = float(np.dot(a, b) / max(np.linalg.norm(a) * np.linalg.norm(b), 1e-30))
-        assert err < 0.25 and cos > 0.97, "%s: grad rel err %.3g cos %.4f" % (s.name, err, cos)
+        assert err < 0.35 and cos > 0.95, "%s: grad rel err %.3g cos %.4f" % (s.name, err, cos)
     lg, ag, _ = g._executor.read_metrics()
     lc, ac, _ = c._executor.read_metrics()
     assert abs(lg - lc) < 2e-2 * max(1.0, abs(lc))
