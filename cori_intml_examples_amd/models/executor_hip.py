@@ -258,6 +258,12 @@ class HipExecutor(Executor):
         for dst, src in zip(self.slots, slots):
             dst[:self.store.numel].copy_(torch.as_tensor(src, device=self.device).reshape(-1))
 
+    def m_schedule_value(self) -> float:
+        return float(self._st_f64[self.K.STEP_STATE_MSCHED_OFFSET // 8])
+
+    def set_m_schedule(self, v: float) -> None:
+        self._st_f64[self.K.STEP_STATE_MSCHED_OFFSET // 8] = float(v)
+
     def _sync_lr(self):
         lr = float(self.opt.lr)
         if lr != self._lr_host:

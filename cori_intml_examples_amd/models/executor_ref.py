@@ -202,6 +202,12 @@ class RefExecutor(Executor):
     def last_batch_metrics(self):
         return self._last
 
+    def m_schedule_value(self) -> float:
+        return float(self.m_schedule)
+
+    def set_m_schedule(self, v: float) -> None:
+        self.m_schedule = float(v)
+
     def optimizer_state(self):
         return [s[:self.store.numel] for s in self.slots]
 

@@ -358,7 +358,9 @@ class Sequential(Model):
         return self.layers
 
     def get_config(self):
-        return [{"class_name": type(l).__name__, "config": l.get_config()} for l in self.layers]
+        # Keras 2.2.4 form ({"name", "layers"}); 2.2.0's bare list is accepted on load
+        return {"name": self.name,
+                "layers": [{"class_name": type(l).__name__, "config": l.get_config()} for l in self.layers]}
 
 
 _SEQ = [0]
