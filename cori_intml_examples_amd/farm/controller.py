@@ -31,13 +31,14 @@ from . import protocol as P
 
 class _Task:
     __slots__ = ("msg_id", "client", "target", "kind", "payload", "engine", "state", "abort_deadline",
-                 "submitted")
+                 "interrupt_at", "submitted")
 
     def __init__(self, msg_id, client, target, kind, payload):
         self.msg_id, self.client, self.target, self.kind, self.payload = msg_id, client, target, kind, payload
         self.engine: Optional[int] = None
         self.state = "queued"         # queued | running | done
         self.abort_deadline: Optional[float] = None
+        self.interrupt_at: Optional[float] = None
         self.submitted = time.time()
 
 
@@ -312,8 +313,12 @@ class Controller:
             return
         rec = self.engines.get(task.engine)
         if rec is not None:
-            self._send(rec.conn, {"type": "interrupt", "msg_id": mid})
-            task.abort_deadline = time.time() + (self.abort_grace if grace is None else float(grace))
+            # staged cancel: cooperative flag now (training stops at the next batch end),
+            # KeyboardInterrupt at half the grace period, engine kill at the full grace
+            g = self.abort_grace if grace is None else float(grace)
+            self._send(rec.conn, {"type": "interrupt", "msg_id": mid, "cooperative_only": True})
+            task.interrupt_at = time.time() + 0.5 * g
+            task.abort_deadline = time.time() + g
 
     def _kill_engine(self, eid: int, why: str):
         rec = self.engines.get(eid)
@@ -327,6 +332,11 @@ class Controller:
     def _supervise(self):
         now = time.time()
         for t in list(self.tasks.values()):
+            if t.state == "running" and t.interrupt_at is not None and now > t.interrupt_at:
+                t.interrupt_at = None
+                rec = self.engines.get(t.engine)
+                if rec is not None:
+                    self._send(rec.conn, {"type": "interrupt", "msg_id": t.msg_id})
             if t.state == "running" and t.abort_deadline is not None and now > t.abort_deadline:
                 t.abort_deadline = None
                 self._kill_engine(t.engine, "abort grace expired")

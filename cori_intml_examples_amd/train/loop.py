@@ -73,6 +73,7 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
     elif verbose:
         print("Train on %d samples" % train.n)
 
+    from ..farm.engine import should_stop as farm_should_stop
     gen = torch.Generator(device="cpu")
     gen.manual_seed((model._seed + 7919 * (dp.rank if dp is not None else 0)) & 0x7FFFFFFF)
     cb.on_train_begin()
@@ -99,6 +100,8 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
             if progbar is not None and verbose == 1:
                 if need_batch_logs or b == nb - 1 or b % 50 == 0:
                     progbar.progress(pos + bs, [])
+            if farm_should_stop():      # Stop button / AsyncResult.abort on a farm engine
+                model.stop_training = True
             if model.stop_training:
                 break
         loss, acc, _ = ex.read_metrics()
