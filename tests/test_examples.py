@@ -1,0 +1,73 @@
+"""End-to-end runs of the notebook-workflow scripts in ``examples/`` (tiny sizes, CPU
+engines) and of the API-name aliases that let reference-style code run unchanged."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EX = os.path.join(ROOT, "examples")
+
+
+def _run(args, timeout=600, cwd=None):
+    env = dict(os.environ, INTML_DEVICE="cpu", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable] + args, cwd=cwd or EX, env=env, capture_output=True, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    return r.stdout
+
+
+def test_compat_aliases_run_reference_style_code():
+    code = r'''
+import cori_intml_examples_amd.compat as c
+print(c.install())
+import numpy as np
+import keras
+from keras.models import Sequential, load_model
+from keras.layers import Conv2D, MaxPooling2D, Dropout, Flatten, Dense, Input
+from keras.losses import categorical_crossentropy
+from keras import backend as K
+from keras.wrappers.scikit_learn import KerasClassifier
+import horovod.keras as hvd
+from ipyparallel.datapub import publish_data
+import ipyparallel as ipp
+import crayai.hpo as hpo
+K.set_image_data_format('channels_last')
+model = Sequential()
+model.add(Conv2D(4, (3, 3), activation='relu', input_shape=(12, 12, 1)))
+model.add(MaxPooling2D(pool_size=(2, 2)))
+model.add(Dropout(0.5))
+model.add(Flatten())
+model.add(Dense(10, activation='softmax'))
+model.compile(optimizer=getattr(keras.optimizers, 'Adam')(lr=0.01), loss=categorical_crossentropy,
+              metrics=['accuracy'])
+x = np.random.rand(64, 12, 12, 1).astype('float32')
+y = keras.utils.to_categorical(np.random.randint(0, 10, 64), 10)
+h = model.fit(x, y, batch_size=16, epochs=1, verbose=0)
+publish_data({'status': 'noop outside an engine'})
+hvd.init()
+print('ok', sorted(h.history), hvd.size(), hpo.Params([['--a', 1, (0, 2)]]).defaults())
+'''
+    out = _run(["-c", code], cwd=ROOT)
+    assert "ok ['acc', 'loss'] 1 {'--a': 1}" in out
+
+
+def test_dist_hpo_mnist_script():
+    out = _run(["dist_hpo_mnist.py", "--cpu", "--engines", "2", "--trials", "2", "--epochs", "1",
+                "--n-train", "400"])
+    assert "Trial 0: 64-32-64 dropout 0.624 Nadam" in out      # np.random.seed(0) sampling order
+    assert "Best model test loss" in out
+
+
+def test_cray_hpo_rpv_script(tmp_path):
+    out = _run(["cray_hpo_rpv.py", "--generations", "2", "--demes", "2", "--pop-size", "2", "--n-epochs", "1",
+                "--train-args", "--n-train 128 --n-valid 64 --batch-size 32", "--log", str(tmp_path / "r.log")])
+    assert "best FoM" in out
+    assert os.path.exists(tmp_path / "Deme1_r.log") and os.path.exists(tmp_path / "Deme2_r.log")
+
+
+def test_widget_hpo_script():
+    out = _run(["widget_hpo_mnist.py", "--cpu", "--engines", "2", "--trials", "2", "--epochs", "2",
+                "--n-train", "300"])
+    assert "Ended Training" in out and "best trial" in out
