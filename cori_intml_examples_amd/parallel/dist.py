@@ -53,7 +53,7 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
         be = tdist.get_backend()
     elif world > 1:
         use_gpu = torch.cuda.is_available() and os.environ.get("INTML_DEVICE", "cuda").startswith("cuda")
-        be = backend or ("nccl" if use_gpu else "gloo")
+        be = backend or os.environ.get("INTML_DP_BACKEND") or ("nccl" if use_gpu else "gloo")
         if use_gpu:
             torch.cuda.set_device(local_rank % torch.cuda.device_count())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -1,0 +1,103 @@
+"""GPU integration: checkpoint round-trip from the HIP executor, the train_rpv CLI on a
+GPU, a farm engine pinned to the GPU, and the HIP data-parallel step with 2 ranks."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _flat(m):
+    return np.concatenate([w.reshape(-1) for w in m.get_weights()])
+
+
+def test_checkpoint_roundtrip_gpu(tmp_path):
+    from cori_intml_examples_amd.apps import zoo
+    from cori_intml_examples_amd.io.datasets import synthetic_rpv
+    from cori_intml_examples_amd.models import load_model
+    x, y, _ = synthetic_rpv(256, channels=3, seed=1)
+    for opt in ("Adam", "Nadam"):
+        m = zoo.rpv_cnn((64, 64, 3), [16, 32, 64], [128], dropout=0.2, optimizer=opt, device="cuda:0")
+        assert type(m._executor).__name__ == "HipExecutor"
+        m.fit(x, y, batch_size=64, epochs=1, verbose=0)
+        p = str(tmp_path / ("m_%s.h5" % opt))
+        m.save(p)
+        m2 = load_model(p)
+        assert type(m2._executor).__name__ == "HipExecutor"
+        np.testing.assert_array_equal(_flat(m), _flat(m2))
+        for a, b in zip(m._executor.optimizer_state(), m2._executor.optimizer_state()):
+            assert bool((a == b).all())
+        assert m.evaluate(x, y, verbose=0) == m2.evaluate(x, y, verbose=0)
+        m2._executor.seed = m._executor.seed
+        m.train_on_batch(x[:64], y[:64])
+        m2.train_on_batch(x[:64], y[:64])
+        np.testing.assert_allclose(_flat(m), _flat(m2), rtol=0, atol=1e-6)
+
+
+def test_train_rpv_cli_gpu():
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("INTML_DEVICE", None)
+    r = subprocess.run([sys.executable, "-m", "cori_intml_examples_amd.apps.train_rpv", "--n-train", "4096",
+                        "--n-valid", "1024", "--n-epochs", "2", "--batch-size", "128", "--fom", "best",
+                        "--channels", "3"], env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "FoM:" in r.stdout and "Total params: 547,841" not in r.stdout   # 3-channel first conv
+    assert "Total params: 548,129" in r.stdout
+
+
+def _gpu_trial(n):
+    import torch
+    from cori_intml_examples_amd.apps.mlextras import IPyParallelLogger
+    from cori_intml_examples_amd.apps.zoo import rpv_cnn
+    from cori_intml_examples_amd.io.datasets import synthetic_rpv
+    x, y, _ = synthetic_rpv(n, channels=3, seed=2)
+    m = rpv_cnn((64, 64, 3), [16, 32, 64], [128], dropout=0.2)
+    h = m.fit(x, y, batch_size=128, epochs=2, validation_split=0.25, verbose=0, callbacks=[IPyParallelLogger()])
+    return {"device": str(m.device), "executor": type(m._executor).__name__, "hist": h.history,
+            "visible": os.environ.get("HIP_VISIBLE_DEVICES"), "gpus": torch.cuda.device_count()}
+
+
+def test_farm_engine_on_gpu():
+    import cloudpickle
+    cloudpickle.register_pickle_by_value(sys.modules[__name__])
+    from cori_intml_examples_amd import farm
+    cl = farm.start_cluster(1, cluster_id="gpu_pytest_%d" % os.getpid(), gpus=[0], timeout=300)
+    try:
+        with cl.client() as c:
+            ar = c.load_balanced_view().apply(_gpu_trial, 1024)
+            out = ar.get(600)
+            assert out["executor"] == "HipExecutor" and out["device"].startswith("cuda")
+            assert out["visible"] == "0" and out["gpus"] == 1
+            assert len(out["hist"]["val_loss"]) == 2
+            assert ar.data["status"] == "Ended Training"
+    finally:
+        cl.stop()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_hip_data_parallel_two_ranks(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT, INTML_DP_BACKEND="gloo")
+    env.pop("INTML_DEVICE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dp_worker_gpu.py"), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    reps = [json.load(open(tmp_path / ("rank%d.json" % i))) for i in range(2)]
+    assert reps[0]["w1"] == reps[1]["w1"] and reps[0]["wf"] == reps[1]["wf"]       # lockstep
+    assert reps[0]["val_loss"] == reps[1]["val_loss"]
+    assert reps[0]["rel_diff"] < 0.05, reps[0]["rel_diff"]      # bf16 half-batches vs one global batch
