@@ -390,8 +390,7 @@ class BatchPlan:
         K = ex.K
         dev = ex.device
         self.graph = None
-        self.graph_pre = None
-        self.graph_post = None
+        self.dp_graphs = None
         z = lambda *s, dt=BF16: torch.zeros(*s, dtype=dt, device=dev)
         self.xb = z(bs, ex.in_H * ex.in_W * ex.in_Cs)
         self.yb = z(bs, ex.plan.head.N, dt=torch.float32)
@@ -565,6 +564,7 @@ class BatchPlan:
 
         # ---------------- backward
         self.red_groups = []       # (lo, hi, [desc tuples]) in backward order
+        self.red_ready = []        # launch count after which each group's partial slabs are final
         hw = store.spec(hd.dense, "kernel")
         descs = [(self.head_wslab.data_ptr(), hd.K * hd.N, self.head_blocks, hd.N, hw.offset, hw.numel,
                   RED_BIAS, 0, 0, 0, 0, 0)]
@@ -575,6 +575,7 @@ class BatchPlan:
                           RED_BIAS, 0, 0, 0, 0, 0))
             hi = max(hi, hb.offset + hb.numel)
         self.red_groups.append((lo, hi, descs))
+        self.red_ready.append(len(self.launches))
         self.wgrad_slabs = []
 
         for g, ds in reversed(list(zip(ex.denses, ex.plan.denses))):
@@ -592,6 +593,7 @@ class BatchPlan:
                 descs.append((bslab.data_ptr(), ld, S, ld, bp_.offset, bp_.numel, RED_BIAS, 0, 0, 0, 0, 0))
                 hi = max(hi, bp_.offset + bp_.numel)
             self.red_groups.append((lo, hi, descs))
+            self.red_ready.append(len(self.launches))
             if g.KSb:
                 a = K.DenseFwdArgs()
                 a.x = self.dense_dh[g.j].data_ptr()
@@ -619,6 +621,7 @@ class BatchPlan:
                 descs.append((bslab.data_ptr(), ld, S, ld, bp_.offset, bp_.numel, RED_BIAS, 0, 0, 0, 0, 0))
                 hi = max(hi, bp_.offset + bp_.numel)
             self.red_groups.append((lo, hi, descs))
+            self.red_ready.append(len(self.launches))
             if g.i > 0:
                 prev = ex.convs[g.i - 1]
                 a = K.ConvMMArgs()
@@ -749,7 +752,8 @@ class BatchPlan:
         return a, (ktw, ntt, S), slab, bslab
 
     def _build_reduce(self):
-        """Group per-layer slab reductions into data-parallel buckets (backward order)."""
+        """Group per-layer slab reductions into data-parallel buckets (backward order) and
+        record, per bucket, the launch after which all its partial slabs are final."""
         ex, K = self.ex, self.ex.K
         groups = [(lo, hi) for lo, hi, _ in self.red_groups]
         reducer = ex.reducer
@@ -758,6 +762,7 @@ class BatchPlan:
         else:
             bucket_groups = [list(range(len(groups)))]
         self.bucket_tables = []
+        self.bucket_ready = []
         for bg in bucket_groups:
             tab = K.RedTable()
             lo = min(self.red_groups[i][0] for i in bg)
@@ -766,11 +771,12 @@ class BatchPlan:
                 for d in self.red_groups[i][2]:
                     tab.add(*d)
             self.bucket_tables.append((lo, hi, tab))
+            self.bucket_ready.append(max(self.red_ready[i] for i in bg))
 
     # ---------------------------------------------------------------- execution
-    def _run_seq(self, names_filter=None):
+    def _run_seq(self, lo: int = 0, hi: Optional[int] = None):
         s = torch.cuda.current_stream().cuda_stream
-        for name, fn in self.launches:
+        for name, fn in self.launches[lo:hi]:
             fn(s)
 
     def _launch_reduce(self, i):
@@ -790,36 +796,55 @@ class BatchPlan:
             if with_optim:
                 self._launch_optim()
 
+    def _dp_segments(self):
+        """[(launch_lo, launch_hi, bucket)]: segment k ends where bucket k's gradients are
+        final and finishes with that bucket's slab reduction; a trailing (lo, hi, None)
+        segment holds the launches after the last bucket (none for a CNN: conv0 has no dgrad)."""
+        segs, lo = [], 0
+        for k, ready in enumerate(self.bucket_ready):
+            segs.append((lo, ready, k))
+            lo = ready
+        if lo < len(self.launches):
+            segs.append((lo, len(self.launches), None))
+        return segs
+
+    def _run_segment(self, lo, hi, k):
+        self._run_seq(lo, hi)
+        if k is not None:
+            self._launch_reduce(k)
+
     def run(self):
         ex = self.ex
         dp = self.training and ex.reducer is not None and ex.reducer.size > 1
-        if dp:
-            ex.grad_scale = 1.0 / ex.reducer.size
-        if not ex.use_graphs:
-            self._body(with_optim=not dp)
-            if dp:
-                self._dp_tail()
+        if not dp:
+            if not ex.use_graphs:
+                self._body(with_optim=True)
+                return
+            if self.graph is None:
+                self.graph = self._capture(lambda: self._body(with_optim=True))
+            self.graph.replay()
             return
-        if dp:
-            if self.graph_pre is None:
-                self.graph_pre = self._capture(lambda: self._body(with_optim=False))
-                self.graph_post = self._capture(self._launch_optim)
-            self.graph_pre.replay()
-            for i in range(len(self.bucket_tables)):
-                ex.reducer.start(i, ex.store.grad)
-            ex.reducer.finish()
-            self.graph_post.replay()
-            return
-        if self.graph is None:
-            self.graph = self._capture(lambda: self._body(with_optim=True))
-        self.graph.replay()
-
-    def _dp_tail(self):
-        ex = self.ex
-        for i in range(len(self.bucket_tables)):
-            ex.reducer.start(i, ex.store.grad)
+        # Data parallel: each bucket's all-reduce is issued as soon as its slab reduction
+        # is done, so RCCL moves the dense bucket over xGMI while the conv backward runs;
+        # the fused optimizer (with the 1/size average folded in) runs after the last wait.
+        ex.grad_scale = 1.0 / ex.reducer.size
+        segs = self._dp_segments()
+        if ex.use_graphs and self.dp_graphs is None:
+            self.dp_graphs = [self._capture(lambda a=lo, b=hi, k=k: self._run_segment(a, b, k))
+                              for lo, hi, k in segs]
+            self.dp_graphs.append(self._capture(self._launch_optim))
+        for j, (lo, hi, k) in enumerate(segs):
+            if ex.use_graphs:
+                self.dp_graphs[j].replay()
+            else:
+                self._run_segment(lo, hi, k)
+            if k is not None:
+                ex.reducer.start(k, ex.store.grad)
         ex.reducer.finish()
-        self._launch_optim()
+        if ex.use_graphs:
+            self.dp_graphs[-1].replay()
+        else:
+            self._launch_optim()
 
     def _capture(self, fn):
         g = torch.cuda.CUDAGraph()

@@ -42,7 +42,7 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
     env_shard = os.environ.get("INTML_DP_SHARD")
     if shard_data is None:
         shard_data = True if env_shard is None else env_shard not in ("0", "false", "False")
-    bucket_bytes = bucket_bytes or int(os.environ.get("INTML_BUCKET_BYTES", 4 << 20))
+    bucket_bytes = bucket_bytes or int(os.environ.get("INTML_BUCKET_BYTES", 1 << 20))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
