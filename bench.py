@@ -22,6 +22,7 @@ import sys
 import time
 
 BASELINE_IMG_PER_S = 1240.0   # RPV single-GPU reference, Train_rpv.ipynb:304-312
+BASELINE_MNIST_IMG_PER_S = 43600.0   # MNIST DP aggregate, 8 Haswell nodes, DistTrain_mnist.ipynb:341-357
 
 
 def main():
@@ -57,14 +58,17 @@ def main():
                             optimizer="Adam", lr=0.001 * size, use_horovod=size > 1, device=dev)
         shape, ncls = (64, 64, args.channels), 1
         cfg_name = "RPV CNN conv[16,32,64] fc[128] 64x64x%d (DistTrain_rpv)" % args.channels
+        metric, baseline = "images/sec (whole node) RPV CNN training", BASELINE_IMG_PER_S
     elif args.model == "mnist":
         model = zoo.mnist_cnn(32, 64, 128, 0.25, 0.5, lr=1.0 * size, use_horovod=size > 1, device=dev)
         shape, ncls = (28, 28, 1), 10
         cfg_name = "MNIST CNN 32-64-128 (DistTrain_mnist)"
+        metric, baseline = "images/sec (whole node) MNIST CNN training", BASELINE_MNIST_IMG_PER_S
     else:
         model = zoo.rpv_legacy_cnn((64, 64, args.channels), device=dev, use_horovod=size > 1)
         shape, ncls = (64, 64, args.channels), 1
         cfg_name = "RPV legacy CNN 34.5M (Train_rpv)"
+        metric, baseline = "images/sec (whole node) RPV legacy CNN training", BASELINE_IMG_PER_S
 
     ex = model._executor
     # synthetic, device-resident dataset (no network / files here)
@@ -109,13 +113,14 @@ def main():
     ms = elapsed / args.steps * 1e3
     value = size * B * args.steps / elapsed
     if rank == 0:
-        out = {"metric": "images/sec (whole node) RPV CNN training",
+        out = {"metric": metric,
                "value": round(value, 1), "unit": "images/s", "n_gpus": size, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": round(value / BASELINE_IMG_PER_S, 2),
+               "scaling": "weak", "vs_baseline": round(value / baseline, 2),
                "dtype": "bf16", "data": "synthetic (device-resident, random-init weights)",
                "config": {"model": cfg_name, "global_batch": B * size, "per_gpu_batch": B,
-                          "seq_len": None, "input": list(shape), "optimizer": "Adam",
+                          "seq_len": None, "input": list(shape),
+                          "optimizer": type(getattr(model.optimizer, "_base_optimizer", model.optimizer)).__name__,
                           "parallelism": "dp%d" % size, "train_loss": round(loss, 5)}}
         print(json.dumps(out), flush=True)
     hvd.shutdown()

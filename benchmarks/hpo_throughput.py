@@ -1,0 +1,90 @@
+#!/usr/bin/env python
+"""HPO throughput benchmark: RPV trials per hour on one MI355X node (BASELINE.json
+"HPO trials/hour"; reference: 128 genetic-search evaluations of train_rpv -- 4 epochs,
+64k train / 32k valid, batch 64 -- in 3h06m36s on 32 Cori nodes = 41.2 evals/hour,
+``CrayHPO_rpv.ipynb:181,1282``).
+
+Trials come from the DistHPO_rpv random-search space (``DistHPO_rpv.ipynb:91-106``),
+each trains on one GPU (farm engine pinned per GPU), all GPUs busy concurrently.  The
+synthetic dataset is generated once per engine and kept resident (device-side).  Wall
+time covers farm start-up, every trial's model build / graph capture / training /
+validation, and result collection.  Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+REF_EVALS_PER_HOUR = 128 / (3 * 3600 + 6 * 60 + 36) * 3600     # 41.2
+
+
+_CACHE = {}
+
+
+def trial(conv_sizes, fc_sizes, lr, dropout, optimizer, n_train=64000, n_valid=32000, batch_size=64,
+          n_epochs=4, channels=1):
+    import time as _t
+    t0 = _t.time()
+    from cori_intml_examples_amd.apps.rpv import build_model, train_model
+    from cori_intml_examples_amd.io.datasets import synthetic_rpv
+    key = (n_train, n_valid, channels)
+    if key not in _CACHE:
+        tr = synthetic_rpv(n_train, channels=channels, seed=1)
+        va = synthetic_rpv(n_valid, channels=channels, seed=2)
+        _CACHE[key] = (tr, va)
+    (x, y, _), (xv, yv, _) = _CACHE[key]
+    t1 = _t.time()
+    model = build_model(x.shape[1:], conv_sizes=conv_sizes, fc_sizes=fc_sizes, dropout=dropout,
+                        optimizer=optimizer, lr=lr)
+    h = train_model(model, x, y, xv, yv, batch_size=batch_size, n_epochs=n_epochs, verbose=0)
+    return {"val_loss": h.history["val_loss"], "data_s": t1 - t0, "train_s": _t.time() - t1,
+            "device": str(model.device)}
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--trials", type=int, default=16)
+    ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--n-train", type=int, default=64000)
+    ap.add_argument("--n-valid", type=int, default=32000)
+    ap.add_argument("--batch-size", type=int, default=64)
+    ap.add_argument("--engines", type=int, default=None)
+    ap.add_argument("--cpu", action="store_true")
+    a = ap.parse_args()
+    import cloudpickle
+    cloudpickle.register_pickle_by_value(sys.modules[__name__])
+    from cori_intml_examples_amd import farm
+    from cori_intml_examples_amd.hpo import random_search as rs
+    t0 = time.time()
+    n_gpu = 0 if a.cpu else farm.detect_gpus()
+    cl = farm.start_cluster(a.engines or max(1, n_gpu), cluster_id="hpo_bench_%d" % os.getpid(),
+                            cpu_only=a.cpu or n_gpu == 0, timeout=300)
+    try:
+        with cl.client() as c:
+            t_up = time.time() - t0
+            trials = rs.rpv_trials(a.trials)
+            ars = rs.submit_trials(c.load_balanced_view(), trial, trials, n_train=a.n_train, n_valid=a.n_valid,
+                                   batch_size=a.batch_size, n_epochs=a.epochs)
+            rs.wait_progress(ars, interval=1.0, printer=lambda s: print(s, file=sys.stderr, flush=True))
+            res = rs.collect(ars)
+    finally:
+        cl.stop()
+    wall = time.time() - t0
+    ok = [r for r in res if r]
+    per_hour = len(ok) / wall * 3600
+    print(json.dumps({
+        "metric": "HPO trials/hour (RPV random search, %d epochs, %dk train / %dk valid, batch %d)"
+                  % (a.epochs, a.n_train // 1000, a.n_valid // 1000, a.batch_size),
+        "value": round(per_hour, 1), "unit": "trials/hour", "n_gpus": n_gpu, "engines": a.engines or max(1, n_gpu),
+        "trials": len(ok), "failed": len(res) - len(ok), "wall_s": round(wall, 2), "startup_s": round(t_up, 2),
+        "mean_train_s": round(sum(r["train_s"] for r in ok) / max(1, len(ok)), 3),
+        "vs_baseline": round(per_hour / REF_EVALS_PER_HOUR, 2), "baseline": "41.2 evals/hour (CrayHPO_rpv, 32 nodes)",
+        "data": "synthetic RPV (1-channel 64x64), resident per engine"}))
+
+
+if __name__ == "__main__":
+    main()
