@@ -11,6 +11,10 @@ namespace py = pybind11;
 
 void launch_conv_halo(const ConvMMArgs& a, int ntc, hipStream_t s);
 size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc);
+void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s);
+size_t conv_tile_lds_bytes(int ntc);
+void launch_wgrad_tile(const WgradArgs& a, int ntc, hipStream_t s);
+size_t wgrad_tile_lds_bytes(int ntc);
 void launch_wgrad_halo(const WgradArgs& a, int MT, int NTT, int splits, hipStream_t s);
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT);
 int head_rows_per_block();
@@ -23,6 +27,7 @@ void launch_step_begin(const StepBeginArgs& a, hipStream_t s);
 void launch_gather(const GatherArgs& a, hipStream_t s);
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s);
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s);
+void launch_pack(const float* master, bf16* arena, const PackTable& tab, hipStream_t s);
 
 static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -116,7 +121,15 @@ PYBIND11_MODULE(_kernels, m) {
         if (t.n >= MAX_PACK) throw std::runtime_error("PackTable full");
         PackDesc& d = t.d[t.n++];
         d.src_off = src_off; d.numel = numel; d.type = type; d.KH = KH; d.KW = KW; d.Cin = Cin;
-        d.Cout = Cout; d.Cs = Cs; d.NT = NT; d.pad_ = 0; d.dst_off = dst_off;
+        d.Cout = Cout; d.Cs = Cs; d.NT = NT; d.dst_off = dst_off;
+        long long krows;   // k extent of the pack
+        if (type == PACK_CONV_FWD || type == PACK_CONV_DGRAD) krows = (long long)KH * KW * Cs;
+        else if (type == PACK_DENSE_FWD) krows = (long long)KH * KW * Cs;
+        else krows = Cout;
+        d.KS = (int)((krows + 31) / 32);
+        d.nvec = d.KS * NT * 64;
+        d.blk0 = t.nblocks;
+        t.nblocks += (d.nvec + 255) / 256;
       });
 
   py::class_<RedTable>(m, "RedTable")
@@ -147,6 +160,12 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("conv_halo_lds_bytes", &conv_halo_lds_bytes);
   m.def("wgrad_halo_lds_bytes", &wgrad_halo_lds_bytes);
   m.def("head_rows_per_block", &head_rows_per_block);
+  m.def("conv_tile_lds_bytes", &conv_tile_lds_bytes);
+  m.def("conv_tile", [](const ConvMMArgs& a, int ntc, uintptr_t s) {
+    launch_conv_tile(a, ntc, S(s)); check_last("conv_tile"); });
+  m.def("wgrad_tile_lds_bytes", &wgrad_tile_lds_bytes);
+  m.def("wgrad_tile", [](const WgradArgs& a, int ntc, uintptr_t s) {
+    launch_wgrad_tile(a, ntc, S(s)); check_last("wgrad_tile"); });
   m.def("conv_halo", [](const ConvMMArgs& a, int ntc, uintptr_t s) {
     launch_conv_halo(a, ntc, S(s)); check_last("conv_halo"); });
   m.def("wgrad_halo", [](const WgradArgs& a, int MT, int NTT, int splits, uintptr_t s) {
@@ -161,4 +180,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("slab_reduce", [](uintptr_t grad, int lo, int hi, const RedTable& t, uintptr_t s) {
     launch_slab_reduce(reinterpret_cast<float*>(grad), lo, hi, t, S(s)); check_last("slab_reduce"); });
   m.def("optim", [](const OptimArgs& a, const PackTable& t, uintptr_t s) { launch_optim(a, t, S(s)); check_last("optim"); });
+  m.def("pack", [](uintptr_t master, uintptr_t arena, const PackTable& t, uintptr_t s) {
+    launch_pack(reinterpret_cast<const float*>(master), reinterpret_cast<bf16*>(arena), t, S(s)); check_last("pack"); });
 }

@@ -173,15 +173,18 @@ struct PackDesc {
   int KH, KW, Cin, Cout;  // conv dims; dense: KH=Hf, KW=Wf (flatten source), Cin=Cf, Cout=N
   int Cs;        // padded channel stride of the relevant activation (fwd: input; dgrad: output)
   int NT;        // n-tiles of the pack
-  int pad_;
+  int KS;        // 32-wide k-steps of the pack
   long long dst_off;  // element offset in the bf16 pack arena
+  int blk0;      // first workgroup of this descriptor in the pack launch
+  int nvec;      // 16-byte fragment vectors of the pack (KS * NT * 64)
 };
 
 #define MAX_PACK 24
 
 struct PackTable {
   int n;
-  int pad_[3];
+  int nblocks;   // workgroups of the pack launch (256 vectors each)
+  int pad_[2];
   PackDesc d[MAX_PACK];
 };
 

@@ -146,105 +146,131 @@ void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStr
 }
 
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void pack_scatter(const PackTable& tab, bf16* arena, int e, float w) {
-  for (int di = 0; di < tab.n; ++di) {
-    const PackDesc& d = tab.d[di];
-    const int le = e - d.src_off;
-    if (le < 0 || le >= d.numel) continue;
-    int k, n;
-    if (d.type == PACK_CONV_FWD || d.type == PACK_CONV_DGRAD) {
-      const int co = le % d.Cout;
-      const int t2 = le / d.Cout;
-      const int ci = t2 % d.Cin;
-      const int tap = t2 / d.Cin;
-      if (d.type == PACK_CONV_FWD) {
-        k = tap * d.Cs + ci;
-        n = co;
-      } else {
-        const int ky = tap / d.KW, kx = tap - (tap / d.KW) * d.KW;
-        const int tapf = (d.KH - 1 - ky) * d.KW + (d.KW - 1 - kx);
-        k = tapf * d.Cs + co;
-        n = ci;
-      }
+// Weight packs: one launch over every (fp32 master tensor -> bf16 fragment-major pack)
+// descriptor.  A thread writes one 16-byte fragment vector -- 8 consecutive k of one n --
+// gathering its 8 sources from the Keras-layout master (the inverse of the pack layout
+// pack[((ks*NT+nt)*64+lane)*8+j] = B[32ks+8(lane>>4)+j][16nt+(lane&15)]).  Lanes of a
+// wave cover 16 consecutive n, so each gather instruction reads contiguous runs of the
+// row-major master.  Padding rows/columns become zeros.
+__device__ __forceinline__ float pack_src(const PackDesc& d, const float* w, int k, int n) {
+  int kk, nn;   // keras (row, col) of W[in][out] in the flattened master layout
+  if (d.type == PACK_CONV_FWD || d.type == PACK_CONV_DGRAD) {
+    const int KHW = d.KH * d.KW;
+    const int tap = k / d.Cs;
+    const int c = k - tap * d.Cs;
+    int ci, co, t;
+    if (d.type == PACK_CONV_FWD) { t = tap; ci = c; co = n; }
+    else { t = KHW - 1 - tap; co = c; ci = n; }
+    if (tap >= KHW || ci >= d.Cin || co >= d.Cout || t < 0) return 0.f;
+    return w[((size_t)t * d.Cin + ci) * d.Cout + co];
+  }
+  const int kp = d.type == PACK_DENSE_FWD ? k : n;     // padded flat index
+  nn = d.type == PACK_DENSE_FWD ? n : k;
+  const int pix = kp / d.Cs;
+  const int c = kp - pix * d.Cs;
+  if (c >= d.Cin || pix >= d.KH * d.KW || nn >= d.Cout) return 0.f;
+  kk = pix * d.Cin + c;
+  return w[(size_t)kk * d.Cout + nn];
+}
+
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ master, bf16* __restrict__ arena,
+                                                   const PackTable tab) {
+  int di = 0;
+  while (di + 1 < tab.n && (int)blockIdx.x >= tab.d[di + 1].blk0) ++di;
+  const PackDesc& d = tab.d[di];
+  const int v = ((int)blockIdx.x - d.blk0) * 256 + (int)threadIdx.x;
+  if (v >= d.nvec) return;
+  const int lane = v & 63;
+  const int frag = v >> 6;                 // ks * NT + nt
+  const int ks = frag / d.NT, nt = frag - ks * d.NT;
+  const int k0 = ks * 32 + 8 * (lane >> 4);
+  const int n = nt * 16 + (lane & 15);
+  const float* w = master + d.src_off;
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(pack_src(d, w, k0 + j, n));
+  *reinterpret_cast<bf16x8*>(arena + d.dst_off + (size_t)v * 8) = o;
+}
+
+void launch_pack(const float* master, bf16* arena, const PackTable& tab, hipStream_t s) {
+  if (tab.nblocks <= 0) return;
+  hipLaunchKernelGGL(pack_kernel, dim3(tab.nblocks), dim3(256), 0, s, master, arena, tab);
+}
+
+// ---------------------------------------------------------------------------------------
+// Multi-tensor optimizer update over the flat fp32 buffers, 4 elements per thread
+// (16-byte loads/stores; the buffers' capacity is a multiple of 64 elements).
+template <int KIND>
+__device__ __forceinline__ void opt_update(const OptimArgs& a, const StepState* st, float& p, float g, float* s0,
+                                           float* s1) {
+  if (KIND == OPT_ADAM) {
+    const float m = a.beta1 * *s0 + (1.f - a.beta1) * g;
+    const float v = a.beta2 * *s1 + (1.f - a.beta2) * g * g;
+    *s0 = m;
+    *s1 = v;
+    p -= st->s[0] * m / (sqrtf(v) + a.eps);
+  } else if (KIND == OPT_NADAM) {
+    const float mc_t = st->s[0], mc_t1 = st->s[1];
+    const float gp = g * st->s[2];
+    const float m = a.beta1 * *s0 + (1.f - a.beta1) * g;
+    const float v = a.beta2 * *s1 + (1.f - a.beta2) * g * g;
+    *s0 = m;
+    *s1 = v;
+    const float mp = m * st->s[3];
+    const float vp = v * st->s[4];
+    const float mbar = (1.f - mc_t) * gp + mc_t1 * mp;
+    p -= st->s[5] * mbar / (sqrtf(vp) + a.eps);
+  } else if (KIND == OPT_ADADELTA) {
+    const float acc = a.rho * *s0 + (1.f - a.rho) * g * g;
+    const float upd = g * sqrtf(*s1 + a.eps) / sqrtf(acc + a.eps);
+    *s0 = acc;
+    p -= st->s[0] * upd;
+    *s1 = a.rho * *s1 + (1.f - a.rho) * upd * upd;
+  } else if (KIND == OPT_RMSPROP) {
+    const float acc = a.rho * *s0 + (1.f - a.rho) * g * g;
+    *s0 = acc;
+    p -= st->s[0] * g / (sqrtf(acc) + a.eps);
+  } else {   // SGD (+momentum / nesterov)
+    const float lr = st->s[0];
+    if (a.momentum != 0.f) {
+      const float v = a.momentum * *s0 - lr * g;
+      *s0 = v;
+      p += a.nesterov ? (a.momentum * v - lr * g) : v;
     } else {
-      const int nn = le % d.Cout;
-      const int kk = le / d.Cout;
-      const int kp = flat_keras_to_padded(kk, d.Cin, d.Cs);
-      if (d.type == PACK_DENSE_FWD) {
-        k = kp;
-        n = nn;
-      } else {
-        k = nn;
-        n = kp;
-      }
+      p -= lr * g;
     }
-    const int ks = k >> 5, kr = k & 31;
-    const int lane = ((kr >> 3) << 4) | (n & 15);
-    const size_t dst = (size_t)d.dst_off + ((size_t)(ks * d.NT + (n >> 4)) * 64 + lane) * 8 + (kr & 7);
-    arena[dst] = f2bf(w);
   }
 }
 
-__global__ __launch_bounds__(256) void optim_kernel(const OptimArgs a, const PackTable tab) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
+template <int KIND>
+__global__ __launch_bounds__(256) void optim_kernel(const OptimArgs a) {
+  const int e = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (e >= a.n) return;
-  float p = a.p[e];
-  if (!a.pack_only) {
-    const float g = a.g[e] * a.grad_scale;
-    const StepState* st = a.st;
-    switch (a.kind) {
-      case OPT_ADAM: {
-        const float m = a.beta1 * a.s0[e] + (1.f - a.beta1) * g;
-        const float v = a.beta2 * a.s1[e] + (1.f - a.beta2) * g * g;
-        a.s0[e] = m;
-        a.s1[e] = v;
-        p -= st->s[0] * m / (sqrtf(v) + a.eps);
-        break;
-      }
-      case OPT_NADAM: {
-        const float mc_t = st->s[0], mc_t1 = st->s[1];
-        const float gp = g * st->s[2];
-        const float m = a.beta1 * a.s0[e] + (1.f - a.beta1) * g;
-        const float v = a.beta2 * a.s1[e] + (1.f - a.beta2) * g * g;
-        a.s0[e] = m;
-        a.s1[e] = v;
-        const float mp = m * st->s[3];
-        const float vp = v * st->s[4];
-        const float mbar = (1.f - mc_t) * gp + mc_t1 * mp;
-        p -= st->s[5] * mbar / (sqrtf(vp) + a.eps);
-        break;
-      }
-      case OPT_ADADELTA: {
-        const float acc = a.rho * a.s0[e] + (1.f - a.rho) * g * g;
-        const float upd = g * sqrtf(a.s1[e] + a.eps) / sqrtf(acc + a.eps);
-        a.s0[e] = acc;
-        p -= st->s[0] * upd;
-        a.s1[e] = a.rho * a.s1[e] + (1.f - a.rho) * upd * upd;
-        break;
-      }
-      case OPT_RMSPROP: {
-        const float acc = a.rho * a.s0[e] + (1.f - a.rho) * g * g;
-        a.s0[e] = acc;
-        p -= st->s[0] * g / (sqrtf(acc) + a.eps);
-        break;
-      }
-      default: {   // SGD (+momentum / nesterov)
-        const float lr = st->s[0];
-        if (a.momentum != 0.f) {
-          const float v = a.momentum * a.s0[e] - lr * g;
-          a.s0[e] = v;
-          p += a.nesterov ? (a.momentum * v - lr * g) : v;
-        } else {
-          p -= lr * g;
-        }
-      }
-    }
-    a.p[e] = p;
-  }
-  pack_scatter(tab, a.arena, e, p);
+  const StepState* st = a.st;
+  float4 p = *reinterpret_cast<const float4*>(a.p + e);
+  const float4 g = *reinterpret_cast<const float4*>(a.g + e);
+  float4 s0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : float4{0.f, 0.f, 0.f, 0.f};
+  float4 s1 = a.s1 ? *reinterpret_cast<const float4*>(a.s1 + e) : float4{0.f, 0.f, 0.f, 0.f};
+  const float gs = a.grad_scale;
+  opt_update<KIND>(a, st, p.x, g.x * gs, &s0.x, &s1.x);
+  opt_update<KIND>(a, st, p.y, g.y * gs, &s0.y, &s1.y);
+  opt_update<KIND>(a, st, p.z, g.z * gs, &s0.z, &s1.z);
+  opt_update<KIND>(a, st, p.w, g.w * gs, &s0.w, &s1.w);
+  *reinterpret_cast<float4*>(a.p + e) = p;
+  if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
+  if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
 }
 
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s) {
-  if (a.n <= 0) return;
-  hipLaunchKernelGGL(optim_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a, tab);
+  if (a.n > 0 && !a.pack_only) {
+    const dim3 grid((a.n / 4 + 255) / 256);
+    switch (a.kind) {
+      case OPT_ADAM: hipLaunchKernelGGL(optim_kernel<OPT_ADAM>, grid, dim3(256), 0, s, a); break;
+      case OPT_NADAM: hipLaunchKernelGGL(optim_kernel<OPT_NADAM>, grid, dim3(256), 0, s, a); break;
+      case OPT_ADADELTA: hipLaunchKernelGGL(optim_kernel<OPT_ADADELTA>, grid, dim3(256), 0, s, a); break;
+      case OPT_RMSPROP: hipLaunchKernelGGL(optim_kernel<OPT_RMSPROP>, grid, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL(optim_kernel<OPT_SGD>, grid, dim3(256), 0, s, a); break;
+    }
+  }
+  launch_pack(a.p, a.arena, tab, s);      // the MFMA kernels read the bf16 packs
 }

@@ -214,10 +214,10 @@ class HipExecutor(Executor):
         for g, ds in zip(self.denses, self.plan.denses):
             sp = st.spec(ds.dense, "kernel")
             g.pack_fwd = alloc(g.KS, g.NT)
-            tab.add(sp.offset, sp.numel, PACK_DENSE_FWD, 0, 0, g.src.C, g.N, g.src.Cs, g.NT, g.pack_fwd)
+            tab.add(sp.offset, sp.numel, PACK_DENSE_FWD, g.src.H, g.src.W, g.src.C, g.N, g.src.Cs, g.NT, g.pack_fwd)
             if g.KSb:
                 g.pack_bwd = alloc(g.KSb, g.NTb)
-                tab.add(sp.offset, sp.numel, PACK_DENSE_BWD, 0, 0, g.src.C, g.N, g.src.Cs, g.NTb, g.pack_bwd)
+                tab.add(sp.offset, sp.numel, PACK_DENSE_BWD, g.src.H, g.src.W, g.src.C, g.N, g.src.Cs, g.NTb, g.pack_bwd)
         self.pack_table = tab
         self.arena = torch.zeros(max(off, 8), dtype=BF16, device=self.device)
 
@@ -509,8 +509,7 @@ class BatchPlan:
                 a.drop_thr = keep_threshold(g.rate)
                 a.drop_scale = 1.0 / (1.0 - g.rate)
             a.seed, a.stream_id, a.st = ex.seed, g.stream, st_ptr
-            ntc = self._halo_cfg(a, g.NT, g.pool)
-            self.launches.append(("conv_fwd%d" % g.i, lambda s, a=a, n=ntc: K.conv_halo(a, n, s)))
+            self.launches.append(("conv_fwd%d" % g.i, self._conv_launch(a, g.NT, g.pool)))
             x_buf = self.conv_out[g.i]
 
         # ---------------- forward denses
@@ -580,13 +579,18 @@ class BatchPlan:
 
         for g, ds in reversed(list(zip(ex.denses, ex.plan.denses))):
             xin = self._src_buf(g.src)
-            wa, cfg, slab, bslab = self._wgrad_args(xin, 1, 1, g.src.width, 1, 1, 1, 1, 1, 0, 0,
-                                                    self.dense_dh[g.j], g.Ns, g.N, bs, ds.dense.use_bias)
-            self.launches.append(("wgrad_dense%d" % g.j, lambda s, a=wa, c=cfg: K.wgrad(a, c[0], c[1], c[2], s)))
             sp = store.spec(ds.dense, "kernel")
+            # Unpadded flatten source and N % 16 == 0: the single-split slab IS the Keras
+            # (in, out) layout, so the wgrad kernel writes the gradient buffer directly and
+            # the slab round trip disappears (the dense kernel is most of the model's bytes).
+            direct = (g.src.C == g.src.Cs and g.N % 16 == 0 and g.src.width % 16 == 0)
+            wa, cfg, slab, bslab = self._wgrad_args(
+                xin, 1, 1, g.src.width, 1, 1, 1, 1, 1, 0, 0, self.dense_dh[g.j], g.Ns, g.N, bs,
+                ds.dense.use_bias, direct=(store.grad.data_ptr() + 4 * sp.offset) if direct else None)
+            self.launches.append(("wgrad_dense%d" % g.j, lambda s, a=wa, c=cfg: K.wgrad(a, c[0], c[1], c[2], s)))
             S, ld = cfg[2], g.NT * 16
-            descs = [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel, RED_FLATW,
-                      0, 0, g.src.C, g.N, g.src.Cs)]
+            descs = [] if direct else [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel,
+                                        RED_FLATW, 0, 0, g.src.C, g.N, g.src.Cs)]
             lo, hi = sp.offset, sp.offset + sp.numel
             if ds.dense.use_bias:
                 bp_ = store.spec(ds.dense, "bias")
@@ -608,9 +612,13 @@ class BatchPlan:
 
         for g, cs in reversed(list(zip(ex.convs, ex.plan.convs))):
             xin = self.xb if g.i == 0 else self.conv_out[g.i - 1]
-            wa, cfg, slab, bslab = self._wgrad_halo_args(xin, g, bs, cs.conv.use_bias)
-            self.launches.append(("wgrad_conv%d" % g.i,
-                                  lambda s, a=wa, c=cfg: K.wgrad_halo(a, c[0], c[1], c[2], s)))
+            if self._wide(g.Cs_in, g.KS, g.NT):
+                wa, cfg, slab, bslab = self._wgrad_tile_args(xin, g, bs, cs.conv.use_bias)
+                self.launches.append(("wgrad_conv%d" % g.i, lambda s, a=wa, c=cfg: K.wgrad_tile(a, c[0], s)))
+            else:
+                wa, cfg, slab, bslab = self._wgrad_halo_args(xin, g, bs, cs.conv.use_bias)
+                self.launches.append(("wgrad_conv%d" % g.i,
+                                      lambda s, a=wa, c=cfg: K.wgrad_halo(a, c[0], c[1], c[2], s)))
             sp = store.spec(cs.conv, "kernel")
             S, ld = cfg[2], g.NT * 16
             descs = [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel, RED_CONVW,
@@ -639,9 +647,24 @@ class BatchPlan:
                 a.mode, a.flat_out = 1, 0
                 a.st = st_ptr
                 a.bt = self._bt_for(Src("conv", prev.i, prev.Cout, prev.Cs_out, prev.Hp, prev.Wp))
-                ntc = self._halo_cfg(a, g.NTd, False)
-                self.launches.append(("dgrad_conv%d" % g.i, lambda s, a=a, n=ntc: K.conv_halo(a, n, s)))
+                self.launches.append(("dgrad_conv%d" % g.i, self._conv_launch(a, g.NTd, False)))
         self._build_reduce()
+
+    @staticmethod
+    def _wide(Cs_in: int, KS: int, NT: int) -> bool:
+        """Wide layer: conv_halo would have to keep all of K's weights in LDS for fewer
+        n-tiles than a 128-channel tile needs -> use the tiled whole-batch GEMM kernels."""
+        return Cs_in % 32 == 0 and KS * min(NT, 8) > 64
+
+    def _conv_launch(self, a, NT, pool):
+        K = self.ex.K
+        if self._wide(a.Cs_in, a.KS, NT):
+            ntc = 8 if NT > 4 else (4 if NT > 2 else 2)
+            if K.conv_tile_lds_bytes(ntc) > 150 * 1024:
+                raise NotImplementedError("conv tile LDS")
+            return lambda s, a=a, n=ntc: K.conv_tile(a, n, s)
+        ntc = self._halo_cfg(a, NT, pool)
+        return lambda s, a=a, n=ntc: K.conv_halo(a, n, s)
 
     def _halo_cfg(self, a, NT, pool):
         """Pick n-tiles per workgroup (weight LDS slice) and R output rows per block."""
@@ -669,6 +692,36 @@ class BatchPlan:
         if lds > 150 * 1024:
             raise NotImplementedError("conv halo stage too large (%d bytes)" % lds)
         return ntc
+
+    def _wgrad_tile_args(self, xin, g, bs, bias):
+        """Tiled wgrad for wide convs: 128(k) x ntc*16(n) tiles, split-K over pixel ranges."""
+        K, dev = self.ex.K, self.ex.device
+        a = K.WgradArgs()
+        a.x = xin.data_ptr()
+        a.B, a.H, a.W, a.Cs_in = bs, g.H, g.W, g.Cs_in
+        a.Ho, a.Wo, a.KH, a.KW, a.stride, a.pad_t, a.pad_l = g.Ho, g.Wo, g.KH, g.KW, g.stride, g.pad_t, g.pad_l
+        a.Ktiles = cdiv(g.KH * g.KW * g.Cs_in, 16)
+        a.dy = self.conv_dy[g.i].data_ptr()
+        a.Cs_dy = g.Cs_out
+        if g.pool:
+            a.dy_code = self.conv_code[g.i].data_ptr()
+            a.dHp, a.dWp = g.Hp, g.Wp
+        a.NT = g.NT
+        ntc = 8 if g.NT > 4 else (4 if g.NT > 2 else 2)
+        ntc = min(ntc, int(os.environ.get("INTML_WGRAD_TILE_NTC", ntc)))
+        P = bs * g.Ho * g.Wo
+        a.P = P
+        tiles = cdiv(a.Ktiles * 16, 128) * cdiv(g.NT, ntc)
+        per_split_bytes = a.Ktiles * 16 * g.NT * 16 * 4
+        S = max(1, min(cdiv(1024, tiles), (64 << 20) // per_split_bytes, cdiv(P, 256)))
+        a.px_per_split = cdiv(cdiv(P, S), 64) * 64
+        S = cdiv(P, a.px_per_split)
+        slab = torch.zeros(S, a.Ktiles * 16, g.NT * 16, dtype=torch.float32, device=dev)
+        bslab = torch.zeros(S, g.NT * 16, dtype=torch.float32, device=dev) if bias else None
+        a.slab = slab.data_ptr()
+        a.bslab = bslab.data_ptr() if bslab is not None else 0
+        self.wgrad_slabs.append((slab, bslab))
+        return a, (ntc, None, S), slab, bslab
 
     def _wgrad_halo_args(self, xin, g, bs, bias):
         K, dev = self.ex.K, self.ex.device
@@ -714,7 +767,8 @@ class BatchPlan:
         self.wgrad_slabs.append((slab, bslab))
         return a, (MT, NTT, S), slab, bslab
 
-    def _wgrad_args(self, xin, H, W, Cs_in, Ho, Wo, KH, KW, stride, pad_t, pad_l, dy, Cs_dy, N, bs, bias):
+    def _wgrad_args(self, xin, H, W, Cs_in, Ho, Wo, KH, KW, stride, pad_t, pad_l, dy, Cs_dy, N, bs, bias,
+                    direct=None):
         K, dev = self.ex.K, self.ex.device
         a = K.WgradArgs()
         a.x = xin.data_ptr()
@@ -740,13 +794,13 @@ class BatchPlan:
         gz = cdiv(NT, ntt)
         per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
         s_budget = max(1, (4 << 20) // per_split_bytes)
-        S = max(1, min(512 // max(1, gy * gz), s_budget, cdiv(P, 32)))
+        S = 1 if direct else max(1, min(512 // max(1, gy * gz), s_budget, cdiv(P, 32)))
         pps = cdiv(cdiv(P, S), 32) * 32
         S = cdiv(P, pps)
         a.px_per_split = pps
-        slab = torch.zeros(S, a.Ktiles * 16, NT * 16, dtype=torch.float32, device=dev)
+        slab = None if direct else torch.zeros(S, a.Ktiles * 16, NT * 16, dtype=torch.float32, device=dev)
         bslab = torch.zeros(S, NT * 16, dtype=torch.float32, device=dev) if bias else None
-        a.slab = slab.data_ptr()
+        a.slab = direct if direct else slab.data_ptr()
         a.bslab = bslab.data_ptr() if bslab is not None else 0
         self.wgrad_slabs.append((slab, bslab))
         return a, (ktw, ntt, S), slab, bslab

@@ -61,7 +61,8 @@ def _full_dy(bp, g):
     return R.maxpool2x2_backward(dp, code, (g.Ho, g.Wo))
 
 
-CASES = [("rpv", 0.0, 1), ("rpv", 0.3, 3), ("mnist", 0.4, 1), ("odd", 0.25, 2), ("strided", 0.0, 3)]
+CASES = [("rpv", 0.0, 1), ("rpv", 0.3, 3), ("mnist", 0.4, 1), ("odd", 0.25, 2), ("strided", 0.0, 3),
+         ("wide", 0.2, 3), ("wide_strided", 0.0, 3)]
 
 
 @pytest.mark.parametrize("kind,drop,cin", CASES)

@@ -69,6 +69,31 @@ def _build(kind, device, opt="Adam", drop=0.0, cin=1, hw=16):
         m = Model(inp, out, device=device)
         m.compile(optimizer=opt, loss="binary_crossentropy", metrics=["accuracy"])
         return m
+    if kind == "wide":     # 64->128 pooled conv + its dgrad/wgrad take the tiled (wide) kernels
+        inp = Input(shape=(hw, hw, cin))
+        h = inp
+        for c in (32, 64, 128):
+            h = Conv2D(c, (3, 3), activation="relu", padding="same")(h)
+            h = MaxPooling2D((2, 2))(h)
+        h = Dropout(drop)(h)
+        h = Flatten()(h)
+        h = Dense(32, activation="relu")(h)
+        out = Dense(1, activation="sigmoid")(h)
+        m = Model(inp, out, device=device)
+        m.compile(optimizer=opt, loss="binary_crossentropy", metrics=["accuracy"])
+        return m
+    if kind == "wide_strided":     # legacy-RPV-like strided wide convs (input-dilated dgrad)
+        inp = Input(shape=(hw, hw, cin))
+        h = Conv2D(32, (3, 3), activation="relu", strides=1, padding="same")(inp)
+        h = Conv2D(64, (3, 3), activation="relu", strides=2, padding="same")(h)
+        h = Conv2D(64, (3, 3), activation="relu", strides=1, padding="same")(h)
+        h = Conv2D(96, (3, 3), activation="relu", strides=2, padding="same")(h)
+        h = Flatten()(h)
+        h = Dense(32, activation="relu")(h)
+        out = Dense(1, activation="sigmoid")(h)
+        m = Model(inp, out, device=device)
+        m.compile(optimizer=opt, loss="binary_crossentropy", metrics=["accuracy"])
+        return m
     raise ValueError(kind)
 
 
@@ -116,7 +141,7 @@ def _one_step(g, c, x, y):
 
 
 @pytest.mark.parametrize("kind,drop,cin", [("rpv", 0.0, 1), ("rpv", 0.3, 3), ("mnist", 0.0, 1),
-                                           ("mnist", 0.4, 1), ("odd", 0.25, 2), ("strided", 0.0, 3)])
+                                           ("mnist", 0.4, 1), ("odd", 0.25, 2), ("strided", 0.0, 3), ("wide", 0.2, 3), ("wide_strided", 0.0, 3)])
 def test_grads_match_reference(kind, drop, cin):
     g, c = _pair(kind, drop=drop, cin=cin)
     x, y = _data(g, 48)
