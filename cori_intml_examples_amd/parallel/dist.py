@@ -57,7 +57,11 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
         if use_gpu:
             torch.cuda.set_device(local_rank % torch.cuda.device_count())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        tdist.init_process_group(backend=be, rank=rank, world_size=world)
+        # a dead or hung rank turns into an error on every other rank after this timeout
+        # (failure detection) instead of a silent hang
+        import datetime
+        timeout = datetime.timedelta(seconds=float(os.environ.get("INTML_DP_TIMEOUT", 600)))
+        tdist.init_process_group(backend=be, rank=rank, world_size=world, timeout=timeout)
         owns = True
     else:
         be = backend or "none"

@@ -397,3 +397,12 @@ class ParamSpanModel:
     def snapshot(self):
         with self.lock:
             return copy.deepcopy(self.table)
+
+    @property
+    def results(self) -> List[Any]:
+        """The trials' AsyncResults by row (running, completed or stopped) -- what the
+        reference's analysis cells expect as ``psw.model_runs`` (``DistWidgetHPO_mnist.ipynb:
+        269-280``, which referenced a missing attribute)."""
+        return [self.controller.future(i) for i in range(self.n_models)]
+
+    model_runs = results

@@ -218,3 +218,26 @@ def test_cpu_plumbing_config_mnist_learns():
     m = zoo.mnist_cnn(8, 16, 32, dropout=0.25, optimizer="Adadelta", device="cpu")
     h = m.fit(x, y, batch_size=128, epochs=2, validation_data=(xt, yt), verbose=0)
     assert h.history["val_acc"][-1] > 0.5
+
+
+def test_profiling_hooks_and_resume(tmp_path):
+    from cori_intml_examples_amd.models import load_model
+    from cori_intml_examples_amd.utils.profiling import StepTimer, ThroughputLogger, trace
+    x, y, _ = synthetic_rpv(64, size=16, seed=1)
+    m = zoo.rpv_cnn((16, 16, 1), [4, 4, 4], [8], device="cpu")
+    tl = ThroughputLogger()
+    with trace(str(tmp_path / "t.json")):
+        h = m.fit(x, y, batch_size=16, epochs=2, verbose=0, callbacks=[tl])
+    assert (tmp_path / "t.json").exists()
+    assert h.history["img_per_sec"][0] > 0 and len(tl.history) == 2
+    assert h.history["img_per_sec_node"] == h.history["img_per_sec"]      # single process
+    timer = StepTimer()
+    with timer.region("eval"):
+        m.evaluate(x, y, verbose=0)
+    assert timer.summary()["eval"]["calls"] == 1
+    # checkpoint / resume: reload and continue from epoch 2 (Keras initial_epoch)
+    p = str(tmp_path / "ck.h5")
+    m.save(p)
+    m2 = load_model(p)
+    h2 = m2.fit(x, y, batch_size=16, epochs=3, initial_epoch=2, verbose=0)
+    assert h2.epoch == [2] and m2.optimizer.iterations == m.optimizer.iterations + 4
