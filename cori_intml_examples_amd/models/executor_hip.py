@@ -391,6 +391,7 @@ class BatchPlan:
         dev = ex.device
         self.graph = None
         self.dp_graphs = None
+        self.side = torch.cuda.Stream(device=dev) if env_flag("INTML_TWO_STREAMS", True) else None
         z = lambda *s, dt=BF16: torch.zeros(*s, dtype=dt, device=dev)
         self.xb = z(bs, ex.in_H * ex.in_W * ex.in_Cs)
         self.yb = z(bs, ex.plan.head.N, dt=torch.float32)
@@ -574,7 +575,7 @@ class BatchPlan:
                           RED_BIAS, 0, 0, 0, 0, 0))
             hi = max(hi, hb.offset + hb.numel)
         self.red_groups.append((lo, hi, descs))
-        self.red_ready.append(len(self.launches))
+        self._add_group_reduce()
         self.wgrad_slabs = []
 
         for g, ds in reversed(list(zip(ex.denses, ex.plan.denses))):
@@ -587,7 +588,8 @@ class BatchPlan:
             wa, cfg, slab, bslab = self._wgrad_args(
                 xin, 1, 1, g.src.width, 1, 1, 1, 1, 1, 0, 0, self.dense_dh[g.j], g.Ns, g.N, bs,
                 ds.dense.use_bias, direct=(store.grad.data_ptr() + 4 * sp.offset) if direct else None)
-            self.launches.append(("wgrad_dense%d" % g.j, lambda s, a=wa, c=cfg: K.wgrad(a, c[0], c[1], c[2], s)))
+            self.launches.append(("wgrad_dense%d" % g.j, lambda s, a=wa, c=cfg: K.wgrad(a, c[0], c[1], c[2], s),
+                                  "side"))
             S, ld = cfg[2], g.NT * 16
             descs = [] if direct else [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel,
                                         RED_FLATW, 0, 0, g.src.C, g.N, g.src.Cs)]
@@ -597,7 +599,7 @@ class BatchPlan:
                 descs.append((bslab.data_ptr(), ld, S, ld, bp_.offset, bp_.numel, RED_BIAS, 0, 0, 0, 0, 0))
                 hi = max(hi, bp_.offset + bp_.numel)
             self.red_groups.append((lo, hi, descs))
-            self.red_ready.append(len(self.launches))
+            self._add_group_reduce()
             if g.KSb:
                 a = K.DenseFwdArgs()
                 a.x = self.dense_dh[g.j].data_ptr()
@@ -614,11 +616,12 @@ class BatchPlan:
             xin = self.xb if g.i == 0 else self.conv_out[g.i - 1]
             if self._wide(g.Cs_in, g.KS, g.NT):
                 wa, cfg, slab, bslab = self._wgrad_tile_args(xin, g, bs, cs.conv.use_bias)
-                self.launches.append(("wgrad_conv%d" % g.i, lambda s, a=wa, c=cfg: K.wgrad_tile(a, c[0], s)))
+                self.launches.append(("wgrad_conv%d" % g.i, lambda s, a=wa, c=cfg: K.wgrad_tile(a, c[0], s),
+                                      "side"))
             else:
                 wa, cfg, slab, bslab = self._wgrad_halo_args(xin, g, bs, cs.conv.use_bias)
                 self.launches.append(("wgrad_conv%d" % g.i,
-                                      lambda s, a=wa, c=cfg: K.wgrad_halo(a, c[0], c[1], c[2], s)))
+                                      lambda s, a=wa, c=cfg: K.wgrad_halo(a, c[0], c[1], c[2], s), "side"))
             sp = store.spec(cs.conv, "kernel")
             S, ld = cfg[2], g.NT * 16
             descs = [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel, RED_CONVW,
@@ -629,7 +632,7 @@ class BatchPlan:
                 descs.append((bslab.data_ptr(), ld, S, ld, bp_.offset, bp_.numel, RED_BIAS, 0, 0, 0, 0, 0))
                 hi = max(hi, bp_.offset + bp_.numel)
             self.red_groups.append((lo, hi, descs))
-            self.red_ready.append(len(self.launches))
+            self._add_group_reduce()
             if g.i > 0:
                 prev = ex.convs[g.i - 1]
                 a = K.ConvMMArgs()
@@ -805,38 +808,57 @@ class BatchPlan:
         self.wgrad_slabs.append((slab, bslab))
         return a, (ktw, ntt, S), slab, bslab
 
+    def _add_group_reduce(self):
+        """Slab reduction of the group just appended, on the side stream right after its
+        wgrad (it overlaps the main stream's dgrad chain)."""
+        gi = len(self.red_groups) - 1
+        self.launches.append(("reduce_g%d" % gi, lambda s, gi=gi: self._launch_group_reduce(gi, s), "side"))
+        self._add_group_reduce()
+
     def _build_reduce(self):
-        """Group per-layer slab reductions into data-parallel buckets (backward order) and
-        record, per bucket, the launch after which all its partial slabs are final."""
+        """One slab-reduction table per layer group (launched on the side stream right after
+        the group's wgrad); DP buckets merge consecutive groups in backward order and are
+        ready once their last group's reduction has run."""
         ex, K = self.ex, self.ex.K
         groups = [(lo, hi) for lo, hi, _ in self.red_groups]
+        self.group_tables = []
+        for lo, hi, descs in self.red_groups:
+            tab = K.RedTable()
+            for d in descs:
+                tab.add(*d)
+            self.group_tables.append((lo, hi, tab))
         reducer = ex.reducer
         if reducer is not None:
             bucket_groups = reducer.configure(groups)
         else:
             bucket_groups = [list(range(len(groups)))]
-        self.bucket_tables = []
-        self.bucket_ready = []
-        for bg in bucket_groups:
-            tab = K.RedTable()
-            lo = min(self.red_groups[i][0] for i in bg)
-            hi = max(self.red_groups[i][1] for i in bg)
-            for i in bg:
-                for d in self.red_groups[i][2]:
-                    tab.add(*d)
-            self.bucket_tables.append((lo, hi, tab))
-            self.bucket_ready.append(max(self.red_ready[i] for i in bg))
+        self.bucket_ready = [max(self.red_ready[i] for i in bg) for bg in bucket_groups]
 
     # ---------------------------------------------------------------- execution
     def _run_seq(self, lo: int = 0, hi: Optional[int] = None):
-        s = torch.cuda.current_stream().cuda_stream
-        for name, fn in self.launches[lo:hi]:
-            fn(s)
+        """Launch [lo, hi): 'main' launches in order on the current stream; 'side' launches
+        (weight gradients, slab reductions) on the side stream, each after the latest main
+        launch before it -- the two chains run concurrently and join at the end."""
+        main = torch.cuda.current_stream()
+        side_used = False
+        main_moved = True
+        for item in self.launches[lo:hi]:
+            name, fn = item[0], item[1]
+            if len(item) > 2 and item[2] == "side" and self.side is not None:
+                if main_moved:
+                    self.side.wait_stream(main)
+                    main_moved = False
+                fn(self.side.cuda_stream)
+                side_used = True
+            else:
+                fn(main.cuda_stream)
+                main_moved = True
+        if side_used:
+            main.wait_stream(self.side)
 
-    def _launch_reduce(self, i):
-        lo, hi, tab = self.bucket_tables[i]
-        self.ex.K.slab_reduce(self.ex.store.grad.data_ptr(), lo, hi, tab,
-                              torch.cuda.current_stream().cuda_stream)
+    def _launch_group_reduce(self, gi, s):
+        lo, hi, tab = self.group_tables[gi]
+        self.ex.K.slab_reduce(self.ex.store.grad.data_ptr(), lo, hi, tab, s)
 
     def _launch_optim(self):
         ex = self.ex
@@ -844,16 +866,12 @@ class BatchPlan:
 
     def _body(self, with_optim: bool):
         self._run_seq()
-        if self.training:
-            for i in range(len(self.bucket_tables)):
-                self._launch_reduce(i)
-            if with_optim:
-                self._launch_optim()
+        if self.training and with_optim:
+            self._launch_optim()
 
     def _dp_segments(self):
-        """[(launch_lo, launch_hi, bucket)]: segment k ends where bucket k's gradients are
-        final and finishes with that bucket's slab reduction; a trailing (lo, hi, None)
-        segment holds the launches after the last bucket (none for a CNN: conv0 has no dgrad)."""
+        """[(launch_lo, launch_hi, bucket)]: segment k ends with the slab reduction that
+        completes bucket k; a trailing (lo, hi, None) segment holds any later launches."""
         segs, lo = [], 0
         for k, ready in enumerate(self.bucket_ready):
             segs.append((lo, ready, k))
@@ -864,8 +882,6 @@ class BatchPlan:
 
     def _run_segment(self, lo, hi, k):
         self._run_seq(lo, hi)
-        if k is not None:
-            self._launch_reduce(k)
 
     def run(self):
         ex = self.ex

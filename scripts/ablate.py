@@ -47,7 +47,8 @@ def timeit(fn, reps=50):
 
 total = 0.0
 print("%-16s %9s | ablations (us): stage-off  mfma-off  store-off  all-off" % ("launch", "us"))
-for name, fn in bp.launches:
+for item in bp.launches:
+    name, fn = item[0], item[1]
     t = timeit(fn)
     total += t
     line = "%-16s %9.2f" % (name, t)
@@ -60,10 +61,6 @@ for name, fn in bp.launches:
         args.dbg = 0
         line += " | " + "  ".join("%9.2f" % v for v in res)
     print(line, flush=True)
-for i in range(len(bp.bucket_tables)):
-    t = timeit(lambda st, i=i: bp._launch_reduce(i))
-    total += t
-    print("%-16s %9.2f" % ("slab_reduce%d" % i, t))
 K = ex.K
 for gi, (lo, hi, descs) in enumerate(bp.red_groups):
     for d in descs:
