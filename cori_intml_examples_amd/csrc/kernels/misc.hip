@@ -152,27 +152,6 @@ void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStr
 // pack[((ks*NT+nt)*64+lane)*8+j] = B[32ks+8(lane>>4)+j][16nt+(lane&15)]).  Lanes of a
 // wave cover 16 consecutive n, so each gather instruction reads contiguous runs of the
 // row-major master.  Padding rows/columns become zeros.
-__device__ __forceinline__ float pack_src(const PackDesc& d, const float* w, int k, int n) {
-  int kk, nn;   // keras (row, col) of W[in][out] in the flattened master layout
-  if (d.type == PACK_CONV_FWD || d.type == PACK_CONV_DGRAD) {
-    const int KHW = d.KH * d.KW;
-    const int tap = k / d.Cs;
-    const int c = k - tap * d.Cs;
-    int ci, co, t;
-    if (d.type == PACK_CONV_FWD) { t = tap; ci = c; co = n; }
-    else { t = KHW - 1 - tap; co = c; ci = n; }
-    if (tap >= KHW || ci >= d.Cin || co >= d.Cout || t < 0) return 0.f;
-    return w[((size_t)t * d.Cin + ci) * d.Cout + co];
-  }
-  const int kp = d.type == PACK_DENSE_FWD ? k : n;     // padded flat index
-  nn = d.type == PACK_DENSE_FWD ? n : k;
-  const int pix = kp / d.Cs;
-  const int c = kp - pix * d.Cs;
-  if (c >= d.Cin || pix >= d.KH * d.KW || nn >= d.Cout) return 0.f;
-  kk = pix * d.Cin + c;
-  return w[(size_t)kk * d.Cout + nn];
-}
-
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ master, bf16* __restrict__ arena,
                                                    const PackTable tab) {
   int di = 0;
@@ -186,9 +165,44 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ mas
   const int k0 = ks * 32 + 8 * (lane >> 4);
   const int n = nt * 16 + (lane & 15);
   const float* w = master + d.src_off;
+  // The 8 k of this vector share one tap (conv) / pixel (dense) unless Cs == 4: split the
+  // index once, then step the channel -- no per-element divisions.  Loads are unconditional
+  // from a clamped address (select afterwards) so all 8 stay in flight.
+  const bool conv = d.type == PACK_CONV_FWD || d.type == PACK_CONV_DGRAD;
+  const int kp0 = conv || d.type == PACK_DENSE_FWD ? k0 : n;   // the index split by Cs
+  int outer = kp0 / d.Cs;
+  int c = kp0 - outer * d.Cs;
+  const int KHW = d.KH * d.KW;
+  float vals[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int cj = c, oj = outer;
+    if (conv || d.type == PACK_DENSE_FWD) {          // k varies with j
+      cj = c + j;
+      if (cj >= d.Cs) { cj -= d.Cs; ++oj; }          // only when Cs == 4
+    }
+    long long idx;
+    bool ok;
+    if (conv) {
+      const int t = d.type == PACK_CONV_FWD ? oj : KHW - 1 - oj;
+      const int ci = d.type == PACK_CONV_FWD ? cj : n;
+      const int co = d.type == PACK_CONV_FWD ? n : cj;
+      ok = oj < KHW && ci < d.Cin && co < d.Cout;
+      idx = ((long long)t * d.Cin + ci) * d.Cout + co;
+    } else if (d.type == PACK_DENSE_FWD) {
+      ok = cj < d.Cin && oj < KHW && n < d.Cout;
+      idx = (long long)(oj * d.Cin + cj) * d.Cout + n;
+    } else {                                          // PACK_DENSE_BWD: k = output unit
+      const int nn = k0 + j;
+      ok = c < d.Cin && outer < KHW && nn < d.Cout;
+      idx = (long long)(outer * d.Cin + c) * d.Cout + nn;
+    }
+    const float x = w[ok ? idx : 0];
+    vals[j] = ok ? x : 0.f;
+  }
   bf16x8 o;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = f2bf(pack_src(d, w, k0 + j, n));
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(vals[j]);
   *reinterpret_cast<bf16x8*>(arena + d.dst_off + (size_t)v * 8) = o;
 }
 
@@ -263,7 +277,7 @@ __global__ __launch_bounds__(256) void optim_kernel(const OptimArgs a) {
 
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s) {
   if (a.n > 0 && !a.pack_only) {
-    const dim3 grid((a.n / 4 + 255) / 256);
+    const dim3 grid(((a.n + 3) / 4 + 255) / 256);
     switch (a.kind) {
       case OPT_ADAM: hipLaunchKernelGGL(optim_kernel<OPT_ADAM>, grid, dim3(256), 0, s, a); break;
       case OPT_NADAM: hipLaunchKernelGGL(optim_kernel<OPT_NADAM>, grid, dim3(256), 0, s, a); break;

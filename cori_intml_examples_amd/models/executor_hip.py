@@ -391,7 +391,7 @@ class BatchPlan:
         dev = ex.device
         self.graph = None
         self.dp_graphs = None
-        self.side = torch.cuda.Stream(device=dev) if env_flag("INTML_TWO_STREAMS", True) else None
+        self.side = torch.cuda.Stream(device=dev) if env_flag("INTML_TWO_STREAMS", False) else None
         z = lambda *s, dt=BF16: torch.zeros(*s, dtype=dt, device=dev)
         self.xb = z(bs, ex.in_H * ex.in_W * ex.in_Cs)
         self.yb = z(bs, ex.plan.head.N, dt=torch.float32)
@@ -584,7 +584,8 @@ class BatchPlan:
             # Unpadded flatten source and N % 16 == 0: the single-split slab IS the Keras
             # (in, out) layout, so the wgrad kernel writes the gradient buffer directly and
             # the slab round trip disappears (the dense kernel is most of the model's bytes).
-            direct = (g.src.C == g.src.Cs and g.N % 16 == 0 and g.src.width % 16 == 0)
+            direct = (g.src.C == g.src.Cs and g.N % 16 == 0 and g.src.width % 16 == 0
+                      and g.src.width * g.N * 4 > (16 << 20))     # small layers keep split-K slabs
             wa, cfg, slab, bslab = self._wgrad_args(
                 xin, 1, 1, g.src.width, 1, 1, 1, 1, 1, 0, 0, self.dense_dh[g.j], g.Ns, g.N, bs,
                 ds.dense.use_bias, direct=(store.grad.data_ptr() + 4 * sp.offset) if direct else None)
@@ -809,30 +810,50 @@ class BatchPlan:
         return a, (ktw, ntt, S), slab, bslab
 
     def _add_group_reduce(self):
-        """Slab reduction of the group just appended, on the side stream right after its
-        wgrad (it overlaps the main stream's dgrad chain)."""
-        gi = len(self.red_groups) - 1
-        self.launches.append(("reduce_g%d" % gi, lambda s, gi=gi: self._launch_group_reduce(gi, s), "side"))
-        self._add_group_reduce()
+        """Record where the group just appended has its partial slabs final."""
+        self.red_ready.append(len(self.launches))
 
     def _build_reduce(self):
-        """One slab-reduction table per layer group (launched on the side stream right after
-        the group's wgrad); DP buckets merge consecutive groups in backward order and are
-        ready once their last group's reduction has run."""
+        """Merge per-layer slab groups (backward order) into buckets -- the DP reducer's
+        buckets, or the same 1 MiB bucketing without DP (dense layer first, then convs) --
+        and insert one reduction launch per bucket right after its last group's wgrad, on
+        the side stream, so the dense bucket's reduction overlaps the conv backward."""
         ex, K = self.ex, self.ex.K
         groups = [(lo, hi) for lo, hi, _ in self.red_groups]
-        self.group_tables = []
-        for lo, hi, descs in self.red_groups:
-            tab = K.RedTable()
-            for d in descs:
-                tab.add(*d)
-            self.group_tables.append((lo, hi, tab))
         reducer = ex.reducer
         if reducer is not None:
             bucket_groups = reducer.configure(groups)
         else:
-            bucket_groups = [list(range(len(groups)))]
-        self.bucket_ready = [max(self.red_ready[i] for i in bg) for bg in bucket_groups]
+            limit = int(os.environ.get("INTML_BUCKET_BYTES", 1 << 20))
+            bucket_groups, cur, nb = [], [], 0
+            for gi, (lo, hi) in enumerate(groups):
+                cur.append(gi)
+                nb += (hi - lo) * 4
+                if nb >= limit:
+                    bucket_groups.append(cur)
+                    cur, nb = [], 0
+            if cur:
+                bucket_groups.append(cur)
+        self.bucket_tables = []
+        inserts = []                       # (launch index to insert after, bucket)
+        for k, bg in enumerate(bucket_groups):
+            tab = K.RedTable()
+            for i in bg:
+                for d in self.red_groups[i][2]:
+                    tab.add(*d)
+            lo = min(self.red_groups[i][0] for i in bg)
+            hi = max(self.red_groups[i][1] for i in bg)
+            self.bucket_tables.append((lo, hi, tab))
+            inserts.append((max(self.red_ready[i] for i in bg), k))
+        launches, self.bucket_ready = [], [0] * len(bucket_groups)
+        pos = 0
+        for at, k in sorted(inserts):
+            launches.extend(self.launches[pos:at])
+            pos = at
+            launches.append(("reduce_b%d" % k, lambda s, k=k: self._launch_bucket_reduce(k, s), "side"))
+            self.bucket_ready[k] = len(launches)
+        launches.extend(self.launches[pos:])
+        self.launches = launches
 
     # ---------------------------------------------------------------- execution
     def _run_seq(self, lo: int = 0, hi: Optional[int] = None):
@@ -856,8 +877,8 @@ class BatchPlan:
         if side_used:
             main.wait_stream(self.side)
 
-    def _launch_group_reduce(self, gi, s):
-        lo, hi, tab = self.group_tables[gi]
+    def _launch_bucket_reduce(self, k, s):
+        lo, hi, tab = self.bucket_tables[k]
         self.ex.K.slab_reduce(self.ex.store.grad.data_ptr(), lo, hi, tab, s)
 
     def _launch_optim(self):
