@@ -143,7 +143,7 @@ PYBIND11_MODULE(_kernels, m) {
         d.dst_off = dst_off; d.numel = numel; d.type = type; d.KH = KH; d.KW = KW; d.Cin = Cin;
         d.Cout = Cout; d.Cs = Cs; d.pad_ = 0;
         // threads per element: enough lanes that each sums <= ~8 partials
-        d.tpe = S <= 4 ? 1 : S <= 32 ? 4 : S <= 256 ? 16 : 64;
+        d.tpe = S <= 4 ? 1 : S <= 32 ? 4 : S <= 512 ? 16 : 64;
         d.blk0 = t.nblocks;
         const int epb = 256 / d.tpe;
         t.nblocks += (numel + epb - 1) / epb;

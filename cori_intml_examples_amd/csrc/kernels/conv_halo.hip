@@ -117,7 +117,8 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvMMArgs a) {
 
   const FastDiv fwp(a.Wp > 0 ? a.Wp : 1), fwo(a.Wo);
   // per-wave epilogue scratch [16 rows][NTC*16] fp32, after the 16-B aligned halo image
-  float* ep = reinterpret_cast<float*>(xl + (((size_t)R_in * W_in * Cs + 7) & ~(size_t)7)) + wave * 16 * NTC * 16;
+  constexpr int EPW = (TM * 16 * 2 > 16 * 4 ? TM * 16 * 2 : 16 * 4) * NTC * 16 / 4;   // floats per wave
+  float* ep = reinterpret_cast<float*>(xl + (((size_t)R_in * W_in * Cs + 7) & ~(size_t)7)) + wave * EPW;
   const size_t qbase = ((size_t)b * a.Hp + (oy0 >> 1)) * a.Wp;
   for (int tb = wave * TM; tb < ntiles; tb += 4 * TM) {
     bool rv[TM];
@@ -184,27 +185,29 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvMMArgs a) {
       }
     }
 
+    if (!dbg_store) {
 #pragma unroll
-    for (int t = 0; t < TM; ++t) {
-      const int tile = tb + t;
-      if (tile >= ntiles) break;
-      if (!dbg_store) {
+      for (int t = 0; t < TM; ++t)
 #pragma unroll
         for (int nt = 0; nt < NTC; ++nt)
           asm volatile("" ::"v"(acc[t][nt][0]), "v"(acc[t][nt][1]), "v"(acc[t][nt][2]), "v"(acc[t][nt][3]));
-        continue;
-      }
-      // Epilogue through the wave's LDS scratch: lanes write their MFMA-layout results,
-      // then re-read them as 8-channel vectors so every global store is 16 bytes.
-      const int LDC = NTC * 16;
-      const int csh = (a.mode == 1 ? a.bt.pCs : a.Cs_out) - nt0 * 16;   // channels this WG owns
-      const int C = csh < LDC ? csh : LDC;
-      const int cch = C >> 3;                                            // 8-channel chunks
-      if (a.mode == 0 && a.pool) {
-        bf16* epb = reinterpret_cast<bf16*>(ep);                // [4 windows][LDC]
-        uint8_t* epc = reinterpret_cast<uint8_t*>(epb + 4 * LDC);
-        const int w = tile * 4 + g;
-        const size_t q = qbase + w;
+      continue;
+    }
+    // Epilogue through the wave's LDS scratch: lanes write their MFMA-layout results, then
+    // re-read them as 8-channel vectors so every global store is 16 bytes.  The forward
+    // epilogue stages all TM tiles of the pass first (final bf16 values + pool codes), so
+    // one copy loop writes TM*16 pixels / TM*4 windows with all lanes busy.
+    const int LDC = NTC * 16;
+    const int csh = (a.mode == 1 ? a.bt.pCs : a.Cs_out) - nt0 * 16;   // channels this WG owns
+    const int C = csh < LDC ? csh : LDC;
+    const int cch = C >> 3;                                            // 8-channel chunks
+    const FastDiv fcch(cch > 0 ? cch : 1);
+    if (a.mode == 0 && a.pool) {
+      bf16* epb = reinterpret_cast<bf16*>(ep);                // [TM*4 windows][LDC]
+      uint8_t* epc = reinterpret_cast<uint8_t*>(epb + TM * 4 * LDC);
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const size_t q = qbase + (tb + t) * 4 + g;
 #pragma unroll
         for (int nt = 0; nt < NTC; ++nt) {
           const int n = (nt0 + nt) * 16 + r;
@@ -223,19 +226,60 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvMMArgs a) {
               best = dropout_keep((uint32_t)(q * a.N + n), a.seed, a.stream_id, step, a.drop_thr) ? best * a.drop_scale
                                                                                                  : 0.f;
           }
-          epb[g * LDC + nt * 16 + r] = f2bf(best);
-          epc[g * LDC + nt * 16 + r] = (uint8_t)code;
+          epb[(t * 4 + g) * LDC + nt * 16 + r] = f2bf(best);
+          epc[(t * 4 + g) * LDC + nt * 16 + r] = (uint8_t)code;
         }
-        __builtin_amdgcn_wave_barrier();
-        const int nw = min(4, nwin - tile * 4);
-        for (int c = lane; c < nw * cch; c += 64) {
-          const int win = c / cch, c8 = c - win * cch;
-          const size_t o = (qbase + tile * 4 + win) * a.Cs_out + nt0 * 16 + c8 * 8;
-          *reinterpret_cast<uint4*>(a.out + o) = *reinterpret_cast<const uint4*>(epb + win * LDC + c8 * 8);
-          *reinterpret_cast<uint2*>(a.code + o) = *reinterpret_cast<const uint2*>(epc + win * LDC + c8 * 8);
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int nw = max(0, min(TM * 4, nwin - tb * 4));
+      for (int c = lane; c < nw * cch; c += 64) {
+        const int win = fcch.div(c), c8 = c - win * cch;
+        const size_t o = (qbase + tb * 4 + win) * a.Cs_out + nt0 * 16 + c8 * 8;
+        *reinterpret_cast<uint4*>(a.out + o) = *reinterpret_cast<const uint4*>(epb + win * LDC + c8 * 8);
+        *reinterpret_cast<uint2*>(a.code + o) = *reinterpret_cast<const uint2*>(epc + win * LDC + c8 * 8);
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else if (a.mode == 0) {
+      bf16* epb = reinterpret_cast<bf16*>(ep);                // [TM*16 pixels][LDC]
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int p = (tb + t) * 16 + g * 4 + j;
+          const int pc = p < npix ? p : 0;
+          const int pyl = fwo.div(pc);
+          const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (pc - pyl * a.Wo);
+#pragma unroll
+          for (int nt = 0; nt < NTC; ++nt) {
+            const int n = (nt0 + nt) * 16 + r;
+            float x = 0.f;
+            if (n < a.N) {
+              x = acc[t][nt][j] + (a.bias ? a.bias[n] : 0.f);
+              if (a.relu) x = fmaxf(x, 0.f);
+              if (a.drop_thr)
+                x = dropout_keep((uint32_t)(m * a.N + n), a.seed, a.stream_id, step, a.drop_thr) ? x * a.drop_scale
+                                                                                               : 0.f;
+            }
+            epb[(t * 16 + g * 4 + j) * LDC + nt * 16 + r] = f2bf(x);
+          }
         }
-        __builtin_amdgcn_wave_barrier();
-      } else {
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int np = max(0, min(TM * 16, npix - tb * 16));
+      for (int c = lane; c < np * cch; c += 64) {
+        const int pr = fcch.div(c), c8 = c - pr * cch;
+        const int p = tb * 16 + pr;
+        const int pyl = fwo.div(p);
+        const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (p - pyl * a.Wo);
+        *reinterpret_cast<uint4*>(a.out + m * a.Cs_out + nt0 * 16 + c8 * 8) =
+            *reinterpret_cast<const uint4*>(epb + pr * LDC + c8 * 8);
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else {
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const int tile = tb + t;
+        if (tile >= ntiles) break;
 #pragma unroll
         for (int nt = 0; nt < NTC; ++nt)
 #pragma unroll
@@ -243,33 +287,14 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvMMArgs a) {
         __builtin_amdgcn_wave_barrier();
         const int np = min(16, npix - tile * 16);
         for (int c = lane; c < np * cch; c += 64) {
-          const int pr = c / cch, c8 = c - pr * cch;
+          const int pr = fcch.div(c), c8 = c - pr * cch;
           const int p = tile * 16 + pr;
           const int pyl = fwo.div(p);
           const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (p - pyl * a.Wo);
           float v[8];
           *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(ep + pr * LDC + c8 * 8);
           *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(ep + pr * LDC + c8 * 8 + 4);
-          const int n0 = nt0 * 16 + c8 * 8;
-          if (a.mode == 1) {
-            bwd_through_store8(a.bt, m, n0, v, step);
-          } else {
-            bf16x8 o;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const int n = n0 + k;
-              float x = 0.f;
-              if (n < a.N) {
-                x = v[k] + (a.bias ? a.bias[n] : 0.f);
-                if (a.relu) x = fmaxf(x, 0.f);
-                if (a.drop_thr)
-                  x = dropout_keep((uint32_t)(m * a.N + n), a.seed, a.stream_id, step, a.drop_thr) ? x * a.drop_scale
-                                                                                                 : 0.f;
-              }
-              o[k] = f2bf(x);
-            }
-            *reinterpret_cast<bf16x8*>(a.out + m * a.Cs_out + n0) = o;
-          }
+          bwd_through_store8(a.bt, m, nt0 * 16 + c8 * 8, v, step);
         }
         __builtin_amdgcn_wave_barrier();
       }
@@ -282,8 +307,10 @@ size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc) {
   const int ntab = cs4 ? a.KS * 8 : a.KS * 4;
   const int W_in = (a.Wo - 1) * a.stride + a.KW;
   const int R_in = (a.R - 1) * a.stride + a.KH;
+  const int TM = ntc >= 8 ? 2 : 4;
+  const size_t ep_wave = (size_t)(TM * 16 * 2 > 16 * 4 ? TM * 16 * 2 : 16 * 4) * ntc * 16;   // bytes
   return (size_t)((ntab * 4 + 15) & ~15) + 32 + (size_t)a.KS * ntc * 64 * 16 +
-         (((size_t)R_in * W_in * a.Cs_in + 7) & ~(size_t)7) * 2 + (size_t)4 * 16 * ntc * 16 * 4;
+         (((size_t)R_in * W_in * a.Cs_in + 7) & ~(size_t)7) * 2 + 4 * ep_wave;
 }
 
 template <int NTC, int KCH, bool CS4>
