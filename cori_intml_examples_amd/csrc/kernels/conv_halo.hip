@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvMMArgs a) {
 
   const FastDiv fwp(a.Wp > 0 ? a.Wp : 1), fwo(a.Wo);
   // per-wave epilogue scratch [16 rows][NTC*16] fp32, after the 16-B aligned halo image
-  constexpr int EPW = (TM * 16 * 2 > 16 * 4 ? TM * 16 * 2 : 16 * 4) * NTC * 16 / 4;   // floats per wave
+  constexpr int EPW = TM * 16 * 2 * NTC * 16 / 4;   // floats per wave: TM*16 rows x LDC bf16
   float* ep = reinterpret_cast<float*>(xl + (((size_t)R_in * W_in * Cs + 7) & ~(size_t)7)) + wave * EPW;
   const size_t qbase = ((size_t)b * a.Hp + (oy0 >> 1)) * a.Wp;
   for (int tb = wave * TM; tb < ntiles; tb += 4 * TM) {
@@ -239,8 +239,10 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvMMArgs a) {
         *reinterpret_cast<uint2*>(a.code + o) = *reinterpret_cast<const uint2*>(epc + win * LDC + c8 * 8);
       }
       __builtin_amdgcn_wave_barrier();
-    } else if (a.mode == 0) {
+    } else {
+      // unpooled forward and dgrad (mode 1): stage the TM tiles as bf16, then one copy loop
       bf16* epb = reinterpret_cast<bf16*>(ep);                // [TM*16 pixels][LDC]
+      const bool fwd = a.mode == 0;
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
 #pragma unroll
@@ -252,13 +254,16 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvMMArgs a) {
 #pragma unroll
           for (int nt = 0; nt < NTC; ++nt) {
             const int n = (nt0 + nt) * 16 + r;
-            float x = 0.f;
-            if (n < a.N) {
-              x = acc[t][nt][j] + (a.bias ? a.bias[n] : 0.f);
-              if (a.relu) x = fmaxf(x, 0.f);
-              if (a.drop_thr)
-                x = dropout_keep((uint32_t)(m * a.N + n), a.seed, a.stream_id, step, a.drop_thr) ? x * a.drop_scale
-                                                                                               : 0.f;
+            float x = acc[t][nt][j];
+            if (fwd) {
+              x = 0.f;
+              if (n < a.N) {
+                x = acc[t][nt][j] + (a.bias ? a.bias[n] : 0.f);
+                if (a.relu) x = fmaxf(x, 0.f);
+                if (a.drop_thr)
+                  x = dropout_keep((uint32_t)(m * a.N + n), a.seed, a.stream_id, step, a.drop_thr) ? x * a.drop_scale
+                                                                                                 : 0.f;
+              }
             }
             epb[(t * 16 + g * 4 + j) * LDC + nt * 16 + r] = f2bf(x);
           }
@@ -271,33 +276,17 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvMMArgs a) {
         const int p = tb * 16 + pr;
         const int pyl = fwo.div(p);
         const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (p - pyl * a.Wo);
-        *reinterpret_cast<uint4*>(a.out + m * a.Cs_out + nt0 * 16 + c8 * 8) =
-            *reinterpret_cast<const uint4*>(epb + pr * LDC + c8 * 8);
-      }
-      __builtin_amdgcn_wave_barrier();
-    } else {
-#pragma unroll
-      for (int t = 0; t < TM; ++t) {
-        const int tile = tb + t;
-        if (tile >= ntiles) break;
-#pragma unroll
-        for (int nt = 0; nt < NTC; ++nt)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) ep[(g * 4 + j) * LDC + nt * 16 + r] = acc[t][nt][j];
-        __builtin_amdgcn_wave_barrier();
-        const int np = min(16, npix - tile * 16);
-        for (int c = lane; c < np * cch; c += 64) {
-          const int pr = fcch.div(c), c8 = c - pr * cch;
-          const int p = tile * 16 + pr;
-          const int pyl = fwo.div(p);
-          const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (p - pyl * a.Wo);
+        const bf16x8 val = *reinterpret_cast<const bf16x8*>(epb + pr * LDC + c8 * 8);
+        if (fwd) {
+          *reinterpret_cast<bf16x8*>(a.out + m * a.Cs_out + nt0 * 16 + c8 * 8) = val;
+        } else {
           float v[8];
-          *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(ep + pr * LDC + c8 * 8);
-          *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(ep + pr * LDC + c8 * 8 + 4);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = bf2f(val[k]);
           bwd_through_store8(a.bt, m, nt0 * 16 + c8 * 8, v, step);
         }
-        __builtin_amdgcn_wave_barrier();
       }
+      __builtin_amdgcn_wave_barrier();
     }
   }
 }
@@ -308,7 +297,7 @@ size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc) {
   const int W_in = (a.Wo - 1) * a.stride + a.KW;
   const int R_in = (a.R - 1) * a.stride + a.KH;
   const int TM = ntc >= 8 ? 2 : 4;
-  const size_t ep_wave = (size_t)(TM * 16 * 2 > 16 * 4 ? TM * 16 * 2 : 16 * 4) * ntc * 16;   // bytes
+  const size_t ep_wave = (size_t)TM * 16 * 2 * ntc * 16;   // bytes
   return (size_t)((ntab * 4 + 15) & ~15) + 32 + (size_t)a.KS * ntc * 64 * 16 +
          (((size_t)R_in * W_in * a.Cs_in + 7) & ~(size_t)7) * 2 + 4 * ep_wave;
 }
