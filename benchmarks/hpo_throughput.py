@@ -45,6 +45,24 @@ def trial(conv_sizes, fc_sizes, lr, dropout, optimizer, n_train=64000, n_valid=3
             "device": str(model.device)}
 
 
+def trial_mnist(h1, h2, h3, dropout, optimizer, n_train=60000, batch_size=128, n_epochs=16, valid_frac=0.17):
+    """DistHPO_mnist's build_and_train (DistHPO_mnist.ipynb:169-191) on cached synthetic MNIST."""
+    import time as _t
+    t0 = _t.time()
+    from cori_intml_examples_amd.apps.mnist import build_model
+    from cori_intml_examples_amd.io.datasets import synthetic_mnist
+    key = ("mnist", n_train)
+    if key not in _CACHE:
+        x, y, _, _ = synthetic_mnist(n_train, 10)
+        _CACHE[key] = (x, y)
+    x, y = _CACHE[key]
+    t1 = _t.time()
+    model = build_model(h1=h1, h2=h2, h3=h3, dropout=dropout, optimizer=optimizer)
+    h = model.fit(x, y, batch_size=batch_size, epochs=n_epochs, validation_split=valid_frac, verbose=0)
+    return {"val_loss": h.history["val_loss"], "data_s": t1 - t0, "train_s": _t.time() - t1,
+            "device": str(model.device)}
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--trials", type=int, default=16)
@@ -54,7 +72,13 @@ def main():
     ap.add_argument("--batch-size", type=int, default=64)
     ap.add_argument("--engines", type=int, default=None)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--model", choices=["rpv", "mnist"], default="rpv",
+                    help="rpv: CrayHPO_rpv-style evaluations; mnist: DistHPO_mnist (16 epochs, 60k, B=128)")
     a = ap.parse_args()
+    if a.model == "mnist":            # DistHPO_mnist.ipynb:137-153 defaults unless overridden
+        a.epochs = a.epochs if "--epochs" in sys.argv else 16
+        a.n_train = a.n_train if "--n-train" in sys.argv else 60000
+        a.batch_size = a.batch_size if "--batch-size" in sys.argv else 128
     import cloudpickle
     cloudpickle.register_pickle_by_value(sys.modules[__name__])
     from cori_intml_examples_amd import farm
@@ -66,9 +90,14 @@ def main():
     try:
         with cl.client() as c:
             t_up = time.time() - t0
-            trials = rs.rpv_trials(a.trials)
-            ars = rs.submit_trials(c.load_balanced_view(), trial, trials, n_train=a.n_train, n_valid=a.n_valid,
-                                   batch_size=a.batch_size, n_epochs=a.epochs)
+            if a.model == "mnist":
+                trials = rs.mnist_trials(a.trials)
+                ars = rs.submit_trials(c.load_balanced_view(), trial_mnist, trials, n_train=a.n_train,
+                                       batch_size=a.batch_size, n_epochs=a.epochs)
+            else:
+                trials = rs.rpv_trials(a.trials)
+                ars = rs.submit_trials(c.load_balanced_view(), trial, trials, n_train=a.n_train, n_valid=a.n_valid,
+                                       batch_size=a.batch_size, n_epochs=a.epochs)
             rs.wait_progress(ars, interval=1.0, printer=lambda s: print(s, file=sys.stderr, flush=True))
             res = rs.collect(ars)
     finally:
@@ -76,14 +105,20 @@ def main():
     wall = time.time() - t0
     ok = [r for r in res if r]
     per_hour = len(ok) / wall * 3600
+    if a.model == "mnist":
+        metric = ("HPO trials/hour (MNIST random search, %d epochs, %dk samples, valid_frac 0.17, batch %d)"
+                  % (a.epochs, a.n_train // 1000, a.batch_size))
+    else:
+        metric = ("HPO trials/hour (RPV random search, %d epochs, %dk train / %dk valid, batch %d)"
+                  % (a.epochs, a.n_train // 1000, a.n_valid // 1000, a.batch_size))
     print(json.dumps({
-        "metric": "HPO trials/hour (RPV random search, %d epochs, %dk train / %dk valid, batch %d)"
-                  % (a.epochs, a.n_train // 1000, a.n_valid // 1000, a.batch_size),
+        "metric": metric,
         "value": round(per_hour, 1), "unit": "trials/hour", "n_gpus": n_gpu, "engines": a.engines or max(1, n_gpu),
         "trials": len(ok), "failed": len(res) - len(ok), "wall_s": round(wall, 2), "startup_s": round(t_up, 2),
         "mean_train_s": round(sum(r["train_s"] for r in ok) / max(1, len(ok)), 3),
-        "vs_baseline": round(per_hour / REF_EVALS_PER_HOUR, 2), "baseline": "41.2 evals/hour (CrayHPO_rpv, 32 nodes)",
-        "data": "synthetic RPV (1-channel 64x64), resident per engine"}))
+        "vs_baseline": round(per_hour / REF_EVALS_PER_HOUR, 2) if a.model == "rpv" else None,
+        "baseline": "41.2 evals/hour (CrayHPO_rpv, 32 nodes)" if a.model == "rpv" else "no wall-clock recorded",
+        "data": "synthetic %s, resident per engine" % ("RPV (1-channel 64x64)" if a.model == "rpv" else "MNIST")}))
 
 
 if __name__ == "__main__":
