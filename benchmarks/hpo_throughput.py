@@ -22,7 +22,11 @@ sys.path.insert(0, ROOT)
 REF_EVALS_PER_HOUR = 128 / (3 * 3600 + 6 * 60 + 36) * 3600     # 41.2
 
 
-_CACHE = {}
+def _cache():
+    """Engine-resident dataset cache (trial functions are shipped by value, so a module
+    global would be re-created for every task)."""
+    from cori_intml_examples_amd.farm import engine_namespace
+    return engine_namespace().setdefault("_hpo_bench_cache", {})
 
 
 def trial(conv_sizes, fc_sizes, lr, dropout, optimizer, n_train=64000, n_valid=32000, batch_size=64,
@@ -31,6 +35,7 @@ def trial(conv_sizes, fc_sizes, lr, dropout, optimizer, n_train=64000, n_valid=3
     t0 = _t.time()
     from cori_intml_examples_amd.apps.rpv import build_model, train_model
     from cori_intml_examples_amd.io.datasets import synthetic_rpv
+    _CACHE = _cache()
     key = (n_train, n_valid, channels)
     if key not in _CACHE:
         tr = synthetic_rpv(n_train, channels=channels, seed=1)
@@ -42,7 +47,7 @@ def trial(conv_sizes, fc_sizes, lr, dropout, optimizer, n_train=64000, n_valid=3
                         optimizer=optimizer, lr=lr)
     h = train_model(model, x, y, xv, yv, batch_size=batch_size, n_epochs=n_epochs, verbose=0)
     return {"val_loss": h.history["val_loss"], "data_s": t1 - t0, "train_s": _t.time() - t1,
-            "device": str(model.device)}
+            "device": str(model.device), "t0": t0, "t1": _t.time()}
 
 
 def trial_mnist(h1, h2, h3, dropout, optimizer, n_train=60000, batch_size=128, n_epochs=16, valid_frac=0.17):
@@ -51,6 +56,7 @@ def trial_mnist(h1, h2, h3, dropout, optimizer, n_train=60000, batch_size=128, n
     t0 = _t.time()
     from cori_intml_examples_amd.apps.mnist import build_model
     from cori_intml_examples_amd.io.datasets import synthetic_mnist
+    _CACHE = _cache()
     key = ("mnist", n_train)
     if key not in _CACHE:
         x, y, _, _ = synthetic_mnist(n_train, 10)
@@ -60,7 +66,7 @@ def trial_mnist(h1, h2, h3, dropout, optimizer, n_train=60000, batch_size=128, n
     model = build_model(h1=h1, h2=h2, h3=h3, dropout=dropout, optimizer=optimizer)
     h = model.fit(x, y, batch_size=batch_size, epochs=n_epochs, validation_split=valid_frac, verbose=0)
     return {"val_loss": h.history["val_loss"], "data_s": t1 - t0, "train_s": _t.time() - t1,
-            "device": str(model.device)}
+            "device": str(model.device), "t0": t0, "t1": _t.time()}
 
 
 def main():
@@ -71,6 +77,8 @@ def main():
     ap.add_argument("--n-valid", type=int, default=32000)
     ap.add_argument("--batch-size", type=int, default=64)
     ap.add_argument("--engines", type=int, default=None)
+    ap.add_argument("--engines-per-gpu", type=int, default=4,
+                    help="farm engines pinned to each GPU (small models leave most CUs idle)")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--model", choices=["rpv", "mnist"], default="rpv",
                     help="rpv: CrayHPO_rpv-style evaluations; mnist: DistHPO_mnist (16 epochs, 60k, B=128)")
@@ -85,7 +93,9 @@ def main():
     from cori_intml_examples_amd.hpo import random_search as rs
     t0 = time.time()
     n_gpu = 0 if a.cpu else farm.detect_gpus()
-    cl = farm.start_cluster(a.engines or max(1, n_gpu), cluster_id="hpo_bench_%d" % os.getpid(),
+    if a.engines is None:
+        a.engines = max(1, n_gpu) * (a.engines_per_gpu if n_gpu else 1)
+    cl = farm.start_cluster(a.engines, cluster_id="hpo_bench_%d" % os.getpid(),
                             cpu_only=a.cpu or n_gpu == 0, timeout=300)
     try:
         with cl.client() as c:
@@ -113,9 +123,11 @@ def main():
                   % (a.epochs, a.n_train // 1000, a.n_valid // 1000, a.batch_size))
     print(json.dumps({
         "metric": metric,
-        "value": round(per_hour, 1), "unit": "trials/hour", "n_gpus": n_gpu, "engines": a.engines or max(1, n_gpu),
+        "value": round(per_hour, 1), "unit": "trials/hour", "n_gpus": n_gpu, "engines": a.engines,
         "trials": len(ok), "failed": len(res) - len(ok), "wall_s": round(wall, 2), "startup_s": round(t_up, 2),
         "mean_train_s": round(sum(r["train_s"] for r in ok) / max(1, len(ok)), 3),
+        "mean_data_s": round(sum(r["data_s"] for r in ok) / max(1, len(ok)), 3),
+        "mean_trial_s": round(sum(r["t1"] - r["t0"] for r in ok) / max(1, len(ok)), 3),
         "vs_baseline": round(per_hour / REF_EVALS_PER_HOUR, 2) if a.model == "rpv" else None,
         "baseline": "41.2 evals/hour (CrayHPO_rpv, 32 nodes)" if a.model == "rpv" else "no wall-clock recorded",
         "data": "synthetic %s, resident per engine" % ("RPV (1-channel 64x64)" if a.model == "rpv" else "MNIST")}))

@@ -182,6 +182,18 @@ def engine_id() -> Optional[int]:
     return None if _ENGINE is None else _ENGINE.engine_id
 
 
+_LOCAL_NS: Dict[str, Any] = {}
+
+
+def engine_namespace() -> Dict[str, Any]:
+    """The engine's persistent namespace (what ``push``/``pull``/``%%px`` see).  Functions
+    shipped by value get fresh globals per task, so state that must survive across tasks
+    on one engine (a resident dataset, a compiled model) is kept here.  Outside an engine
+    this is a process-wide dict."""
+    e = _ENGINE
+    return _LOCAL_NS if e is None else e.ns
+
+
 def should_stop() -> bool:
     """Cooperative cancellation flag of the running task (Stop button / ``AsyncResult.abort``)."""
     e = _ENGINE

@@ -53,6 +53,26 @@ def test_ids_and_load_balanced(cluster):
     assert lv.map_sync(_square, [1, 2, 3]) == [1, 4, 9]
 
 
+_SHIPPED_GLOBAL = {}
+
+
+def _count_calls():
+    # a by-value function's module globals are rebuilt per task; the engine namespace is not
+    _SHIPPED_GLOBAL["n"] = _SHIPPED_GLOBAL.get("n", 0) + 1
+    ns = farm.engine_namespace()
+    ns["calls"] = ns.get("calls", 0) + 1
+    return ns["calls"], _SHIPPED_GLOBAL["n"]
+
+
+def test_engine_namespace_persists(cluster):
+    _, c = cluster
+    v = c[0]
+    first = v.apply_sync(_count_calls)
+    second = v.apply_sync(_count_calls)
+    assert second[0] == first[0] + 1 and second[1] == 1
+    assert v.pull("calls") == second[0]          # same dict as push/pull/%%px
+
+
 def test_publish_data_streams(cluster):
     _, c = cluster
     a = c.load_balanced_view().apply(_publisher, 5)
