@@ -22,6 +22,8 @@ void launch_wgrad(const WgradArgs& a, int ktw, int ntt, int splits, hipStream_t 
 size_t wgrad_lds_bytes(int KT, int NTT);
 void launch_dense_fwd(const DenseFwdArgs& a, hipStream_t s);
 void launch_dense_epi(const DenseEpiArgs& a, hipStream_t s);
+int dense_groups(int M, int NT, int KS);
+bool dense_big(int NT, int KS);
 void launch_head(const HeadArgs& a, hipStream_t s);
 void launch_step_begin(const StepBeginArgs& a, hipStream_t s);
 void launch_gather(const GatherArgs& a, hipStream_t s);
@@ -173,6 +175,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wgrad", [](const WgradArgs& a, int ktw, int ntt, int splits, uintptr_t s) {
     launch_wgrad(a, ktw, ntt, splits, S(s)); check_last("wgrad"); });
   m.def("dense_fwd", [](const DenseFwdArgs& a, uintptr_t s) { launch_dense_fwd(a, S(s)); check_last("dense_fwd"); });
+  m.def("dense_groups", &dense_groups, "work items per K-split of dense_fwd for (M, NT, KS)");
+  m.def("dense_big", &dense_big, "dense_fwd uses the large-weight LDS path for (NT, KS)");
   m.def("dense_epi", [](const DenseEpiArgs& a, uintptr_t s) { launch_dense_epi(a, S(s)); check_last("dense_epi"); });
   m.def("head", [](const HeadArgs& a, uintptr_t s) { launch_head(a, S(s)); check_last("head"); });
   m.def("step_begin", [](const StepBeginArgs& a, uintptr_t s) { launch_step_begin(a, S(s)); check_last("step_begin"); });

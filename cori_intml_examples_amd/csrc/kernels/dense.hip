@@ -66,6 +66,123 @@ __global__ __launch_bounds__(256) void dense_splitk_kernel(const DenseFwdArgs a)
   }
 }
 
+// Large-weight path (legacy RPV Dense(512) on a 65,536-wide input: 67 MB of bf16 weights,
+// and its dX).  The small-weight kernel above re-reads every weight fragment once per
+// 16-row m-tile, which for a weight matrix that does not stay in L2 multiplies the
+// dominant HBM stream by M/16.  Here one 512-thread workgroup owns ALL rows of its m-group
+// (128) x 8 n-tiles (one per wave) over a K-split:
+//   * the activation tile (128 rows x 32 k per k-step) is staged once per workgroup in LDS
+//     (one 16-B load per thread per k-step, rows padded to 40 elements for conflict-light
+//     fragment reads) and feeds all 8 waves;
+//   * each wave streams only its own weight fragments (1 KB coalesced per k-step) straight
+//     into VGPRs -- every weight byte crosses HBM once;
+//   * DL_KST k-steps per stage, double-buffered in LDS and registers: the next stage's
+//     loads (~32 KB per workgroup) are in flight while the current stage's MFMAs run.
+namespace {
+constexpr int DL_KST = 4;
+constexpr int DL_LDA = 40;
+constexpr int DL_ROWS = 128;
+constexpr long long DL_BIG_BYTES = 8ll << 20;   // weight bytes above which the LDS path is used
+}
+
+__global__ __launch_bounds__(512) void dense_lds_kernel(const DenseFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* const As = reinterpret_cast<bf16*>(smem);  // [2][DL_KST][DL_ROWS][DL_LDA]
+  constexpr int STG = DL_KST * DL_ROWS * DL_LDA;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const int nblocks = (a.NT + 7) / 8, mgroups = (a.M + DL_ROWS - 1) / DL_ROWS;
+  const int nb = (int)(blockIdx.x % nblocks);
+  const int t2 = (int)(blockIdx.x / nblocks);
+  const int mg = t2 % mgroups, s = t2 / mgroups;
+  const int nt = nb * 8 + wave;
+  const int ntc = min(nt, a.NT - 1);
+  const int arow = mg * DL_ROWS + (tid >> 2);
+  const bool av = arow < a.M;
+  const bf16* ap = a.x + (size_t)(av ? arow : 0) * a.Ks + (tid & 3) * 8;
+  const int ks_lo = s * a.ks_per_split;
+  const int ks_hi = min(a.KS, ks_lo + a.ks_per_split);
+  const int nst = (ks_hi - ks_lo + DL_KST - 1) / DL_KST;
+  bf16x8 ra[DL_KST], rb[DL_KST], rbn[DL_KST];
+  auto issue = [&](int st) {
+#pragma unroll
+    for (int kk = 0; kk < DL_KST; ++kk) {
+      const int k = ks_lo + st * DL_KST + kk;
+      const bool kv = k < ks_hi;
+      const int ks = kv ? k : ks_hi - 1;
+      const int k0 = ks * 32 + (tid & 3) * 8;
+      ra[kk] = load_bf16x8_if(kv && av && k0 < a.Ks, ap + ks * 32, a.x);
+      rbn[kk] = load_bf16x8(a.wpk + ((size_t)(ks * a.NT + ntc) * 64 + lane) * 8);
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int kk = 0; kk < DL_KST; ++kk) {
+      *reinterpret_cast<bf16x8*>(As + buf * STG + kk * DL_ROWS * DL_LDA + (tid >> 2) * DL_LDA + (tid & 3) * 8) = ra[kk];
+      rb[kk] = rbn[kk];
+    }
+  };
+  f32x4 acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nst > 0) {
+    issue(0);
+    stash(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    const bool more = st + 1 < nst;
+    if (more) issue(st + 1);
+    const bf16* A = As + cur * STG;
+#pragma unroll
+    for (int kk = 0; kk < DL_KST; ++kk) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(A + kk * DL_ROWS * DL_LDA + (t * 16 + r) * DL_LDA + 8 * g);
+        acc[t] = mfma16(af, rb[kk], acc[t]);
+      }
+    }
+    if (more) stash(cur ^ 1);
+    __syncthreads();
+  }
+  if (nt >= a.NT) return;
+  if (a.mode == 1) {
+    const BwdThrough& bt = a.bt;
+    const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
+    const int col = nt * 16 + r;
+    if (col >= bt.pH * bt.pW * bt.pCs) return;
+    const int y = col / (bt.pW * bt.pCs);
+    const int rem = col - y * bt.pW * bt.pCs;
+    const int x = rem / bt.pCs;
+    const int c = rem - x * bt.pCs;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mg * DL_ROWS + t * 16 + g * 4 + j;
+        if (m < a.M) bwd_through_store(bt, m, y, x, c, acc[t][j], step);
+      }
+    return;
+  }
+  const int ld = a.NT * 16;
+  float* out = a.part + (size_t)s * a.M * ld;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = mg * DL_ROWS + t * 16 + g * 4 + j;
+      if (m < a.M) out[(size_t)m * ld + nt * 16 + r] = acc[t][j];
+    }
+}
+
+bool dense_big(int NT, int KS) { return (long long)NT * KS * 1024 > DL_BIG_BYTES; }
+
+// Work items per K-split: waves (small path) or workgroups (large-weight path).
+int dense_groups(int M, int NT, int KS) {
+  if (dense_big(NT, KS)) return ((M + DL_ROWS - 1) / DL_ROWS) * ((NT + 7) / 8);
+  return ((M + 15) / 16) * NT;
+}
+
 // 64 outputs per workgroup, the 4 waves split the K-splits (independent loads in flight),
 // fixed-order LDS combine (deterministic).
 __global__ __launch_bounds__(256) void dense_epilogue_kernel(const DenseEpiArgs a) {
@@ -105,10 +222,15 @@ __global__ __launch_bounds__(256) void dense_epilogue_kernel(const DenseEpiArgs 
 }
 
 void launch_dense_fwd(const DenseFwdArgs& a, hipStream_t s) {
+  if (dense_big(a.NT, a.KS)) {
+    const long long wgs = (long long)dense_groups(a.M, a.NT, a.KS) * a.splits;
+    const size_t lds = (size_t)2 * DL_KST * DL_ROWS * DL_LDA * sizeof(bf16);
+    hipLaunchKernelGGL(dense_lds_kernel, dim3((unsigned)wgs), dim3(512), lds, s, a);
+    return;
+  }
   const long long waves = (long long)((a.M + 15) / 16) * a.NT * a.splits;
   hipLaunchKernelGGL(dense_splitk_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a);
 }
-
 void launch_dense_epi(const DenseEpiArgs& a, hipStream_t s) {
   const long long n = (long long)a.M * a.Ns;
   hipLaunchKernelGGL(dense_epilogue_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, a);

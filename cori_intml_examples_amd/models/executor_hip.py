@@ -406,8 +406,13 @@ class BatchPlan:
         self.dense_splits = []
         for g in ex.denses:
             self.dense_out.append(z(bs, g.Ns))
-            mt = cdiv(bs, 16)
-            splits = max(1, min(g.KS, 2048 // max(1, mt * g.NT)))
+            if K.dense_big(g.NT, g.KS):
+                # large weights: ~256 workgroups (one per CU) of >= 8 k-steps; each owns
+                # 128 rows x 8 n-tiles, so every weight byte streams from HBM once
+                splits = max(1, min(cdiv(256, K.dense_groups(bs, g.NT, g.KS)), cdiv(g.KS, 8)))
+            else:
+                # ~2048 16x16-tile waves: latency-bound small layers want parallelism
+                splits = max(1, min(g.KS, 2048 // max(1, K.dense_groups(bs, g.NT, g.KS))))
             kps = cdiv(g.KS, splits)
             splits = cdiv(g.KS, kps)
             self.dense_splits.append((splits, kps))
