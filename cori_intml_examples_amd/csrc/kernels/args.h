@@ -49,6 +49,9 @@ struct ConvMMArgs {
   int R = 1;
   const uint8_t* in_code = nullptr;
   int in_pH = 0, in_pW = 0;
+  // >= 16 zero bytes in global memory: source of padded / out-of-range rows for the LDS-DMA
+  // conv_tile path (set => that path is used when there is no unpool-on-load input)
+  const bf16* zero = nullptr;
   int dbg = 0;   // ablation (timing only, wrong results): 1 skip staging, 2 skip MFMA, 4 skip stores
 };
 

@@ -63,7 +63,7 @@ PYBIND11_MODULE(_kernels, m) {
       RW(ConvMMArgs, flat_out) RW(ConvMMArgs, relu) RW(ConvMMArgs, pool) PTR(ConvMMArgs, out)
       RW(ConvMMArgs, Cs_out) RW(ConvMMArgs, Hp) RW(ConvMMArgs, Wp) PTR(ConvMMArgs, code)
       RW(ConvMMArgs, drop_thr) RW(ConvMMArgs, drop_scale) RW(ConvMMArgs, seed) RW(ConvMMArgs, stream_id)
-      PTR(ConvMMArgs, st) RW(ConvMMArgs, bt) RW(ConvMMArgs, R) PTR(ConvMMArgs, in_code)
+      PTR(ConvMMArgs, st) RW(ConvMMArgs, bt) RW(ConvMMArgs, R) PTR(ConvMMArgs, in_code) PTR(ConvMMArgs, zero)
       RW(ConvMMArgs, in_pH) RW(ConvMMArgs, in_pW) RW(ConvMMArgs, dbg);
 
   py::class_<WgradArgs>(m, "WgradArgs")

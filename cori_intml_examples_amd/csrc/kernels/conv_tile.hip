@@ -2,19 +2,29 @@
 // the legacy RPV model (64..256 channels, Train_rpv.ipynb:205-219) and wide HPO trials.
 //
 // conv_halo keeps ALL of K's weights in LDS per workgroup, which forces a single 16-channel
-// n-tile per workgroup once K is large (every A fragment then feeds one MFMA).  This kernel
-// is a classic LDS-blocked GEMM over the whole batch instead:
+// n-tile per workgroup once K is large (every A fragment then feeds one MFMA).  These
+// kernels are LDS-blocked GEMMs over the whole batch instead:
 //   * block tile 128 output rows (pixels over the batch, or 2x2 pool windows x 4 positions)
 //     x BN = NTC*16 output channels, 256 threads = 2 x 2 waves, wave tile 64 x BN/2
 //     (4 x NTC/2 MFMA 16x16x32 tiles: each A fragment feeds NTC/2 MFMAs, each B fragment 4);
-//   * per 32-wide k-step (inside one tap, since Cs_in % 32 == 0) the block stages
-//     A_s[128][32] (16 B per lane: 8 channels of one tap-shifted NHWC pixel; zero padding,
-//     input dilation for strided dgrad and unpool-on-load from pooled dP + argmax codes are
-//     resolved in the gather) and B_s = the fragment-major weight pack slice (1 KB per
-//     n-tile, a straight copy) into a double-buffered LDS ring: the global loads of k-step
-//     j+1 are in flight while the MFMAs of step j run, one barrier per k-step;
-//   * A_s rows are padded to 40 elements so the ds_read_b128 fragment reads of 16 lanes on
-//     16 different rows spread over the LDS banks.
+//   * a k-step is 32 channels of one tap (Cs_in % 32 == 0): A_s[128][32] holds 8 channels
+//     of one tap-shifted NHWC pixel per 16-byte chunk (zero padding and the input dilation
+//     of strided dgrad resolved in the gather), B_s is the fragment-major weight pack slice
+//     (1 KB per n-tile, a straight copy); the LDS ring is double-buffered, one barrier per
+//     stage of 2 k-steps.
+//
+// Two staging paths:
+//   conv_gl_kernel   (default) LDS-DMA: `global_load_lds_dwordx4` writes A and B straight
+//                    into LDS with no VGPR round trip and no ds_write pass (which made the
+//                    register-staged kernel LDS-store bound: 32 KB of ds_write_b128 per
+//                    stage ~ 415 cycles against 512 MFMA cycles).  The DMA destination is
+//                    lane-linear, so zero padding comes from pointing a lane's SOURCE at a
+//                    zero buffer, and the bank-conflict swizzle of A is applied on the
+//                    source side: 64-B rows, chunk c of row r stored at position
+//                    c ^ ((-(r>>2)) & 3) within its row, which makes every 16-lane group
+//                    of a fragment ds_read_b128 cover all 64 banks once.
+//   conv_tile_kernel register-staged, for the unpool-on-load input (dP + argmax codes)
+//                    whose gather needs arithmetic; rows padded to 40 elements.
 // Epilogues are conv_halo's (mode 0: bias/ReLU/pool+argmax/dropout -> bf16 NHWC; mode 1:
 // backward-through the previous stage), staged through LDS for 16-byte stores.
 #include <type_traits>
@@ -23,42 +33,16 @@
 
 namespace {
 constexpr int BM = 128;         // rows per block
-constexpr int LDA = 40;         // A_s row stride (elements): 32 + 8 pad
+constexpr int LDA = 40;         // register path: A_s row stride (elements): 32 + 8 pad
 constexpr int KST = 2;          // k-steps per pipeline stage (one barrier per stage)
-}
 
-template <int NTC>
-__global__ __launch_bounds__(256) void conv_tile_kernel(const ConvMMArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NW = NTC / 2;                         // n-tiles per wave
-  constexpr int A_EL = BM * LDA;                      // A_s elements per k-step
-  constexpr int B_EL = NTC * 64 * 8;                  // B_s elements per k-step
-  constexpr int STG_EL = KST * (A_EL + B_EL);         // one LDS buffer = KST k-steps
-  bf16* const lds = reinterpret_cast<bf16*>(smem);    // [2][KST][A] [KST][B]
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
-  const int wm = wave & 1, wn = wave >> 1;
-  const int nt0 = blockIdx.y * NTC;
-  const int Cs = a.Cs_in, s = a.stride, dil = a.in_dil;
-  const int cps = Cs >> 5;                            // k-steps per tap
-  const bool pool = a.mode == 0 && a.pool;
-  // Strided dgrad (input dilation dil > 1): output pixels are split into dil x dil parity
-  // classes (grid.z); in a class only taps with (o - pad + k) % dil == 0 contribute, so the
-  // K loop visits just those (~1/dil^2 of the dense-dilated work).
-  const int cy = dil > 1 ? (int)blockIdx.z / dil : 0, cx = dil > 1 ? (int)blockIdx.z % dil : 0;
-  const int Hc = dil > 1 ? (a.Ho - cy + dil - 1) / dil : a.Ho;
-  const int Wc = dil > 1 ? (a.Wo - cx + dil - 1) / dil : a.Wo;
-  const int ky0 = dil > 1 ? ((a.pad_t - cy) % dil + dil) % dil : 0;
-  const int kx0 = dil > 1 ? ((a.pad_l - cx) % dil + dil) % dil : 0;
-  const int nky = ky0 < a.KH ? (a.KH - ky0 + dil - 1) / dil : 0;
-  const int nkx = kx0 < a.KW ? (a.KW - kx0 + dil - 1) / dil : 0;
-  const int KS = nky * nkx * cps;                     // k-steps actually visited
-  const long long nrows = pool ? (long long)a.B * a.Hp * a.Wp * 4 : (long long)a.B * Hc * Wc;
-  const long long row0 = (long long)blockIdx.x * BM;
-  if (row0 >= nrows) return;                          // (parity classes differ in size)
-  const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
-  const int IH = a.in_code ? a.in_pH : a.H, IW = a.in_code ? a.in_pW : a.W;
-
-  auto row_coords = [&](long long rr, int& b, int& oy, int& ox) {
+// Output-row space of one launch: 2x2 pool windows x 4 positions, or the pixels of one
+// input-dilation parity class (strided dgrad), or plain pixels.
+struct TileRows {
+  bool pool;
+  int dil, cy, cx, Hc, Wc;
+  long long nrows;
+  __device__ void coords(const ConvMMArgs& a, long long rr, int& b, int& oy, int& ox) const {
     if (pool) {
       const long long w = rr >> 2;
       const int q = (int)(rr & 3);
@@ -76,29 +60,59 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(const ConvMMArgs a) {
       oy = cy + i * dil;
       ox = cx + j * dil;
     }
-  };
+  }
+};
 
-  // ---- this thread's two A-gather rows (128 rows x 4 chunks of 8 channels = 512 loads)
-  const int ach = tid & 3;                            // 8-channel chunk of the k-step
+// Strided dgrad (input dilation dil > 1): output pixels are split into dil x dil parity
+// classes (grid.z); in a class only taps with (o - pad + k) % dil == 0 contribute, so the
+// K loop visits just those (~1/dil^2 of the dense-dilated work).
+struct TapLattice {
+  int ky0, kx0, nky, nkx, KS;
+};
+
+__device__ __forceinline__ void tile_geometry(const ConvMMArgs& a, TileRows& tr, TapLattice& tl) {
+  const int dil = a.in_dil;
+  tr.pool = a.mode == 0 && a.pool;
+  tr.dil = dil;
+  tr.cy = dil > 1 ? (int)blockIdx.z / dil : 0;
+  tr.cx = dil > 1 ? (int)blockIdx.z % dil : 0;
+  tr.Hc = dil > 1 ? (a.Ho - tr.cy + dil - 1) / dil : a.Ho;
+  tr.Wc = dil > 1 ? (a.Wo - tr.cx + dil - 1) / dil : a.Wo;
+  tr.nrows = tr.pool ? (long long)a.B * a.Hp * a.Wp * 4 : (long long)a.B * tr.Hc * tr.Wc;
+  tl.ky0 = dil > 1 ? ((a.pad_t - tr.cy) % dil + dil) % dil : 0;
+  tl.kx0 = dil > 1 ? ((a.pad_l - tr.cx) % dil + dil) % dil : 0;
+  tl.nky = tl.ky0 < a.KH ? (a.KH - tl.ky0 + dil - 1) / dil : 0;
+  tl.nkx = tl.kx0 < a.KW ? (a.KW - tl.kx0 + dil - 1) / dil : 0;
+  tl.KS = tl.nky * tl.nkx * (a.Cs_in >> 5);
+}
+
+// k-step walker over the class's tap lattice for this thread's two gather rows; per-row
+// input coordinates / validity are recomputed only when the tap changes.
+struct Walker {
   int gb[2], gy[2], gx[2];
   bool gv[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const long long row = row0 + (tid >> 2) + 64 * u;
-    gv[u] = row < nrows;
-    row_coords(gv[u] ? row : 0, gb[u], gy[u], gx[u]);
-  }
-  // k-step walker: tap (ty, tx) in the class's tap lattice, channel step cstep; per-row
-  // input coordinates / validity are recomputed only when the tap changes.
-  int wty = 0, wtx = 0, wcs = 0;
+  int wty, wtx, wcs, cps, chunk;
   int iyr[2], ixr[2];
   bool okr[2];
   const bf16* rowp[2];
-  auto set_tap = [&]() {
-    const int ky = ky0 + wty * dil, kx = kx0 + wtx * dil;
+
+  __device__ void init(const ConvMMArgs& a, const TileRows& tr, long long r0, long long r1, int ch) {
+    const long long rows[2] = {r0, r1};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      int iy = gy[u] * s - a.pad_t + ky, ix = gx[u] * s - a.pad_l + kx;
+      gv[u] = rows[u] < tr.nrows;
+      tr.coords(a, gv[u] ? rows[u] : 0, gb[u], gy[u], gx[u]);
+    }
+    wty = wtx = wcs = 0;
+    cps = a.Cs_in >> 5;
+    chunk = ch;
+  }
+  __device__ void set_tap(const ConvMMArgs& a, const TapLattice& tl) {
+    const int dil = a.in_dil;
+    const int ky = tl.ky0 + wty * dil, kx = tl.kx0 + wtx * dil;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      int iy = gy[u] * a.stride - a.pad_t + ky, ix = gx[u] * a.stride - a.pad_l + kx;
       bool ok = gv[u] && iy >= 0 && ix >= 0;
       if (dil > 1) {          // exact: the class guarantees divisibility
         iy /= dil;
@@ -108,107 +122,29 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(const ConvMMArgs a) {
       iyr[u] = iy;
       ixr[u] = ix;
       okr[u] = ok;
-      rowp[u] = ok ? a.x + (((size_t)gb[u] * a.H + iy) * a.W + ix) * Cs + 8 * ach : a.x;
+      rowp[u] = ok ? a.x + (((size_t)gb[u] * a.H + iy) * a.W + ix) * a.Cs_in + 8 * chunk : a.x;
     }
-  };
-  auto next_k = [&]() {
+  }
+  __device__ void next_k(const ConvMMArgs& a, const TapLattice& tl) {
     if (++wcs == cps) {
       wcs = 0;
-      if (++wtx == nkx) { wtx = 0; ++wty; }
-      set_tap();
+      if (++wtx == tl.nkx) { wtx = 0; ++wty; }
+      set_tap(a, tl);
     }
-  };
-  auto pack_ks = [&]() { return ((ky0 + wty * dil) * a.KW + (kx0 + wtx * dil)) * cps + wcs; };
-  auto load_a = [&](int u) -> bf16x8 {
-    if (a.in_code) {
-      const size_t boff = (size_t)gb[u] * IH * IW * Cs;
-      return unpool_load8(a.x + boff, a.in_code + boff, IH, IW, Cs, iyr[u], ixr[u], wcs * 32 + 8 * ach, okr[u]);
-    }
-    return load_bf16x8_if(okr[u], rowp[u] + wcs * 32, a.x);
-  };
-  // ---- B gather: NTC*64 16-byte fragment vectors per k-step
-  constexpr int BV = (NTC * 64 + 255) / 256;
-  auto load_b = [&](int ksp, int u) -> bf16x8 {
-    const int v = tid + 256 * u;
-    const int nt = nt0 + (v >> 6);
-    const bool ok = v < NTC * 64 && nt < a.NT;
-    return load_bf16x8_if(ok, a.wpk + ((size_t)(ksp * a.NT + nt) * 64 + (v & 63)) * 8, a.wpk);
-  };
-  f32x4 acc[4][NW];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int n = 0; n < NW; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // One register stage (KST k-steps) in flight while the previous stage's MFMAs run out of
-  // the other LDS buffer.  Loads are unconditional (past the last k-step the walker stays
-  // put and the extra results are simply not used): a load under a branch would make
-  // hipcc drain vmcnt at the join.
-  bf16x8 ra[KST][2], rb[KST][BV];
-  int kl = 0;                                         // k-steps issued so far
-  auto issue_stage = [&]() {
-#pragma unroll
-    for (int kk = 0; kk < KST; ++kk) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) ra[kk][u] = load_a(u);
-      const int kp = pack_ks();
-#pragma unroll
-      for (int u = 0; u < BV; ++u) rb[kk][u] = load_b(kp, u);
-      if (++kl < KS) next_k();
-    }
-  };
-  auto store_stage = [&](int buf) {
-    bf16* base = lds + buf * STG_EL;
-#pragma unroll
-    for (int kk = 0; kk < KST; ++kk) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-        *reinterpret_cast<bf16x8*>(base + kk * A_EL + ((tid >> 2) + 64 * u) * LDA + 8 * ach) = ra[kk][u];
-#pragma unroll
-      for (int u = 0; u < BV; ++u) {
-        const int v = tid + 256 * u;
-        if (v < NTC * 64) *reinterpret_cast<bf16x8*>(base + KST * A_EL + kk * B_EL + (size_t)v * 8) = rb[kk][u];
-      }
-    }
-  };
-  auto compute_stage = [&](int buf, int nvalid) {
-    const bf16* base = lds + buf * STG_EL;
-#pragma unroll
-    for (int kk = 0; kk < KST; ++kk) {
-      if (kk < nvalid) {                              // workgroup-uniform
-        const bf16* A = base + kk * A_EL;
-        const bf16* Bb = base + KST * A_EL + kk * B_EL;
-        bf16x8 af[4], bfr[NW];
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          af[t] = *reinterpret_cast<const bf16x8*>(A + ((wm * 4 + t) * 16 + r) * LDA + 8 * g);
-#pragma unroll
-        for (int n = 0; n < NW; ++n)
-          bfr[n] = *reinterpret_cast<const bf16x8*>(Bb + ((size_t)(wn * NW + n) * 64 + lane) * 8);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int n = 0; n < NW; ++n) acc[t][n] = mfma16(af[t], bfr[n], acc[t][n]);
-      }
-    }
-  };
-  const int nst = (KS + KST - 1) / KST;
-  if (KS > 0) {
-    set_tap();
-    issue_stage();
-    store_stage(0);
   }
-  __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int cur = st & 1;
-    const bool more = st + 1 < nst;
-    if (more) issue_stage();                          // next stage's loads fly during the MFMAs
-    compute_stage(cur, KS - st * KST);
-    if (more) store_stage(cur ^ 1);                   // other buffer: last read one stage ago
-    __syncthreads();
+  __device__ int pack_ks(const ConvMMArgs& a, const TapLattice& tl) const {
+    return ((tl.ky0 + wty * a.in_dil) * a.KW + (tl.kx0 + wtx * a.in_dil)) * cps + wcs;
   }
+};
 
-  // ---- epilogue through LDS scratch (per wave: [16 rows][NW*16] fp32)
+// Shared epilogue: per wave [16 rows][NW*16] through LDS scratch, 16-byte global stores.
+template <int NTC>
+__device__ __forceinline__ void tile_epilogue(const ConvMMArgs& a, const TileRows& tr, f32x4 (&acc)[4][NTC / 2],
+                                              char* smem, long long row0, int nt0, uint32_t step) {
+  constexpr int NW = NTC / 2;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const int wm = wave & 1, wn = wave >> 1;
+  const long long nrows = tr.nrows;
   const int LDC = NW * 16;
   float* ep = reinterpret_cast<float*>(smem) + wave * 16 * LDC;
   const int cbase = (nt0 + wn * NW) * 16;              // first channel of this wave
@@ -219,7 +155,7 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(const ConvMMArgs a) {
   for (int t = 0; t < 4; ++t) {
     const long long tile = (row0 >> 4) + wm * 4 + t;  // global 16-row tile index
     if (tile * 16 >= nrows) break;
-    if (pool) {
+    if (tr.pool) {
       bf16* epb = reinterpret_cast<bf16*>(ep);
       uint8_t* epc = reinterpret_cast<uint8_t*>(epb + 4 * LDC);
       const long long q = tile * 4 + g;               // global pool-window index
@@ -264,9 +200,9 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(const ConvMMArgs a) {
       for (int c = lane; c < np * cch; c += 64) {
         const int pr = c / cch, c8 = c - pr * cch;
         size_t m = (size_t)(tile * 16 + pr);
-        if (dil > 1) {                                // parity class row -> flat output pixel
+        if (tr.dil > 1) {                             // parity class row -> flat output pixel
           int b, oy, ox;
-          row_coords((long long)m, b, oy, ox);
+          tr.coords(a, (long long)m, b, oy, ox);
           m = ((size_t)b * a.Ho + oy) * a.Wo + ox;
         }
         float v[8];
@@ -297,11 +233,236 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(const ConvMMArgs a) {
     }
   }
 }
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// LDS-DMA path.  Per k-step: A = 128 rows x 64 B = 8 wave-instructions (2 per wave), B =
+// NTC fragments x 1 KB; stage = KST k-steps, two stages in LDS.  The DMA of stage st+1 is
+// issued before the MFMAs of stage st; the stage-end __syncthreads() (which waits vmcnt(0))
+// retires it before anyone reads it.
+template <int NTC>
+__global__ __launch_bounds__(256) void conv_gl_kernel(const ConvMMArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NW = NTC / 2;
+  constexpr int A_BYTES = BM * 64;
+  constexpr int STEP_BYTES = A_BYTES + NTC * 1024;
+  constexpr int STG_BYTES = KST * STEP_BYTES;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int nt0 = blockIdx.y * NTC;
+  TileRows tr;
+  TapLattice tl;
+  tile_geometry(a, tr, tl);
+  const long long row0 = (long long)blockIdx.x * BM;
+  if (row0 >= tr.nrows) return;                       // (parity classes differ in size)
+  const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
+  const int KS = tl.KS;
+
+  // this lane's DMA slots: rows 16*(2*wave+u) + lane/4, LDS position lane&3 holding the
+  // swizzled source chunk
+  const int chunk = (lane & 3) ^ ((-(lane >> 4)) & 3);
+  Walker wk;
+  wk.init(a, tr, row0 + 16 * (2 * wave) + (lane >> 2), row0 + 16 * (2 * wave + 1) + (lane >> 2), chunk);
+  const bf16* zero = a.zero;
+
+  auto issue_stage = [&](int buf, int kl0) {
+    char* base = smem + buf * STG_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < KST; ++kk) {
+      char* sb = base + kk * STEP_BYTES;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16* src = wk.okr[u] ? wk.rowp[u] + wk.wcs * 32 : zero;
+        __builtin_amdgcn_global_load_lds(src, sb + (2 * wave + u) * 1024, 16, 0, 0);
+      }
+      const int kp = wk.pack_ks(a, tl);
+#pragma unroll
+      for (int j = 0; j < (NTC + 3) / 4; ++j) {      // fragment n = wave + 4j
+        const int n = wave + 4 * j;
+        if (NTC % 4 == 0 || n < NTC) {                // wave-uniform
+          const int nt = min(nt0 + n, a.NT - 1);     // clamped: columns past N are dropped
+          __builtin_amdgcn_global_load_lds(a.wpk + ((size_t)(kp * a.NT + nt) * 64 + lane) * 8,
+                                           sb + A_BYTES + n * 1024, 16, 0, 0);
+        }
+      }
+      if (kl0 + kk + 1 < KS) wk.next_k(a, tl);
+    }
+  };
+
+  f32x4 acc[4][NW];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < NW; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int rsw = (-(r >> 2)) & 3;                     // read-side swizzle of this lane's row
+
+  auto compute_stage = [&](int buf, int nvalid) {
+    const char* base = smem + buf * STG_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < KST; ++kk) {
+      if (kk < nvalid) {                              // workgroup-uniform
+        const char* A = base + kk * STEP_BYTES;
+        const char* Bb = A + A_BYTES;
+        bf16x8 af[4], bfr[NW];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          af[t] = *reinterpret_cast<const bf16x8*>(A + ((wm * 4 + t) * 16 + r) * 64 + ((g ^ rsw) << 4));
+#pragma unroll
+        for (int n = 0; n < NW; ++n)
+          bfr[n] = *reinterpret_cast<const bf16x8*>(Bb + ((wn * NW + n) * 64 + lane) * 16);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int n = 0; n < NW; ++n) acc[t][n] = mfma16(af[t], bfr[n], acc[t][n]);
+      }
+    }
+  };
+
+  const int nst = (KS + KST - 1) / KST;
+  if (KS > 0) {
+    wk.set_tap(a, tl);
+    issue_stage(0, 0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nst) issue_stage(cur ^ 1, (st + 1) * KST);   // buffer last read in stage st-1
+    compute_stage(cur, KS - st * KST);
+    __syncthreads();                                  // vmcnt(0): stage st+1 has landed
+  }
+  tile_epilogue<NTC>(a, tr, acc, smem, row0, nt0, step);
+}
+
+// ------------------------------------------------------------------------------------------
+// Register-staged path (unpool-on-load input).
+template <int NTC>
+__global__ __launch_bounds__(256) void conv_tile_kernel(const ConvMMArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NW = NTC / 2;                         // n-tiles per wave
+  constexpr int A_EL = BM * LDA;                      // A_s elements per k-step
+  constexpr int B_EL = NTC * 64 * 8;                  // B_s elements per k-step
+  constexpr int STG_EL = KST * (A_EL + B_EL);         // one LDS buffer = KST k-steps
+  bf16* const lds = reinterpret_cast<bf16*>(smem);    // [2][KST][A] [KST][B]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int nt0 = blockIdx.y * NTC;
+  TileRows tr;
+  TapLattice tl;
+  tile_geometry(a, tr, tl);
+  const long long row0 = (long long)blockIdx.x * BM;
+  if (row0 >= tr.nrows) return;
+  const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
+  const int KS = tl.KS, Cs = a.Cs_in;
+  const int IH = a.in_code ? a.in_pH : a.H, IW = a.in_code ? a.in_pW : a.W;
+
+  // this thread's two A-gather rows (128 rows x 4 chunks of 8 channels = 512 loads)
+  const int ach = tid & 3;
+  Walker wk;
+  wk.init(a, tr, row0 + (tid >> 2), row0 + (tid >> 2) + 64, ach);
+  auto load_a = [&](int u) -> bf16x8 {
+    if (a.in_code) {
+      const size_t boff = (size_t)wk.gb[u] * IH * IW * Cs;
+      return unpool_load8(a.x + boff, a.in_code + boff, IH, IW, Cs, wk.iyr[u], wk.ixr[u], wk.wcs * 32 + 8 * ach,
+                          wk.okr[u]);
+    }
+    return load_bf16x8_if(wk.okr[u], wk.rowp[u] + wk.wcs * 32, a.x);
+  };
+  // B gather: NTC*64 16-byte fragment vectors per k-step
+  constexpr int BV = (NTC * 64 + 255) / 256;
+  auto load_b = [&](int ksp, int u) -> bf16x8 {
+    const int v = tid + 256 * u;
+    const int nt = nt0 + (v >> 6);
+    const bool ok = v < NTC * 64 && nt < a.NT;
+    return load_bf16x8_if(ok, a.wpk + ((size_t)(ksp * a.NT + nt) * 64 + (v & 63)) * 8, a.wpk);
+  };
+  f32x4 acc[4][NW];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < NW; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // One register stage (KST k-steps) in flight while the previous stage's MFMAs run out of
+  // the other LDS buffer.  Loads are unconditional (past the last k-step the walker stays
+  // put and the extra results are simply not used): a load under a branch would make
+  // hipcc drain vmcnt at the join.
+  bf16x8 ra[KST][2], rb[KST][BV];
+  int kl = 0;                                         // k-steps issued so far
+  auto issue_stage = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < KST; ++kk) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) ra[kk][u] = load_a(u);
+      const int kp = wk.pack_ks(a, tl);
+#pragma unroll
+      for (int u = 0; u < BV; ++u) rb[kk][u] = load_b(kp, u);
+      if (++kl < KS) wk.next_k(a, tl);
+    }
+  };
+  auto store_stage = [&](int buf) {
+    bf16* base = lds + buf * STG_EL;
+#pragma unroll
+    for (int kk = 0; kk < KST; ++kk) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        *reinterpret_cast<bf16x8*>(base + kk * A_EL + ((tid >> 2) + 64 * u) * LDA + 8 * ach) = ra[kk][u];
+#pragma unroll
+      for (int u = 0; u < BV; ++u) {
+        const int v = tid + 256 * u;
+        if (v < NTC * 64) *reinterpret_cast<bf16x8*>(base + KST * A_EL + kk * B_EL + (size_t)v * 8) = rb[kk][u];
+      }
+    }
+  };
+  auto compute_stage = [&](int buf, int nvalid) {
+    const bf16* base = lds + buf * STG_EL;
+#pragma unroll
+    for (int kk = 0; kk < KST; ++kk) {
+      if (kk < nvalid) {                              // workgroup-uniform
+        const bf16* A = base + kk * A_EL;
+        const bf16* Bb = base + KST * A_EL + kk * B_EL;
+        bf16x8 af[4], bfr[NW];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          af[t] = *reinterpret_cast<const bf16x8*>(A + ((wm * 4 + t) * 16 + r) * LDA + 8 * g);
+#pragma unroll
+        for (int n = 0; n < NW; ++n)
+          bfr[n] = *reinterpret_cast<const bf16x8*>(Bb + ((size_t)(wn * NW + n) * 64 + lane) * 8);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int n = 0; n < NW; ++n) acc[t][n] = mfma16(af[t], bfr[n], acc[t][n]);
+      }
+    }
+  };
+  const int nst = (KS + KST - 1) / KST;
+  if (KS > 0) {
+    wk.set_tap(a, tl);
+    issue_stage();
+    store_stage(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    const bool more = st + 1 < nst;
+    if (more) issue_stage();                          // next stage's loads fly during the MFMAs
+    compute_stage(cur, KS - st * KST);
+    if (more) store_stage(cur ^ 1);                   // other buffer: last read one stage ago
+    __syncthreads();
+  }
+  tile_epilogue<NTC>(a, tr, acc, smem, row0, nt0, step);
+}
+
+static size_t epilogue_bytes(int ntc) { return (size_t)4 * 16 * (ntc / 2) * 16 * 4; }
+
+static size_t gl_lds_bytes(int ntc) {
+  const size_t stage = (size_t)2 * KST * (BM * 64 + ntc * 1024);
+  return stage > epilogue_bytes(ntc) ? stage : epilogue_bytes(ntc);
+}
 
 size_t conv_tile_lds_bytes(int ntc) {
   const size_t stage = (size_t)2 * KST * (BM * LDA + ntc * 64 * 8) * 2;
-  const size_t ep = (size_t)4 * 16 * (ntc / 2) * 16 * 4;
-  return stage > ep ? stage : ep;
+  const size_t reg = stage > epilogue_bytes(ntc) ? stage : epilogue_bytes(ntc);
+  const size_t gl = gl_lds_bytes(ntc);
+  return reg > gl ? reg : gl;
 }
 
 template <int NTC>
@@ -312,7 +473,10 @@ static void launch_t(const ConvMMArgs& a, hipStream_t s) {
   const long long maxrows = pool ? nrows : (long long)a.B * ((a.Ho + d - 1) / d) * ((a.Wo + d - 1) / d);
   const int gx = (int)((maxrows + BM - 1) / BM);
   const int gy = (a.NT + NTC - 1) / NTC;
-  hipLaunchKernelGGL(conv_tile_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), conv_tile_lds_bytes(NTC), s, a);
+  if (a.in_code == nullptr && a.zero != nullptr)
+    hipLaunchKernelGGL(conv_gl_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), gl_lds_bytes(NTC), s, a);
+  else
+    hipLaunchKernelGGL(conv_tile_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), conv_tile_lds_bytes(NTC), s, a);
 }
 
 void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s) {

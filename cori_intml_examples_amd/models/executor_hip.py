@@ -671,6 +671,11 @@ class BatchPlan:
             ntc = 8 if NT > 4 else (4 if NT > 2 else 2)
             if K.conv_tile_lds_bytes(ntc) > 150 * 1024:
                 raise NotImplementedError("conv tile LDS")
+            if env_flag("INTML_CONV_GLDS", True):
+                # LDS-DMA staging: padded rows read from a zero buffer (the DMA cannot zero-fill)
+                if getattr(self, "_zero16", None) is None:
+                    self._zero16 = torch.zeros(64, dtype=torch.bfloat16, device=self.ex.device)
+                a.zero = self._zero16.data_ptr()
             return lambda s, a=a, n=ntc: K.conv_tile(a, n, s)
         ntc = self._halo_cfg(a, NT, pool)
         return lambda s, a=a, n=ntc: K.conv_halo(a, n, s)
