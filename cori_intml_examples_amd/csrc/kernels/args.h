@@ -74,6 +74,9 @@ struct WgradArgs {
   int R = 1, blocks_per_split = 1;
   const uint8_t* dy_code = nullptr;
   int dHp = 0, dWp = 0;
+  // >= 16 zero bytes: LDS-DMA source of padded rows (set => wgrad_tile uses the DMA path
+  // when it applies: 8 n-tiles per workgroup, unpooled dY)
+  const bf16* zero = nullptr;
   int dbg = 0;   // ablation (timing only): 1 skip staging, 2 skip MFMA, 4 skip slab stores
 };
 

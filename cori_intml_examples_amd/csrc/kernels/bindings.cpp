@@ -73,7 +73,7 @@ PYBIND11_MODULE(_kernels, m) {
       RW(WgradArgs, pad_t) RW(WgradArgs, pad_l) RW(WgradArgs, Ktiles) PTR(WgradArgs, dy)
       RW(WgradArgs, Cs_dy) RW(WgradArgs, NT) RW(WgradArgs, P) RW(WgradArgs, px_per_split)
       RW(WgradArgs, KT) PTR(WgradArgs, slab) PTR(WgradArgs, bslab) RW(WgradArgs, R)
-      RW(WgradArgs, blocks_per_split) PTR(WgradArgs, dy_code) RW(WgradArgs, dHp) RW(WgradArgs, dWp)
+      RW(WgradArgs, blocks_per_split) PTR(WgradArgs, dy_code) PTR(WgradArgs, zero) RW(WgradArgs, dHp) RW(WgradArgs, dWp)
       RW(WgradArgs, dbg);
 
   py::class_<DenseFwdArgs>(m, "DenseFwdArgs")

@@ -202,6 +202,161 @@ __global__ __launch_bounds__(256) void wgrad_tile_kernel(const WgradArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// LDS-DMA path (NTC == 8, unpooled dY): A_s and B_s are [64 px][128] bf16 images with
+// 256-B rows filled by global_load_lds_dwordx4 (4 + 4 wave-instructions per wave per stage,
+// no VGPR staging, no ds_write), double-buffered with the DMA of stage j+1 in flight during
+// stage j's MFMAs.  The DMA destination is lane-linear, so the conflict-avoiding layout is
+// produced on the source side: the 16-B chunk c of row R sits at position c ^ h(R),
+// h(R) = 2 * ((R & 3) | ((R >> 3) & 1) << 2), which spreads each 32-lane group of a
+// ds_read_b64_tr_b16 fragment read (rows 8g + i/4 and 8g + i/4 + 4 share h) over all 64
+// banks.  Padding (outside the image, k >= K, n >= Cs_dy, pixels past the split) reads a
+// zero buffer.
+namespace {
+__device__ __forceinline__ int wg_swz(int R) { return ((R & 3) | (((R >> 3) & 1) << 2)) << 1; }
+}
+
+__global__ __launch_bounds__(256) void wgrad_gl_kernel(const WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NTC = 8, NW = 4;
+  constexpr int ROWB = 256;                       // bytes per pixel row of either image
+  constexpr int IMG = WT_PX * ROWB;               // 16 KB
+  constexpr int STG = 2 * IMG;                    // A + B per stage
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, g = lane >> 4;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int k0 = blockIdx.y * WT_MK;
+  const int nt0 = blockIdx.z * NTC;
+  const int K = a.Ktiles * 16;
+  const int Cs = a.Cs_in, s = a.stride;
+  const bool do_bias = a.bslab != nullptr && blockIdx.y == 0 && wm == 0;
+  const long long P = (long long)a.B * a.Ho * a.Wo;
+  const long long p_begin = (long long)blockIdx.x * a.px_per_split;
+  const long long p_end = min(P, p_begin + a.px_per_split);
+  const int hw = a.Ho * a.Wo;
+  const bf16* zero = a.zero;
+
+  // this lane's DMA slots, u = 0..3: row R = 16*wave + 4u + g, position i -> source chunk
+  // c = i ^ h(R); per u the chunk's (tap, channel) for A and channel for B are fixed.
+  int tky[4], tkx[4], tch[4], bn[4];
+  bool tok[4], bok[4];
+  long long pb_[4];
+  int pbb[4], pby[4], pbx[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int R = 16 * wave + 4 * u + g;
+    const int c = i ^ wg_swz(R);
+    const int k = k0 + 8 * c;
+    const int tap = k / Cs;
+    tok[u] = k < K && tap < a.KH * a.KW;
+    tky[u] = tap / a.KW;
+    tkx[u] = tap - tky[u] * a.KW;
+    tch[u] = k - tap * Cs;
+    bn[u] = nt0 * 16 + 8 * c;
+    bok[u] = bn[u] < a.Cs_dy;
+    pb_[u] = p_begin + R;
+    const long long pc = pb_[u] < P ? pb_[u] : P - 1;
+    pbb[u] = (int)(pc / hw);
+    const int rem = (int)(pc - (long long)pbb[u] * hw);
+    pby[u] = rem / a.Wo;
+    pbx[u] = rem - pby[u] * a.Wo;
+  }
+  const int adv_y = WT_PX / a.Wo, adv_x = WT_PX - (WT_PX / a.Wo) * a.Wo;
+
+  auto issue = [&](int buf) {
+    char* as_ = smem + buf * STG;
+    char* bs_ = as_ + IMG;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool pv = pb_[u] < p_end;
+      const int iy = pby[u] * s - a.pad_t + tky[u], ix = pbx[u] * s - a.pad_l + tkx[u];
+      const bool ok = pv && tok[u] && iy >= 0 && ix >= 0 && iy < a.H && ix < a.W;
+      const bf16* srca = ok ? a.x + (((size_t)pbb[u] * a.H + iy) * a.W + ix) * Cs + tch[u] : zero;
+      __builtin_amdgcn_global_load_lds(srca, as_ + (16 * wave + 4 * u) * ROWB, 16, 0, 0);
+      const bf16* srcb = pv && bok[u] ? a.dy + (size_t)pb_[u] * a.Cs_dy + bn[u] : zero;
+      __builtin_amdgcn_global_load_lds(srcb, bs_ + (16 * wave + 4 * u) * ROWB, 16, 0, 0);
+      // advance this slot's pixel by one stage
+      pb_[u] += WT_PX;
+      pbx[u] += adv_x;
+      pby[u] += adv_y;
+      if (pbx[u] >= a.Wo) { pbx[u] -= a.Wo; ++pby[u]; }
+      while (pby[u] >= a.Ho) { pby[u] -= a.Ho; ++pbb[u]; }
+    }
+  };
+
+  f32x4 acc[4][NW], bacc[NW];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < NW; ++v) acc[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int v = 0; v < NW; ++v) bacc[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = f2bf(1.f);
+
+  // fragment read addresses: rows P0 = 32ks + 8g + i/4 and P0 + 4 (same swizzle), element
+  // column 16*tile + 4*(i&3) -> chunk 2*tile + ((i&3)>>1), 8-B half (i&1)
+  auto tr_frag = [&](const char* img, int P0, int tile) -> bf16x8 {
+    const int pos = (2 * tile + ((i & 3) >> 1)) ^ wg_swz(P0);
+    const bf16* p0 = reinterpret_cast<const bf16*>(img + P0 * ROWB + pos * 16 + (i & 1) * 8);
+    const bf16* p1 = reinterpret_cast<const bf16*>(img + (P0 + 4) * ROWB + pos * 16 + (i & 1) * 8);
+    return __builtin_shufflevector(tr_read_t(p0), tr_read_t(p1), 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto mma = [&](int buf) {
+    const char* as_ = smem + buf * STG;
+    const char* bs_ = as_ + IMG;
+#pragma unroll
+    for (int ks = 0; ks < WT_PX / 32; ++ks) {
+      const int P0 = ks * 32 + 8 * g + (i >> 2);
+      bf16x8 af[4], bfr[NW];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) af[u] = tr_frag(as_, P0, wm * 4 + u);
+#pragma unroll
+      for (int v = 0; v < NW; ++v) bfr[v] = tr_frag(bs_, P0, wn * NW + v);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < NW; ++v) acc[u][v] = mfma16(af[u], bfr[v], acc[u][v]);
+      if (do_bias) {
+#pragma unroll
+        for (int v = 0; v < NW; ++v) bacc[v] = mfma16(ones, bfr[v], bacc[v]);
+      }
+    }
+  };
+  const int nstage = (int)((p_end - p_begin + WT_PX - 1) / WT_PX);
+  if (nstage > 0) issue(0);
+  __syncthreads();
+  for (int st = 0; st < nstage; ++st) {
+    if (st + 1 < nstage) issue((st & 1) ^ 1);      // buffer last read in stage st-1
+    mma(st & 1);
+    __syncthreads();                                // vmcnt(0): stage st+1 has landed
+  }
+
+  const int ld = a.NT * 16;
+  float* slab = a.slab + (size_t)blockIdx.x * K * ld;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int kr = k0 + (wm * 4 + u) * 16 + g * 4;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+      const int n = (nt0 + wn * NW + v) * 16 + i;
+      if (n >= ld) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (kr + j < K) slab[(size_t)(kr + j) * ld + n] = acc[u][v][j];
+    }
+  }
+  if (do_bias && g == 0) {
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+      const int n = (nt0 + wn * NW + v) * 16 + i;
+      if (n < ld) a.bslab[(size_t)blockIdx.x * ld + n] = bacc[v][0];
+    }
+  }
+}
+
+static size_t wgrad_gl_lds_bytes() { return (size_t)2 * 2 * WT_PX * 256; }
+
 size_t wgrad_tile_lds_bytes(int ntc) {
   return (size_t)2 * WT_PX * ((WT_MK + 8) + (ntc * 16 + 8)) * 2;
 }
@@ -212,7 +367,10 @@ static void launch_wt(const WgradArgs& a, hipStream_t s) {
   const int S = (int)((P + a.px_per_split - 1) / a.px_per_split);
   const int gy = (a.Ktiles * 16 + WT_MK - 1) / WT_MK;
   const int gz = (a.NT + NTC - 1) / NTC;
-  hipLaunchKernelGGL(wgrad_tile_kernel<NTC>, dim3(S, gy, gz), dim3(256), wgrad_tile_lds_bytes(NTC), s, a);
+  if (NTC == 8 && a.zero != nullptr && a.dy_code == nullptr)
+    hipLaunchKernelGGL(wgrad_gl_kernel, dim3(S, gy, gz), dim3(256), wgrad_gl_lds_bytes(), s, a);
+  else
+    hipLaunchKernelGGL(wgrad_tile_kernel<NTC>, dim3(S, gy, gz), dim3(256), wgrad_tile_lds_bytes(NTC), s, a);
 }
 
 void launch_wgrad_tile(const WgradArgs& a, int ntc, hipStream_t s) {

@@ -665,6 +665,12 @@ class BatchPlan:
         n-tiles than a 128-channel tile needs -> use the tiled whole-batch GEMM kernels."""
         return Cs_in % 32 == 0 and KS * min(NT, 8) > 64
 
+    def _zero_buf(self):
+        """Zero bytes for the LDS-DMA kernels: padded rows read from here (DMA cannot zero-fill)."""
+        if getattr(self, "_zero16", None) is None:
+            self._zero16 = torch.zeros(64, dtype=torch.bfloat16, device=self.ex.device)
+        return self._zero16
+
     def _conv_launch(self, a, NT, pool):
         K = self.ex.K
         if self._wide(a.Cs_in, a.KS, NT):
@@ -672,10 +678,7 @@ class BatchPlan:
             if K.conv_tile_lds_bytes(ntc) > 150 * 1024:
                 raise NotImplementedError("conv tile LDS")
             if env_flag("INTML_CONV_GLDS", True):
-                # LDS-DMA staging: padded rows read from a zero buffer (the DMA cannot zero-fill)
-                if getattr(self, "_zero16", None) is None:
-                    self._zero16 = torch.zeros(64, dtype=torch.bfloat16, device=self.ex.device)
-                a.zero = self._zero16.data_ptr()
+                a.zero = self._zero_buf().data_ptr()
             return lambda s, a=a, n=ntc: K.conv_tile(a, n, s)
         ntc = self._halo_cfg(a, NT, pool)
         return lambda s, a=a, n=ntc: K.conv_halo(a, n, s)
@@ -723,6 +726,8 @@ class BatchPlan:
         a.NT = g.NT
         ntc = 8 if g.NT > 4 else (4 if g.NT > 2 else 2)
         ntc = min(ntc, int(os.environ.get("INTML_WGRAD_TILE_NTC", ntc)))
+        if env_flag("INTML_CONV_GLDS", True):
+            a.zero = self._zero_buf().data_ptr()
         P = bs * g.Ho * g.Wo
         a.P = P
         tiles = cdiv(a.Ktiles * 16, 128) * cdiv(g.NT, ntc)
