@@ -151,7 +151,8 @@ struct OptimArgs {
   const float* g = nullptr;
   float* s0 = nullptr;
   float* s1 = nullptr;
-  int n = 0;
+  int n = 0;                     // elements [lo, lo + n) are updated (lo need not be aligned)
+  int lo = 0;
   const StepState* st = nullptr;
   int kind = 0;
   float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-7f, rho = 0.95f, momentum = 0.f;

@@ -1,3 +1,4 @@
+#include <algorithm>
 // pybind11 bindings for the gfx950 kernels.  Argument structs are exposed as Python
 // classes (pointer fields take integer device addresses, e.g. tensor.data_ptr()); the
 // launch_* functions take the HIP stream as an integer (torch stream.cuda_stream), so
@@ -110,7 +111,7 @@ PYBIND11_MODULE(_kernels, m) {
 
   py::class_<OptimArgs>(m, "OptimArgs")
       .def(py::init<>())
-      PTR(OptimArgs, p) PTR(OptimArgs, g) PTR(OptimArgs, s0) PTR(OptimArgs, s1) RW(OptimArgs, n)
+      PTR(OptimArgs, p) PTR(OptimArgs, g) PTR(OptimArgs, s0) PTR(OptimArgs, s1) RW(OptimArgs, n) RW(OptimArgs, lo)
       PTR(OptimArgs, st) RW(OptimArgs, kind) RW(OptimArgs, beta1) RW(OptimArgs, beta2) RW(OptimArgs, eps)
       RW(OptimArgs, rho) RW(OptimArgs, momentum) RW(OptimArgs, nesterov) RW(OptimArgs, grad_scale)
       RW(OptimArgs, pack_only) PTR(OptimArgs, arena);
@@ -120,6 +121,30 @@ PYBIND11_MODULE(_kernels, m) {
       .def_readonly("n", &PackTable::n)
       .def("add", [](PackTable& t, int src_off, int numel, int type, int KH, int KW, int Cin, int Cout,
                       int Cs, int NT, long long dst_off) {
+        if (type == PACK_DENSE_FWD || type == PACK_DENSE_BWD) {
+          // dense packs go to the tiled pair kernel: FWD opens a pair, BWD completes it
+          if (type == PACK_DENSE_FWD) {
+            if (t.nd >= MAX_DENSE_PAIRS) throw std::runtime_error("PackTable: too many dense layers");
+            DensePair& p = t.dp[t.nd++];
+            p.src_off = src_off; p.KHW = KH * KW; p.Cin = Cin; p.Cs = Cs; p.N = Cout;
+            p.KS = (int)(((long long)KH * KW * Cs + 31) / 32); p.NT = NT;
+            p.KSb = 0; p.NTb = 0; p.dst_fwd = dst_off; p.dst_bwd = -1;
+          } else {
+            if (t.nd == 0 || t.dp[t.nd - 1].src_off != src_off)
+              throw std::runtime_error("PackTable: dense BWD pack must follow its FWD pack");
+            DensePair& p = t.dp[t.nd - 1];
+            p.KSb = (Cout + 31) / 32; p.NTb = NT; p.dst_bwd = dst_off;
+          }
+          t.dblocks = 0;
+          for (int i = 0; i < t.nd; ++i) {
+            DensePair& p = t.dp[i];
+            const int ncols = std::max(p.NT * 16, p.KSb * 32);
+            p.ntn = (ncols + 127) / 128;
+            p.blk0 = t.dblocks;
+            t.dblocks += p.KS * p.ntn;
+          }
+          return;
+        }
         if (t.n >= MAX_PACK) throw std::runtime_error("PackTable full");
         PackDesc& d = t.d[t.n++];
         d.src_off = src_off; d.numel = numel; d.type = type; d.KH = KH; d.KW = KW; d.Cin = Cin;

@@ -181,11 +181,27 @@ struct PackDesc {
 
 #define MAX_PACK 24
 
+// A dense layer's forward and backward packs, produced together from ONE read of the
+// master by 32(k) x 128(n) tiles staged in LDS (dense_pack_kernel).
+struct DensePair {
+  int src_off;
+  int KHW, Cin, Cs, N;     // flatten source grid (H*W), channels, padded channel stride, units
+  int KS, NT;              // forward pack: 32-wide k-steps over the padded input, n-tiles over N
+  int KSb, NTb;            // backward pack (0 if none): k-steps over N, n-tiles over padded input
+  int ntn;                 // 128-column tiles
+  int blk0;
+  long long dst_fwd, dst_bwd;
+};
+
+#define MAX_DENSE_PAIRS 4
+
 struct PackTable {
   int n;
-  int nblocks;   // workgroups of the pack launch (256 vectors each)
-  int pad_[2];
+  int nblocks;   // workgroups of the generic pack launch (256 vectors each)
+  int nd;        // dense pairs
+  int dblocks;   // workgroups of the dense pack launch
   PackDesc d[MAX_PACK];
+  DensePair dp[MAX_DENSE_PAIRS];
 };
 
 // Dense flatten mapping: keras flat index (h,w,c) over C channels -> padded index over Cs.

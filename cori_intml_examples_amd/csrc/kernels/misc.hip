@@ -146,18 +146,18 @@ void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStr
 }
 
 // ---------------------------------------------------------------------------------------
-// Weight packs: one launch over every (fp32 master tensor -> bf16 fragment-major pack)
+// Conv weight packs: one launch over every (fp32 master tensor -> bf16 fragment-major pack)
 // descriptor.  A thread writes one 16-byte fragment vector -- 8 consecutive k of one n --
 // gathering its 8 sources from the Keras-layout master (the inverse of the pack layout
 // pack[((ks*NT+nt)*64+lane)*8+j] = B[32ks+8(lane>>4)+j][16nt+(lane&15)]).  Lanes of a
 // wave cover 16 consecutive n, so each gather instruction reads contiguous runs of the
-// row-major master.  Padding rows/columns become zeros.
-__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ master, bf16* __restrict__ arena,
-                                                   const PackTable tab) {
+// row-major master.  Padding rows/columns become zeros.  (Dense layers: dense_pack_kernel.)
+__device__ __forceinline__ void conv_pack_block(const float* __restrict__ master, bf16* __restrict__ arena,
+                                                const PackTable& tab, int blk) {
   int di = 0;
-  while (di + 1 < tab.n && (int)blockIdx.x >= tab.d[di + 1].blk0) ++di;
+  while (di + 1 < tab.n && blk >= tab.d[di + 1].blk0) ++di;
   const PackDesc& d = tab.d[di];
-  const int v = ((int)blockIdx.x - d.blk0) * 256 + (int)threadIdx.x;
+  const int v = (blk - d.blk0) * 256 + (int)threadIdx.x;
   if (v >= d.nvec) return;
   const int lane = v & 63;
   const int frag = v >> 6;                 // ks * NT + nt
@@ -165,38 +165,23 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ mas
   const int k0 = ks * 32 + 8 * (lane >> 4);
   const int n = nt * 16 + (lane & 15);
   const float* w = master + d.src_off;
-  // The 8 k of this vector share one tap (conv) / pixel (dense) unless Cs == 4: split the
-  // index once, then step the channel -- no per-element divisions.  Loads are unconditional
-  // from a clamped address (select afterwards) so all 8 stay in flight.
-  const bool conv = d.type == PACK_CONV_FWD || d.type == PACK_CONV_DGRAD;
-  const int kp0 = conv || d.type == PACK_DENSE_FWD ? k0 : n;   // the index split by Cs
-  int outer = kp0 / d.Cs;
-  int c = kp0 - outer * d.Cs;
+  // The 8 k of this vector share one tap unless Cs == 4: split the index once, then step
+  // the channel -- no per-element divisions.  Loads are unconditional from a clamped
+  // address (select afterwards) so all 8 stay in flight.
+  int outer = k0 / d.Cs;
+  int c = k0 - outer * d.Cs;
   const int KHW = d.KH * d.KW;
+  const bool fwd = d.type == PACK_CONV_FWD;
   float vals[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    int cj = c, oj = outer;
-    if (conv || d.type == PACK_DENSE_FWD) {          // k varies with j
-      cj = c + j;
-      if (cj >= d.Cs) { cj -= d.Cs; ++oj; }          // only when Cs == 4
-    }
-    long long idx;
-    bool ok;
-    if (conv) {
-      const int t = d.type == PACK_CONV_FWD ? oj : KHW - 1 - oj;
-      const int ci = d.type == PACK_CONV_FWD ? cj : n;
-      const int co = d.type == PACK_CONV_FWD ? n : cj;
-      ok = oj < KHW && ci < d.Cin && co < d.Cout;
-      idx = ((long long)t * d.Cin + ci) * d.Cout + co;
-    } else if (d.type == PACK_DENSE_FWD) {
-      ok = cj < d.Cin && oj < KHW && n < d.Cout;
-      idx = (long long)(oj * d.Cin + cj) * d.Cout + n;
-    } else {                                          // PACK_DENSE_BWD: k = output unit
-      const int nn = k0 + j;
-      ok = c < d.Cin && outer < KHW && nn < d.Cout;
-      idx = (long long)(outer * d.Cin + c) * d.Cout + nn;
-    }
+    int cj = c + j, oj = outer;
+    if (cj >= d.Cs) { cj -= d.Cs; ++oj; }            // only when Cs == 4
+    const int t = fwd ? oj : KHW - 1 - oj;
+    const int ci = fwd ? cj : n;
+    const int co = fwd ? n : cj;
+    const bool ok = oj < KHW && ci < d.Cin && co < d.Cout;
+    const long long idx = ((long long)t * d.Cin + ci) * d.Cout + co;
     const float x = w[ok ? idx : 0];
     vals[j] = ok ? x : 0.f;
   }
@@ -206,9 +191,82 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ mas
   *reinterpret_cast<bf16x8*>(arena + d.dst_off + (size_t)v * 8) = o;
 }
 
+// Dense pair: one workgroup = 32 padded-k rows x 128 n columns of W (Keras [k][n] fp32,
+// read once, coalesced rows) staged as bf16 in LDS; it writes the 8 forward-pack fragments
+// (8 consecutive k of one n per lane: an LDS column read) and the 8 backward-pack
+// fragments (8 consecutive n of one k: one 16-byte LDS row read) the tile covers.  Each
+// fragment store is 1 KB contiguous.  Replaces two strided gathers of the master (the
+// backward one reading 32-byte pieces of 64 different rows per instruction).
+__device__ __forceinline__ void dense_pack_block(const float* __restrict__ master, bf16* __restrict__ arena,
+                                                 const PackTable& tab, int blk, bf16 (*tile)[136]) {
+  int di = 0;
+  while (di + 1 < tab.nd && blk >= tab.dp[di + 1].blk0) ++di;
+  const DensePair& d = tab.dp[di];
+  const int local = blk - d.blk0;
+  const int kt = local / d.ntn, ntile = local - kt * d.ntn;
+  const int k0 = kt * 32, n0 = ntile * 128;
+  const int t = threadIdx.x;
+  const float* w = master + d.src_off;
+  // stage: thread -> row (t>>5) + 8*pass, 4 consecutive columns
+  const int c4 = (t & 31) * 4;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const int row = (t >> 5) + 8 * pass;
+    const int k = k0 + row;
+    const int oj = k / d.Cs, cj = k - oj * d.Cs;
+    const bool kok = cj < d.Cin && oj < d.KHW;
+    const long long rbase = (long long)(oj * d.Cin + cj) * d.N;
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = n0 + c4 + q;
+      const bool ok = kok && n < d.N;
+      const float x = w[ok ? rbase + n : 0];
+      v[q] = ok ? x : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tile[row][c4 + q] = f2bf(v[q]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int v = t + 256 * h;
+    const int f = v >> 6, l = v & 63;
+    // forward fragment (ks = kt, nt = 8*ntile + f)
+    const int nt = ntile * 8 + f;
+    if (nt < d.NT) {
+      bf16x8 o;
+      const int col = 16 * f + (l & 15), r0 = 8 * (l >> 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = tile[r0 + j][col];
+      *reinterpret_cast<bf16x8*>(arena + d.dst_fwd + ((size_t)(kt * d.NT + nt) * 64 + l) * 8) = o;
+    }
+    // backward fragment (nt' = 2*kt + (f & 1), ks' = 4*ntile + (f >> 1))
+    if (d.dst_bwd >= 0) {
+      const int ntb = 2 * kt + (f & 1), ksb = 4 * ntile + (f >> 1);
+      if (ntb < d.NTb && ksb < d.KSb) {
+        const int row = 16 * (f & 1) + (l & 15), col = 32 * (f >> 1) + 8 * (l >> 4);
+        *reinterpret_cast<bf16x8*>(arena + d.dst_bwd + ((size_t)(ksb * d.NTb + ntb) * 64 + l) * 8) =
+            *reinterpret_cast<const bf16x8*>(&tile[row][col]);
+      }
+    }
+  }
+}
+
+// One launch for both: workgroups [0, nblocks) pack conv descriptors, the rest dense pairs.
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ master, bf16* __restrict__ arena,
+                                                   const PackTable tab) {
+  __shared__ __attribute__((aligned(16))) bf16 tile[32][136];
+  if ((int)blockIdx.x >= tab.nblocks) {
+    dense_pack_block(master, arena, tab, (int)blockIdx.x - tab.nblocks, tile);
+    return;
+  }
+  conv_pack_block(master, arena, tab, (int)blockIdx.x);
+}
+
 void launch_pack(const float* master, bf16* arena, const PackTable& tab, hipStream_t s) {
-  if (tab.nblocks <= 0) return;
-  hipLaunchKernelGGL(pack_kernel, dim3(tab.nblocks), dim3(256), 0, s, master, arena, tab);
+  const int blocks = tab.nblocks + tab.dblocks;
+  if (blocks > 0) hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, s, master, arena, tab);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -256,20 +314,31 @@ __device__ __forceinline__ void opt_update(const OptimArgs& a, const StepState* 
   }
 }
 
+// The range [lo, lo + n) is processed in aligned float4 groups from lo & ~3; elements of a
+// boundary group outside the range are written back unchanged (no other kernel writes them
+// concurrently: the per-bucket optimizer launches of one step are stream-ordered).
 template <int KIND>
 __global__ __launch_bounds__(256) void optim_kernel(const OptimArgs a) {
-  const int e = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (e >= a.n) return;
+  const int base = a.lo & ~3, end = a.lo + a.n;
+  const int e = base + (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (e >= end) return;
   const StepState* st = a.st;
   float4 p = *reinterpret_cast<const float4*>(a.p + e);
   const float4 g = *reinterpret_cast<const float4*>(a.g + e);
   float4 s0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : float4{0.f, 0.f, 0.f, 0.f};
   float4 s1 = a.s1 ? *reinterpret_cast<const float4*>(a.s1 + e) : float4{0.f, 0.f, 0.f, 0.f};
   const float gs = a.grad_scale;
-  opt_update<KIND>(a, st, p.x, g.x * gs, &s0.x, &s1.x);
-  opt_update<KIND>(a, st, p.y, g.y * gs, &s0.y, &s1.y);
-  opt_update<KIND>(a, st, p.z, g.z * gs, &s0.z, &s1.z);
-  opt_update<KIND>(a, st, p.w, g.w * gs, &s0.w, &s1.w);
+  if (e >= a.lo && e + 4 <= end) {
+    opt_update<KIND>(a, st, p.x, g.x * gs, &s0.x, &s1.x);
+    opt_update<KIND>(a, st, p.y, g.y * gs, &s0.y, &s1.y);
+    opt_update<KIND>(a, st, p.z, g.z * gs, &s0.z, &s1.z);
+    opt_update<KIND>(a, st, p.w, g.w * gs, &s0.w, &s1.w);
+  } else {
+    if (e >= a.lo && e < end) opt_update<KIND>(a, st, p.x, g.x * gs, &s0.x, &s1.x);
+    if (e + 1 >= a.lo && e + 1 < end) opt_update<KIND>(a, st, p.y, g.y * gs, &s0.y, &s1.y);
+    if (e + 2 >= a.lo && e + 2 < end) opt_update<KIND>(a, st, p.z, g.z * gs, &s0.z, &s1.z);
+    if (e + 3 >= a.lo && e + 3 < end) opt_update<KIND>(a, st, p.w, g.w * gs, &s0.w, &s1.w);
+  }
   *reinterpret_cast<float4*>(a.p + e) = p;
   if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
   if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
@@ -277,7 +346,8 @@ __global__ __launch_bounds__(256) void optim_kernel(const OptimArgs a) {
 
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s) {
   if (a.n > 0 && !a.pack_only) {
-    const dim3 grid(((a.n + 3) / 4 + 255) / 256);
+    const int span = a.lo + a.n - (a.lo & ~3);
+    const dim3 grid(((span + 3) / 4 + 255) / 256);
     switch (a.kind) {
       case OPT_ADAM: hipLaunchKernelGGL(optim_kernel<OPT_ADAM>, grid, dim3(256), 0, s, a); break;
       case OPT_NADAM: hipLaunchKernelGGL(optim_kernel<OPT_NADAM>, grid, dim3(256), 0, s, a); break;

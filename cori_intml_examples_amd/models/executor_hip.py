@@ -14,6 +14,7 @@ reductions.  Metrics accumulate on the device; the host syncs once per epoch.
 """
 from __future__ import annotations
 
+import gc
 import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
@@ -194,7 +195,17 @@ class HipExecutor(Executor):
     def _build_packs(self):
         K = self.K
         st = self.store
-        tab = K.PackTable()
+        self.pack_descs = []          # descriptor tuples, for per-bucket pack tables
+
+        class _Tab:
+            def __init__(self, outer):
+                self.t, self.outer = K.PackTable(), outer
+
+            def add(self, *d):
+                self.t.add(*d)
+                self.outer.pack_descs.append(d)
+
+        tab = _Tab(self)
         off = 0
 
         def alloc(ks, nt):
@@ -218,7 +229,7 @@ class HipExecutor(Executor):
             if g.KSb:
                 g.pack_bwd = alloc(g.KSb, g.NTb)
                 tab.add(sp.offset, sp.numel, PACK_DENSE_BWD, g.src.H, g.src.W, g.src.C, g.N, g.src.Cs, g.NTb, g.pack_bwd)
-        self.pack_table = tab
+        self.pack_table = tab.t
         self.arena = torch.zeros(max(off, 8), dtype=BF16, device=self.device)
 
     # ------------------------------------------------------------------ params / optimizer
@@ -392,6 +403,14 @@ class BatchPlan:
         self.graph = None
         self.dp_graphs = None
         self.side = torch.cuda.Stream(device=dev) if env_flag("INTML_TWO_STREAMS", False) else None
+        # opt-in: per-bucket optimizer (+ weight re-pack) on its own stream as soon as the
+        # bucket's gradients are final and no later backward kernel reads its packs, so the
+        # dense layer's update overlaps the conv backward.  Measured slower on one MI355X
+        # (the memory-bound update steals HBM bandwidth from the concurrent wgrad and the
+        # split launches cost more than they hide: RPV 200 -> 229 us, legacy 1.42 -> 1.44 ms)
+        self.early_optim = self.training and env_flag("INTML_EARLY_OPTIM", False)
+        self.opt_stream = torch.cuda.Stream(device=dev) if self.early_optim else None
+        self.opt_at = []
         z = lambda *s, dt=BF16: torch.zeros(*s, dtype=dt, device=dev)
         self.xb = z(bs, ex.in_H * ex.in_W * ex.in_Cs)
         self.yb = z(bs, ex.plan.head.N, dt=torch.float32)
@@ -569,6 +588,7 @@ class BatchPlan:
 
         # ---------------- backward
         self.red_groups = []       # (lo, hi, [desc tuples]) in backward order
+        self.pack_readers = []     # (launch name, param lo, hi): backward launches reading a layer's pack
         self.red_ready = []        # launch count after which each group's partial slabs are final
         hw = store.spec(hd.dense, "kernel")
         descs = [(self.head_wslab.data_ptr(), hd.K * hd.N, self.head_blocks, hd.N, hw.offset, hw.numel,
@@ -617,6 +637,7 @@ class BatchPlan:
                 a.st = st_ptr
                 a.bt = self._bt_for(g.src)
                 self.launches.append(("dense_dx%d" % g.j, lambda s, a=a: K.dense_fwd(a, s)))
+                self.pack_readers.append(("dense_dx%d" % g.j, sp.offset, sp.offset + sp.numel))
 
         for g, cs in reversed(list(zip(ex.convs, ex.plan.convs))):
             xin = self.xb if g.i == 0 else self.conv_out[g.i - 1]
@@ -657,6 +678,7 @@ class BatchPlan:
                 a.st = st_ptr
                 a.bt = self._bt_for(Src("conv", prev.i, prev.Cout, prev.Cs_out, prev.Hp, prev.Wp))
                 self.launches.append(("dgrad_conv%d" % g.i, self._conv_launch(a, g.NTd, False)))
+                self.pack_readers.append(("dgrad_conv%d" % g.i, sp.offset, sp.offset + sp.numel))
         self._build_reduce()
 
     @staticmethod
@@ -869,6 +891,44 @@ class BatchPlan:
             self.bucket_ready[k] = len(launches)
         launches.extend(self.launches[pos:])
         self.launches = launches
+        if self.early_optim:
+            self._insert_optim()
+
+    def _insert_optim(self):
+        """One ("optim_b<k>", ..., "opt") launch per bucket at the first point where the
+        bucket's gradients are final (its slab reduction) and every backward launch that
+        reads one of its layers' packs (dense dX, conv dgrad) has been issued."""
+        K = self.ex.K
+        index = {item[0]: i for i, item in enumerate(self.launches)}
+        forks = []
+        self.opt_tables = []
+        for k, (lo, hi, _) in enumerate(self.bucket_tables):
+            at = self.bucket_ready[k]
+            for name, rlo, rhi in self.pack_readers:
+                if rlo < hi and rhi > lo:
+                    at = max(at, index[name] + 1)
+            forks.append((at, k))
+            tab = K.PackTable()
+            for d in self.ex.pack_descs:
+                if lo <= d[0] < hi:
+                    tab.add(*d)
+            self.opt_tables.append(tab)
+        launches, pos = [], 0
+        self.opt_at = [0] * len(forks)
+        for at, k in sorted(forks):
+            launches.extend(self.launches[pos:at])
+            pos = at
+            self.opt_at[k] = len(launches)
+            launches.append(("optim_b%d" % k, lambda s, k=k: self._launch_optim_bucket(k, s), "opt"))
+        launches.extend(self.launches[pos:])
+        self.launches = launches
+
+    def _launch_optim_bucket(self, k, s):
+        ex = self.ex
+        lo, hi, _ = self.bucket_tables[k]
+        a = ex._optim_args(False)           # built at launch/capture time: current grad_scale
+        a.lo, a.n = lo, hi - lo
+        ex.K.optim(a, self.opt_tables[k], s)
 
     # ---------------------------------------------------------------- execution
     def _run_seq(self, lo: int = 0, hi: Optional[int] = None):
@@ -876,21 +936,32 @@ class BatchPlan:
         (weight gradients, slab reductions) on the side stream, each after the latest main
         launch before it -- the two chains run concurrently and join at the end."""
         main = torch.cuda.current_stream()
-        side_used = False
+        side_used = opt_used = False
         main_moved = True
         for item in self.launches[lo:hi]:
             name, fn = item[0], item[1]
-            if len(item) > 2 and item[2] == "side" and self.side is not None:
+            tag = item[2] if len(item) > 2 else "main"
+            if tag == "side" and self.side is not None:
                 if main_moved:
                     self.side.wait_stream(main)
                     main_moved = False
                 fn(self.side.cuda_stream)
                 side_used = True
+            elif tag == "opt":
+                if self.opt_stream is None:
+                    continue
+                self.opt_stream.wait_stream(main)
+                if side_used:
+                    self.opt_stream.wait_stream(self.side)
+                fn(self.opt_stream.cuda_stream)
+                opt_used = True
             else:
                 fn(main.cuda_stream)
                 main_moved = True
         if side_used:
             main.wait_stream(self.side)
+        if opt_used:
+            main.wait_stream(self.opt_stream)
 
     def _launch_bucket_reduce(self, k, s):
         lo, hi, tab = self.bucket_tables[k]
@@ -902,16 +973,22 @@ class BatchPlan:
 
     def _body(self, with_optim: bool):
         self._run_seq()
-        if self.training and with_optim:
+        if self.training and with_optim and not self.early_optim:
             self._launch_optim()
 
     def _dp_segments(self):
         """[(launch_lo, launch_hi, bucket)]: segment k ends with the slab reduction that
-        completes bucket k; a trailing (lo, hi, None) segment holds any later launches."""
+        completes bucket k (with the early optimizer: at bucket k's optimizer launch, which is
+        left out of the segments); a trailing (lo, hi, None) segment holds any later launches."""
         segs, lo = [], 0
-        for k, ready in enumerate(self.bucket_ready):
-            segs.append((lo, ready, k))
-            lo = ready
+        if self.early_optim:
+            for at, k in sorted((at, k) for k, at in enumerate(self.opt_at)):
+                segs.append((lo, at, k))
+                lo = at + 1
+        else:
+            for k, ready in enumerate(self.bucket_ready):
+                segs.append((lo, ready, k))
+                lo = ready
         if lo < len(self.launches):
             segs.append((lo, len(self.launches), None))
         return segs
@@ -935,6 +1012,9 @@ class BatchPlan:
         # the fused optimizer (with the 1/size average folded in) runs after the last wait.
         ex.grad_scale = 1.0 / ex.reducer.size
         segs = self._dp_segments()
+        if self.early_optim:
+            self._run_dp_early(segs)
+            return
         if ex.use_graphs and self.dp_graphs is None:
             self.dp_graphs = [self._capture(lambda a=lo, b=hi, k=k: self._run_segment(a, b, k))
                               for lo, hi, k in segs]
@@ -952,11 +1032,48 @@ class BatchPlan:
         else:
             self._launch_optim()
 
+    def _run_dp_early(self, segs):
+        """DP with per-bucket optimizers: after segment k, bucket k's all-reduce is issued
+        (RCCL orders it after the segment) and the optimizer stream waits for exactly that
+        all-reduce, then updates + re-packs the bucket while the main stream replays the
+        remaining backward."""
+        ex = self.ex
+        main = torch.cuda.current_stream()
+        if ex.use_graphs and self.dp_graphs is None:
+            self.dp_graphs = [self._capture(lambda a=lo, b=hi, k=k: self._run_segment(a, b, k))
+                              for lo, hi, k in segs]
+            self.opt_graphs = [self._capture(lambda k=k: self._launch_optim_bucket(
+                k, torch.cuda.current_stream().cuda_stream)) for k in range(len(self.opt_at))]
+        for j, (lo, hi, k) in enumerate(segs):
+            if ex.use_graphs:
+                self.dp_graphs[j].replay()
+            else:
+                self._run_segment(lo, hi, k)
+            if k is None:
+                continue
+            ex.reducer.start(k, ex.store.grad)
+            with torch.cuda.stream(self.opt_stream):
+                ex.reducer.wait(k)
+                if ex.use_graphs:
+                    self.opt_graphs[k].replay()
+                else:
+                    self._launch_optim_bucket(k, self.opt_stream.cuda_stream)
+        main.wait_stream(self.opt_stream)
+
     def _capture(self, fn):
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=self.ex.device)
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.graph(g, stream=s):
-            fn()
+        # no Python GC inside the capture: collecting an unreachable plan of another model
+        # destroys its graphs/events, which HIP forbids while a stream is capturing (abort)
+        gc_was = gc.isenabled()
+        gc.collect()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g, stream=s):
+                fn()
+        finally:
+            if gc_was:
+                gc.enable()
         torch.cuda.current_stream().wait_stream(s)
         return g

@@ -228,7 +228,7 @@ class GradReducer:
         self.size = size()
         self.buckets: List[Tuple[int, int]] = [(0, store.numel)]
         self.bucket_groups: List[List[int]] = [[0]]
-        self._pending = []
+        self._pending = {}                  # bucket -> (work, bf16 buffer or None, view)
 
     def configure(self, groups: Sequence[Tuple[int, int]]) -> List[List[int]]:
         """Merge backward-ordered groups into buckets; returns group indices per bucket."""
@@ -259,18 +259,25 @@ class GradReducer:
         if self.compression == "bf16":
             buf = view.to(torch.bfloat16)
             work = tdist.all_reduce(buf, async_op=True)
-            self._pending.append((work, buf, view))
+            self._pending[bucket] = (work, buf, view)
         else:
             work = tdist.all_reduce(view, async_op=True)
-            self._pending.append((work, None, None))
+            self._pending[bucket] = (work, None, None)
+
+    def wait(self, bucket: int) -> None:
+        """Make the current stream wait for one bucket's all-reduce (and decompress it)."""
+        item = self._pending.pop(bucket, None)
+        if item is None:
+            return
+        work, buf, view = item
+        work.wait()
+        if buf is not None:
+            view.copy_(buf.to(torch.float32))
 
     def finish(self) -> None:
         """Make the current stream wait for every in-flight bucket."""
-        for work, buf, view in self._pending:
-            work.wait()
-            if buf is not None:
-                view.copy_(buf.to(torch.float32))
-        self._pending.clear()
+        for bucket in sorted(self._pending):
+            self.wait(bucket)
 
     def reduce_all(self, grad: torch.Tensor, average: bool = True) -> None:
         for i in range(len(self.buckets)):
