@@ -236,17 +236,26 @@ __device__ __forceinline__ void tile_epilogue(const ConvMMArgs& a, const TileRow
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
-// LDS-DMA path.  Per k-step: A = 128 rows x 64 B = 8 wave-instructions (2 per wave), B =
-// NTC fragments x 1 KB; stage = KST k-steps, two stages in LDS.  The DMA of stage st+1 is
-// issued before the MFMAs of stage st; the stage-end __syncthreads() (which waits vmcnt(0))
-// retires it before anyone reads it.
+// LDS-DMA path (NTC 4 or 8).  Per k-step: A = 128 rows x 64 B = 8 wave-instructions (2 per
+// wave), B = NTC fragments x 1 KB (NTC/4 per wave).  A ring of GL_NBUF one-k-step buffers
+// keeps GL_DIST k-steps of DMA in flight: iteration st waits (counted vmcnt, never 0 in
+// the loop) for its own stage-st DMA, passes a raw s_barrier (every wave's stage st has
+// landed and every wave has finished computing stage st-1), re-issues the freed buffer
+// with stage st+GL_DIST, then runs stage st's MFMAs.  (__syncthreads() would drain vmcnt to
+// 0 and serialise the ring: one k-step of latency per k-step, the previous 2-buffer form.)
+namespace {
+constexpr int GL_NBUF = 4;
+constexpr int GL_DIST = GL_NBUF - 1;
+}
+
 template <int NTC>
 __global__ __launch_bounds__(256) void conv_gl_kernel(const ConvMMArgs a) {
+  static_assert(NTC % 4 == 0, "uniform per-wave DMA count needs NTC % 4 == 0");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NW = NTC / 2;
   constexpr int A_BYTES = BM * 64;
   constexpr int STEP_BYTES = A_BYTES + NTC * 1024;
-  constexpr int STG_BYTES = KST * STEP_BYTES;
+  constexpr int PER_STEP = 2 + NTC / 4;               // DMA instructions per wave per k-step
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
   const int wm = wave & 1, wn = wave >> 1;
   const int nt0 = blockIdx.y * NTC;
@@ -265,28 +274,23 @@ __global__ __launch_bounds__(256) void conv_gl_kernel(const ConvMMArgs a) {
   wk.init(a, tr, row0 + 16 * (2 * wave) + (lane >> 2), row0 + 16 * (2 * wave + 1) + (lane >> 2), chunk);
   const bf16* zero = a.zero;
 
-  auto issue_stage = [&](int buf, int kl0) {
-    char* base = smem + buf * STG_BYTES;
+  // issue k-step k (the walker's current position) into ring slot k % GL_NBUF
+  auto issue = [&](int k) {
+    char* sb = smem + (k % GL_NBUF) * STEP_BYTES;
 #pragma unroll
-    for (int kk = 0; kk < KST; ++kk) {
-      char* sb = base + kk * STEP_BYTES;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const bf16* src = wk.okr[u] ? wk.rowp[u] + wk.wcs * 32 : zero;
-        __builtin_amdgcn_global_load_lds(src, sb + (2 * wave + u) * 1024, 16, 0, 0);
-      }
-      const int kp = wk.pack_ks(a, tl);
-#pragma unroll
-      for (int j = 0; j < (NTC + 3) / 4; ++j) {      // fragment n = wave + 4j
-        const int n = wave + 4 * j;
-        if (NTC % 4 == 0 || n < NTC) {                // wave-uniform
-          const int nt = min(nt0 + n, a.NT - 1);     // clamped: columns past N are dropped
-          __builtin_amdgcn_global_load_lds(a.wpk + ((size_t)(kp * a.NT + nt) * 64 + lane) * 8,
-                                           sb + A_BYTES + n * 1024, 16, 0, 0);
-        }
-      }
-      if (kl0 + kk + 1 < KS) wk.next_k(a, tl);
+    for (int u = 0; u < 2; ++u) {
+      const bf16* src = wk.okr[u] ? wk.rowp[u] + wk.wcs * 32 : zero;
+      __builtin_amdgcn_global_load_lds(src, sb + (2 * wave + u) * 1024, 16, 0, 0);
     }
+    const int kp = wk.pack_ks(a, tl);
+#pragma unroll
+    for (int j = 0; j < NTC / 4; ++j) {              // fragment n = wave + 4j
+      const int n = wave + 4 * j;
+      const int nt = min(nt0 + n, a.NT - 1);         // clamped: columns past N are dropped
+      __builtin_amdgcn_global_load_lds(a.wpk + ((size_t)(kp * a.NT + nt) * 64 + lane) * 8,
+                                       sb + A_BYTES + n * 1024, 16, 0, 0);
+    }
+    if (k + 1 < KS) wk.next_k(a, tl);
   };
 
   f32x4 acc[4][NW];
@@ -296,40 +300,34 @@ __global__ __launch_bounds__(256) void conv_gl_kernel(const ConvMMArgs a) {
     for (int n = 0; n < NW; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int rsw = (-(r >> 2)) & 3;                     // read-side swizzle of this lane's row
 
-  auto compute_stage = [&](int buf, int nvalid) {
-    const char* base = smem + buf * STG_BYTES;
+  if (KS > 0) wk.set_tap(a, tl);
 #pragma unroll
-    for (int kk = 0; kk < KST; ++kk) {
-      if (kk < nvalid) {                              // workgroup-uniform
-        const char* A = base + kk * STEP_BYTES;
-        const char* Bb = A + A_BYTES;
-        bf16x8 af[4], bfr[NW];
+  for (int k = 0; k < GL_DIST; ++k)
+    if (k < KS) issue(k);
+  for (int st = 0; st < KS; ++st) {
+    // own DMA of stage st retired: later stages issued so far = min(GL_DIST-1, KS-1-st)
+    const int later = min(GL_DIST - 1, KS - 1 - st);
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PER_STEP) : "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PER_STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (st + GL_DIST < KS) issue(st + GL_DIST);        // slot of stage st-1: free after the barrier
+    const char* A = smem + (st % GL_NBUF) * STEP_BYTES;
+    const char* Bb = A + A_BYTES;
+    bf16x8 af[4], bfr[NW];
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          af[t] = *reinterpret_cast<const bf16x8*>(A + ((wm * 4 + t) * 16 + r) * 64 + ((g ^ rsw) << 4));
+    for (int t = 0; t < 4; ++t)
+      af[t] = *reinterpret_cast<const bf16x8*>(A + ((wm * 4 + t) * 16 + r) * 64 + ((g ^ rsw) << 4));
 #pragma unroll
-        for (int n = 0; n < NW; ++n)
-          bfr[n] = *reinterpret_cast<const bf16x8*>(Bb + ((wn * NW + n) * 64 + lane) * 16);
+    for (int n = 0; n < NW; ++n)
+      bfr[n] = *reinterpret_cast<const bf16x8*>(Bb + ((wn * NW + n) * 64 + lane) * 16);
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int n = 0; n < NW; ++n) acc[t][n] = mfma16(af[t], bfr[n], acc[t][n]);
-      }
-    }
-  };
-
-  const int nst = (KS + KST - 1) / KST;
-  if (KS > 0) {
-    wk.set_tap(a, tl);
-    issue_stage(0, 0);
+      for (int n = 0; n < NW; ++n) acc[t][n] = mfma16(af[t], bfr[n], acc[t][n]);
   }
-  __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int cur = st & 1;
-    if (st + 1 < nst) issue_stage(cur ^ 1, (st + 1) * KST);   // buffer last read in stage st-1
-    compute_stage(cur, KS - st * KST);
-    __syncthreads();                                  // vmcnt(0): stage st+1 has landed
-  }
+  __syncthreads();                                    // ring reads done before epilogue scratch reuse
   tile_epilogue<NTC>(a, tr, acc, smem, row0, nt0, step);
 }
 
@@ -454,7 +452,7 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(const ConvMMArgs a) {
 static size_t epilogue_bytes(int ntc) { return (size_t)4 * 16 * (ntc / 2) * 16 * 4; }
 
 static size_t gl_lds_bytes(int ntc) {
-  const size_t stage = (size_t)2 * KST * (BM * 64 + ntc * 1024);
+  const size_t stage = (size_t)GL_NBUF * (BM * 64 + ntc * 1024);
   return stage > epilogue_bytes(ntc) ? stage : epilogue_bytes(ntc);
 }
 
@@ -473,10 +471,13 @@ static void launch_t(const ConvMMArgs& a, hipStream_t s) {
   const long long maxrows = pool ? nrows : (long long)a.B * ((a.Ho + d - 1) / d) * ((a.Wo + d - 1) / d);
   const int gx = (int)((maxrows + BM - 1) / BM);
   const int gy = (a.NT + NTC - 1) / NTC;
-  if (a.in_code == nullptr && a.zero != nullptr)
-    hipLaunchKernelGGL(conv_gl_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), gl_lds_bytes(NTC), s, a);
-  else
-    hipLaunchKernelGGL(conv_tile_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), conv_tile_lds_bytes(NTC), s, a);
+  if constexpr (NTC % 4 == 0) {
+    if (a.in_code == nullptr && a.zero != nullptr) {
+      hipLaunchKernelGGL(conv_gl_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), gl_lds_bytes(NTC), s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL(conv_tile_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), conv_tile_lds_bytes(NTC), s, a);
 }
 
 void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s) {
