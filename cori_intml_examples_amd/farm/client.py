@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import threading
 import time
+from multiprocessing import AuthenticationError
 from multiprocessing.connection import Client as _Conn
 from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Union
 
@@ -327,7 +328,9 @@ class Client:
             try:
                 self._conn = _Conn(info["address"], authkey=P.authkey(info))
                 break
-            except (FileNotFoundError, ConnectionRefusedError):
+            except (OSError, EOFError, AuthenticationError):
+                # not listening yet, or a handshake cut short (controller busy / restarting):
+                # transient until the deadline
                 if time.time() > deadline:
                     raise TimeoutError("farm controller for %r is not accepting connections" % self.cluster_id)
                 time.sleep(0.2)

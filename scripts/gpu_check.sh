@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 600 python -m pytest tests -q -m gpu -x ${PYTEST_ARGS} > gpurun_out/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -v -m gpu -x --timeout 120 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/tests.log 2>&1
 echo "pytest exit $?" >> gpurun_out/tests.log
 tail -n 5 gpurun_out/tests.log
 timeout -k 10 300 python bench.py --steps 200 --warmup 30 ${BENCH_ARGS} > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -n 20 gpurun_out/bench.log; exit 1; }
