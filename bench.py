@@ -53,19 +53,21 @@ def main():
     os.environ.setdefault("INTML_DEVICE", str(dev))
 
     B = args.batch
+    # INTML_DP_FORCE=1 runs the full data-parallel step (RCCL all-reduces in the graph) at N=1
+    dp = size > 1 or os.environ.get("INTML_DP_FORCE", "0") not in ("0", "")
     if args.model == "rpv":
         model = zoo.rpv_cnn((64, 64, args.channels), conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.2,
-                            optimizer="Adam", lr=0.001 * size, use_horovod=size > 1, device=dev)
+                            optimizer="Adam", lr=0.001 * size, use_horovod=dp, device=dev)
         shape, ncls = (64, 64, args.channels), 1
         cfg_name = "RPV CNN conv[16,32,64] fc[128] 64x64x%d (DistTrain_rpv)" % args.channels
         metric, baseline = "images/sec (whole node) RPV CNN training", BASELINE_IMG_PER_S
     elif args.model == "mnist":
-        model = zoo.mnist_cnn(32, 64, 128, 0.25, 0.5, lr=1.0 * size, use_horovod=size > 1, device=dev)
+        model = zoo.mnist_cnn(32, 64, 128, 0.25, 0.5, lr=1.0 * size, use_horovod=dp, device=dev)
         shape, ncls = (28, 28, 1), 10
         cfg_name = "MNIST CNN 32-64-128 (DistTrain_mnist)"
         metric, baseline = "images/sec (whole node) MNIST CNN training", BASELINE_MNIST_IMG_PER_S
     else:
-        model = zoo.rpv_legacy_cnn((64, 64, args.channels), device=dev, use_horovod=size > 1)
+        model = zoo.rpv_legacy_cnn((64, 64, args.channels), device=dev, use_horovod=dp)
         shape, ncls = (64, 64, args.channels), 1
         cfg_name = "RPV legacy CNN 34.5M (Train_rpv)"
         metric, baseline = "images/sec (whole node) RPV legacy CNN training", BASELINE_IMG_PER_S

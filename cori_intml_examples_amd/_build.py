@@ -95,8 +95,25 @@ def build_h5(verbose=False):
     return out
 
 
+def comm_so_path():
+    return os.path.join(HERE, "_comm" + EXT)
+
+
+def build_comm(verbose=False):
+    """RCCL data-plane engine.  Links librccl.so.1 (same SONAME as the copy PyTorch loads,
+    so one RCCL instance serves the process)."""
+    src = os.path.join(CSRC, "comm", "engine.cpp")
+    out = comm_so_path()
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    if _newer(out, [src]):
+        _run([HIPCC, "-O2", "-shared", "-fPIC", "-std=c++17", "-x", "hip", "--offload-arch=" + ARCH,
+              src, "-o", out, "-I" + os.path.join(rocm, "include")] + _py_includes()
+             + ["-L" + os.path.join(rocm, "lib"), "-lrccl", "-lpthread"], verbose)
+    return out
+
+
 def build_all(verbose=False):
-    outs = [build_kernels(verbose)]
+    outs = [build_kernels(verbose), build_comm(verbose)]
     h5 = build_h5(verbose)
     if h5:
         outs.append(h5)
@@ -110,7 +127,7 @@ def main(argv=None):
     a = ap.parse_args(argv)
     if a.clean:
         shutil.rmtree(BUILD, ignore_errors=True)
-        for p in (kernels_so_path(), h5_so_path()):
+        for p in (kernels_so_path(), h5_so_path(), comm_so_path()):
             if os.path.exists(p):
                 os.remove(p)
     for o in build_all(a.verbose):

@@ -411,6 +411,12 @@ class BatchPlan:
         self.early_optim = self.training and env_flag("INTML_EARLY_OPTIM", False)
         self.opt_stream = torch.cuda.Stream(device=dev) if self.early_optim else None
         self.opt_at = []
+        # Native RCCL data plane: the bucket all-reduces are part of the launch sequence (on
+        # their own comm stream) and captured with the rest of the step into ONE HIP graph.
+        red = ex.reducer
+        self.comm_in_graph = (self.training and red is not None and getattr(red, "capturable", False)
+                              and red.active and env_flag("INTML_COMM_CAPTURE", True))
+        self.comm_stream = torch.cuda.Stream(device=dev) if self.comm_in_graph else None
         z = lambda *s, dt=BF16: torch.zeros(*s, dtype=dt, device=dev)
         self.xb = z(bs, ex.in_H * ex.in_W * ex.in_Cs)
         self.yb = z(bs, ex.plan.head.N, dt=torch.float32)
@@ -888,6 +894,8 @@ class BatchPlan:
             launches.extend(self.launches[pos:at])
             pos = at
             launches.append(("reduce_b%d" % k, lambda s, k=k: self._launch_bucket_reduce(k, s), "side"))
+            if self.comm_in_graph:
+                launches.append(("allreduce_b%d" % k, lambda s, k=k: reducer.launch(k, ex.store.grad, s), "comm"))
             self.bucket_ready[k] = len(launches)
         launches.extend(self.launches[pos:])
         self.launches = launches
@@ -936,7 +944,7 @@ class BatchPlan:
         (weight gradients, slab reductions) on the side stream, each after the latest main
         launch before it -- the two chains run concurrently and join at the end."""
         main = torch.cuda.current_stream()
-        side_used = opt_used = False
+        side_used = opt_used = comm_used = False
         main_moved = True
         for item in self.launches[lo:hi]:
             name, fn = item[0], item[1]
@@ -953,8 +961,19 @@ class BatchPlan:
                 self.opt_stream.wait_stream(main)
                 if side_used:
                     self.opt_stream.wait_stream(self.side)
+                if comm_used:
+                    self.opt_stream.wait_stream(self.comm_stream)
                 fn(self.opt_stream.cuda_stream)
                 opt_used = True
+            elif tag == "comm":
+                # fork: the comm stream follows everything issued so far (the bucket's slab
+                # reduction), RCCL runs there while the main stream continues the backward
+                cs = self.comm_stream
+                cs.wait_stream(main)
+                if side_used:
+                    cs.wait_stream(self.side)
+                fn(cs)
+                comm_used = True
             else:
                 fn(main.cuda_stream)
                 main_moved = True
@@ -962,6 +981,8 @@ class BatchPlan:
             main.wait_stream(self.side)
         if opt_used:
             main.wait_stream(self.opt_stream)
+        if comm_used:
+            main.wait_stream(self.comm_stream)
 
     def _launch_bucket_reduce(self, k, s):
         lo, hi, tab = self.bucket_tables[k]
@@ -998,19 +1019,25 @@ class BatchPlan:
 
     def run(self):
         ex = self.ex
-        dp = self.training and ex.reducer is not None and ex.reducer.size > 1
-        if not dp:
+        dp = self.training and ex.reducer is not None and ex.reducer.active
+        if dp:
+            ex.grad_scale = 1.0 / ex.reducer.size
+        if not dp or self.comm_in_graph:
+            # single launch sequence; with the native RCCL engine it includes the bucket
+            # all-reduces on the comm stream (one graph replay per DP step)
             if not ex.use_graphs:
                 self._body(with_optim=True)
-                return
-            if self.graph is None:
-                self.graph = self._capture(lambda: self._body(with_optim=True))
-            self.graph.replay()
+            else:
+                if self.graph is None:
+                    self.graph = self._capture(lambda: self._body(with_optim=True))
+                self.graph.replay()
+            if dp:
+                ex.reducer.after_step()
             return
-        # Data parallel: each bucket's all-reduce is issued as soon as its slab reduction
-        # is done, so RCCL moves the dense bucket over xGMI while the conv backward runs;
-        # the fused optimizer (with the 1/size average folded in) runs after the last wait.
-        ex.grad_scale = 1.0 / ex.reducer.size
+        # Data parallel, torch.distributed data plane: each bucket's all-reduce is issued
+        # between graph segments as soon as its slab reduction is done, so RCCL moves the
+        # dense bucket over xGMI while the conv backward runs; the fused optimizer (with the
+        # 1/size average folded in) runs after the last wait.
         segs = self._dp_segments()
         if self.early_optim:
             self._run_dp_early(segs)
@@ -1070,7 +1097,8 @@ class BatchPlan:
         gc.collect()
         gc.disable()
         try:
-            with torch.cuda.graph(g, stream=s):
+            # thread-local capture mode: RCCL / watchdog threads may query events meanwhile
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 fn()
         finally:
             if gc_was:

@@ -33,7 +33,12 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
          bucket_bytes: Optional[int] = None) -> S.DPState:
     """Initialise the data-parallel group from torchrun-style env vars
     (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  Without them this
-    is a size-1 group (no process group is created)."""
+    is a size-1 group (no process group is created).
+
+    On GPUs the data plane is the native RCCL engine (``parallel/comm.py``) and the
+    torch.distributed group is a gloo control plane; ``INTML_COMM=torch`` (or an explicit
+    ``INTML_DP_BACKEND``) uses torch.distributed (``nccl`` = RCCL) for both.
+    ``INTML_DP_FORCE=1`` runs the DP machinery even at size 1 (tests on a 1-GPU box)."""
     st = S.current()
     if st is not None:
         if shard_data is not None:
@@ -47,32 +52,48 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     local_size = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    owns = False
+    force = os.environ.get("INTML_DP_FORCE", "0") not in ("0", "", "false", "False")
+    use_gpu = torch.cuda.is_available() and os.environ.get("INTML_DEVICE", "cuda").startswith("cuda")
+    timeout_s = float(os.environ.get("INTML_DP_TIMEOUT", 600))
+    owns, comm = False, None
     if tdist.is_available() and tdist.is_initialized():
         world, rank = tdist.get_world_size(), tdist.get_rank()
         be = tdist.get_backend()
     elif world > 1:
-        use_gpu = torch.cuda.is_available() and os.environ.get("INTML_DEVICE", "cuda").startswith("cuda")
+        from . import comm as C
+        mode = C.comm_mode(use_gpu, backend)
         be = backend or os.environ.get("INTML_DP_BACKEND") or ("nccl" if use_gpu else "gloo")
+        if mode == "native":
+            be = "gloo"                  # control plane only; RCCL is driven natively
         if use_gpu:
             torch.cuda.set_device(local_rank % torch.cuda.device_count())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # a dead or hung rank turns into an error on every other rank after this timeout
         # (failure detection) instead of a silent hang
         import datetime
-        timeout = datetime.timedelta(seconds=float(os.environ.get("INTML_DP_TIMEOUT", 600)))
+        timeout = datetime.timedelta(seconds=timeout_s)
         tdist.init_process_group(backend=be, rank=rank, world_size=world, timeout=timeout)
         owns = True
+        if mode == "native":
+            comm = C.NativeComm(rank, world, torch.device("cuda", torch.cuda.current_device()), timeout_s)
     else:
         be = backend or "none"
+        if force and use_gpu:
+            from . import comm as C
+            if C.comm_mode(use_gpu, backend) == "native":
+                comm = C.NativeComm(0, 1, torch.device("cuda", torch.cuda.current_device()), timeout_s)
+                be = "rccl"
     st = S.DPState(rank=rank, size=world, local_rank=local_rank, local_size=local_size,
-                   backend=be, shard_data=shard_data, bucket_bytes=bucket_bytes, owns_pg=owns)
+                   backend=be, shard_data=shard_data, bucket_bytes=bucket_bytes, owns_pg=owns,
+                   comm=comm)
     S.set_state(st)
     return st
 
 
 def shutdown() -> None:
     st = S.current()
+    if st is not None and st.comm is not None:
+        st.comm.close()
     if st is not None and st.owns_pg and tdist.is_initialized():
         tdist.destroy_process_group()
     S.set_state(None)
@@ -97,12 +118,24 @@ def _active() -> bool:
     return st is not None and st.size > 1 and tdist.is_initialized()
 
 
+def _native():
+    """The RCCL data-plane engine when it is in use (also at size 1 under INTML_DP_FORCE)."""
+    st = S.current()
+    return st.comm if st is not None else None
+
+
 # ------------------------------------------------------------------------------ collectives
 def allreduce(value, average: bool = True, name: Optional[str] = None):
-    """All-reduce a tensor / numpy array / python scalar (returns the same kind)."""
+    """All-reduce a tensor / numpy array / python scalar (returns the same kind).
+    Device tensors go over RCCL; host values over the control plane."""
+    comm = _native()
+    is_t = isinstance(value, torch.Tensor)
+    if comm is not None and is_t and value.is_cuda:
+        t = value.detach().clone().contiguous()
+        comm.all_reduce(t)
+        return t / comm.size if average else t
     if not _active():
         return value
-    is_t = isinstance(value, torch.Tensor)
     dev = _comm_device()
     t = value if is_t else torch.as_tensor(np.asarray(value, dtype=np.float64))
     src = t
@@ -125,6 +158,15 @@ def allgather(value) -> list:
 
 
 def broadcast(tensor: torch.Tensor, root_rank: int = 0) -> torch.Tensor:
+    comm = _native()
+    if comm is not None and tensor.is_cuda and comm.size > 1:
+        if tensor.is_contiguous():
+            comm.broadcast(tensor, root_rank)
+        else:
+            tmp = tensor.contiguous()
+            comm.broadcast(tmp, root_rank)
+            tensor.copy_(tmp)
+        return tensor
     if _active():
         dev = _comm_device()
         if tensor.device == dev:
@@ -213,13 +255,31 @@ class Compression:
 
 
 # ------------------------------------------------------------------------------ grad reducer
+def merge_buckets(groups: Sequence[Tuple[int, int]], bucket_bytes: int):
+    """Merge backward-ordered flat (lo, hi) groups into buckets of >= ``bucket_bytes``
+    (fp32); returns (group indices per bucket, (lo, hi) per bucket)."""
+    buckets, cur, cur_bytes = [], [], 0
+    for gi, (lo, hi) in enumerate(groups):
+        cur.append(gi)
+        cur_bytes += (hi - lo) * 4
+        if cur_bytes >= bucket_bytes:
+            buckets.append(cur)
+            cur, cur_bytes = [], 0
+    if cur:
+        buckets.append(cur)
+    spans = [(min(groups[g][0] for g in b), max(groups[g][1] for g in b)) for b in buckets]
+    return buckets, spans
+
+
 class GradReducer:
-    """Bucketed gradient all-reduce over the flat grad buffer.
+    """Bucketed gradient all-reduce over the flat grad buffer (torch.distributed data plane).
 
     ``groups`` are (lo, hi) flat ranges in the order their gradients become final
     during backward.  Consecutive groups are merged until ``bucket_bytes``; each
-    bucket is ONE RCCL all-reduce (async, on RCCL's stream) over a contiguous view.
+    bucket is ONE all-reduce (async, on the backend's stream) over a contiguous view,
+    issued by the executor between graph segments.
     """
+    capturable = False
 
     def __init__(self, store, compression=None, bucket_bytes: int = 4 << 20):
         self.store = store
@@ -230,24 +290,14 @@ class GradReducer:
         self.bucket_groups: List[List[int]] = [[0]]
         self._pending = {}                  # bucket -> (work, bf16 buffer or None, view)
 
+    @property
+    def active(self) -> bool:
+        return self.size > 1 and _active()
+
     def configure(self, groups: Sequence[Tuple[int, int]]) -> List[List[int]]:
         """Merge backward-ordered groups into buckets; returns group indices per bucket."""
-        buckets, cur, cur_bytes = [], [], 0
-        for gi, (lo, hi) in enumerate(groups):
-            cur.append(gi)
-            cur_bytes += (hi - lo) * 4
-            if cur_bytes >= self.bucket_bytes:
-                buckets.append(cur)
-                cur, cur_bytes = [], 0
-        if cur:
-            buckets.append(cur)
-        self.bucket_groups = buckets
-        self.buckets = []
-        for b in buckets:
-            lo = min(groups[g][0] for g in b)
-            hi = max(groups[g][1] for g in b)
-            self.buckets.append((lo, hi))
-        return buckets
+        self.bucket_groups, self.buckets = merge_buckets(groups, self.bucket_bytes)
+        return self.bucket_groups
 
     def start(self, bucket: int, grad: torch.Tensor):
         """Launch the all-reduce of one bucket asynchronously (stream-ordered after the
@@ -279,6 +329,9 @@ class GradReducer:
         for bucket in sorted(self._pending):
             self.wait(bucket)
 
+    def after_step(self) -> None:
+        pass
+
     def reduce_all(self, grad: torch.Tensor, average: bool = True) -> None:
         for i in range(len(self.buckets)):
             self.start(i, grad)
@@ -287,9 +340,82 @@ class GradReducer:
             grad[: self.store.numel].div_(self.size)
 
 
-def make_reducer(executor, optimizer) -> GradReducer:
+class NativeGradReducer:
+    """Bucketed gradient all-reduce on the native RCCL engine, CAPTURABLE: the executor
+    inserts ``launch(k, ..)`` into the step's launch sequence on a comm stream forked after
+    bucket k's slab reduction, so the whole DP step (backward, RCCL all-reduces over
+    xGMI, optimizer) is ONE HIP graph replay.  The 1/size average is folded into the fused
+    optimizer (``grad_scale``).  Hvd ``Compression.fp16`` maps to a bf16 wire format
+    (fp32 -> bf16 staging copy, bf16 all-reduce, copy back), all on the comm stream."""
+    capturable = True
+
+    def __init__(self, store, comm, compression=None, bucket_bytes: int = 1 << 20):
+        self.store, self.comm = store, comm
+        self.compression = compression
+        self.bucket_bytes = bucket_bytes
+        self.size = comm.size
+        self.buckets: List[Tuple[int, int]] = [(0, store.numel)]
+        self.bucket_groups: List[List[int]] = [[0]]
+        self.stream = torch.cuda.Stream(device=comm.device)   # for the segmented (uncaptured) mode
+        self._stage = {}
+
+    @property
+    def active(self) -> bool:
+        return True
+
+    def configure(self, groups: Sequence[Tuple[int, int]]) -> List[List[int]]:
+        bg, spans = merge_buckets(groups, self.bucket_bytes)
+        if spans == self.buckets and (self._stage or self.compression != "bf16"):
+            return self.bucket_groups       # same layout (another batch size): keep the staging
+        self.bucket_groups, self.buckets = bg, spans   # buffers earlier graphs reference
+        self._stage = {}
+        if self.compression == "bf16":
+            for k, (lo, hi) in enumerate(self.buckets):
+                self._stage[k] = torch.empty(hi - lo, dtype=torch.bfloat16, device=self.comm.device)
+        return self.bucket_groups
+
+    def launch(self, bucket: int, grad: torch.Tensor, stream: torch.cuda.Stream) -> None:
+        """Enqueue bucket ``bucket``'s all-reduce on ``stream`` (capturable)."""
+        lo, hi = self.buckets[bucket]
+        view = grad[lo:hi]
+        buf = self._stage.get(bucket)
+        if buf is None:
+            self.comm.all_reduce(view, stream=stream)
+            return
+        with torch.cuda.stream(stream):
+            buf.copy_(view)
+            self.comm.all_reduce(buf, stream=stream)
+            view.copy_(buf)
+
+    # segmented (uncaptured) protocol, same as GradReducer
+    def start(self, bucket: int, grad: torch.Tensor):
+        self.stream.wait_stream(torch.cuda.current_stream())
+        self.launch(bucket, grad, self.stream)
+
+    def wait(self, bucket: int) -> None:
+        torch.cuda.current_stream().wait_stream(self.stream)
+
+    def finish(self) -> None:
+        torch.cuda.current_stream().wait_stream(self.stream)
+
+    def after_step(self) -> None:
+        """Watchdog marker after a step (raises if a peer failed / RCCL reported an error)."""
+        self.comm.mark()
+
+    def reduce_all(self, grad: torch.Tensor, average: bool = True) -> None:
+        for i in range(len(self.buckets)):
+            self.start(i, grad)
+        self.finish()
+        if average:
+            grad[: self.store.numel].div_(self.size)
+
+
+def make_reducer(executor, optimizer):
     if not is_initialized():
         init()
     st = _st()
     bb = getattr(optimizer, "bucket_bytes", None) or st.bucket_bytes
-    return GradReducer(executor.store, getattr(optimizer, "compression", None), bb)
+    comp = getattr(optimizer, "compression", None)
+    if st.comm is not None and getattr(executor.store, "device", torch.device("cpu")).type == "cuda":
+        return NativeGradReducer(executor.store, st.comm, comp, bb)
+    return GradReducer(executor.store, comp, bb)

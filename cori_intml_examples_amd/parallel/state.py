@@ -2,7 +2,7 @@
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Optional
+from typing import Any, Optional
 
 
 @dataclass
@@ -15,6 +15,7 @@ class DPState:
     shard_data: bool = True
     bucket_bytes: int = 4 << 20
     owns_pg: bool = False
+    comm: Any = None              # parallel.comm.NativeComm (RCCL data plane) or None
 
 
 _STATE: Optional[DPState] = None

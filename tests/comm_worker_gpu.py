@@ -1,0 +1,103 @@
+"""GPU worker for tests/test_comm.py: the native RCCL data-plane engine on ONE MI355X.
+
+RCCL refuses two ranks on one GPU, so this runs the engine at size 1 under
+INTML_DP_FORCE=1: the executor takes its data-parallel path with the bucket all-reduces
+CAPTURED into the step's HIP graph on the comm stream.  With one rank the all-reduce is the
+identity and grad_scale is 1, so the trained weights must match a non-DP model bit for bit;
+the same for the segmented (uncaptured) mode.  Writes a JSON report."""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["INTML_DP_FORCE"] = "1"
+
+import torch  # noqa: E402
+
+from cori_intml_examples_amd.apps import zoo  # noqa: E402
+from cori_intml_examples_amd.io.datasets import synthetic_rpv  # noqa: E402
+from cori_intml_examples_amd.parallel import comm as C  # noqa: E402
+from cori_intml_examples_amd.parallel import dist, hvd  # noqa: E402
+
+
+def flat(m):
+    return np.concatenate([w.reshape(-1) for w in m.get_weights()])
+
+
+def main(out):
+    rep = {}
+    st = hvd.init()
+    rep["backend"] = st.backend
+    rep["native"] = st.comm is not None
+    comm = st.comm
+    dev = torch.device("cuda", 0)
+    # primitives (size 1: sum/avg are the identity; gather/scatter are copies)
+    t = torch.arange(1000, dtype=torch.float32, device=dev)
+    comm.all_reduce(t)
+    b = torch.arange(64, dtype=torch.bfloat16, device=dev)
+    comm.all_reduce(b, op="avg")
+    o = torch.empty(1000, device=dev)
+    comm.all_gather(t, o)
+    rs = torch.empty(1000, device=dev)
+    comm.reduce_scatter(t, rs)
+    comm.broadcast(t, 0)
+    torch.cuda.synchronize()
+    ref = torch.arange(1000, dtype=torch.float32, device=dev)
+    rep["prims_ok"] = bool(torch.equal(t, ref) and torch.equal(o, ref) and torch.equal(rs, ref)
+                           and torch.equal(b.float(), torch.arange(64, device=dev).float()))
+    rep["allreduce_tensor"] = float(hvd.allreduce(torch.ones(4, device=dev) * 3).sum())
+
+    kw = dict(conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.0, optimizer="Adam", lr=1e-3, device="cuda:0")
+    x, y, _ = synthetic_rpv(512, channels=3, seed=5)
+    base = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw)
+    w0 = base.get_weights()
+
+    def train(m):
+        for i in range(4):
+            m.train_on_batch(x[i * 128:(i + 1) * 128], y[i * 128:(i + 1) * 128])
+        torch.cuda.synchronize()
+        return flat(m)
+
+    wb = train(base)
+    results = {}
+    for name, env in (("captured", {"INTML_COMM_CAPTURE": "1"}), ("segmented", {"INTML_COMM_CAPTURE": "0"})):
+        os.environ.update(env)
+        m = zoo.rpv_cnn((64, 64, 3), use_horovod=True, **kw)
+        m.set_weights(w0)
+        red = m._executor.reducer
+        w = train(m)
+        results[name] = {"reducer": type(red).__name__, "buckets": [list(b) for b in red.buckets]}
+        plan = next(iter(m._executor._plans.values()))
+        results[name]["comm_in_graph"] = bool(plan.comm_in_graph)
+        results[name]["n_comm_launches"] = sum(1 for it in plan.launches if len(it) > 2 and it[2] == "comm")
+        results[name]["max_abs_diff"] = float(np.abs(w - wb).max())
+    os.environ["INTML_COMM_CAPTURE"] = "1"
+    opt = hvd.DistributedOptimizer("Adam", compression=hvd.Compression.fp16)
+    m = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw)
+    m.compile(optimizer=opt, loss="binary_crossentropy", metrics=["accuracy"])
+    m.set_weights(w0)
+    w = train(m)
+    step = np.linalg.norm(wb - np.concatenate([a.reshape(-1) for a in w0]))
+    results["bf16_wire"] = {"rel_diff": float(np.linalg.norm(w - wb) / max(step, 1e-30))}
+    rep["train"] = results
+
+    # failure detection: an aborted communicator raises on its next use
+    spare = C.NativeComm(0, 1, dev, timeout_s=30.0)
+    spare.abort("fault injection")
+    try:
+        spare.all_reduce(torch.ones(8, device=dev))
+        rep["abort_raises"] = False
+    except RuntimeError as e:
+        rep["abort_raises"] = "fault injection" in str(e)
+    spare.close()
+    comm.mark()
+    rep["healthy"] = not comm.failed
+    with open(out, "w") as f:
+        json.dump(rep, f, indent=1)
+    dist.shutdown()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -1,0 +1,64 @@
+"""Native RCCL data-plane engine (parallel/comm.py, csrc/comm/engine.cpp).
+
+CPU: bucket merging and data-plane selection.  GPU: the engine's collectives, the DP step
+with the all-reduces captured into the HIP graph (bit-identical to non-DP at size 1), the
+segmented fallback, the bf16 wire format, and abort-based failure detection."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_merge_buckets_backward_order():
+    from cori_intml_examples_amd.parallel.dist import merge_buckets
+    # RPV M2 (1 channel, 547,841 params) flat groups in backward order: head, dense1, conv3,
+    # conv2, conv1
+    groups = [(547712, 547841), (23296, 547712), (4800, 23296), (160, 4800), (0, 160)]
+    bg, spans = merge_buckets(groups, 1 << 20)
+    assert bg == [[0, 1], [2, 3, 4]]                       # dense bucket first, convs second
+    assert spans == [(23296, 547841), (0, 23296)]
+    bg, spans = merge_buckets(groups, 1)
+    assert len(bg) == 5 and spans[0] == groups[0]
+
+
+def test_comm_mode_selection(monkeypatch):
+    from cori_intml_examples_amd.parallel import comm as C
+    assert C.comm_mode(False, None) == "torch"                       # CPU: gloo data plane
+    monkeypatch.setenv("INTML_COMM", "torch")
+    assert C.comm_mode(True, None) == "torch"
+    monkeypatch.delenv("INTML_COMM")
+    assert C.comm_mode(True, "gloo") == "torch"                      # explicit backend wins
+    monkeypatch.setenv("INTML_DP_BACKEND", "gloo")
+    assert C.comm_mode(True, None) == "torch"
+
+
+def test_comm_extension_builds_and_imports():
+    from cori_intml_examples_amd.parallel import comm as C
+    assert C.available()
+    m = C._module()
+    assert len(m.unique_id()) == 128 and m.version() >= 22000
+
+
+@pytest.mark.gpu
+def test_native_comm_engine_gpu(tmp_path):
+    out = tmp_path / "comm.json"
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("WORLD_SIZE", "RANK", "INTML_DP_BACKEND", "INTML_COMM"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "comm_worker_gpu.py"), str(out)],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rep = json.load(open(out))
+    assert rep["native"] and rep["prims_ok"], rep
+    assert rep["allreduce_tensor"] == pytest.approx(12.0)
+    cap, seg = rep["train"]["captured"], rep["train"]["segmented"]
+    assert cap["reducer"] == "NativeGradReducer" and cap["comm_in_graph"]
+    assert cap["n_comm_launches"] == len(cap["buckets"]) == 2
+    assert cap["max_abs_diff"] == 0.0, cap           # size-1 all-reduce in the graph is exact
+    assert not seg["comm_in_graph"] and seg["max_abs_diff"] == 0.0, seg
+    assert rep["train"]["bf16_wire"]["rel_diff"] < 0.05, rep["train"]["bf16_wire"]
+    assert rep["abort_raises"] and rep["healthy"], rep
