@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--samples", type=int, default=32768, help="resident synthetic samples per rank")
     ap.add_argument("--model", default="rpv", choices=["rpv", "mnist", "rpv_legacy"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--steps-per-graph", type=int, default=int(os.environ.get("INTML_STEPS_PER_GRAPH", 8)),
+                    help="full training steps per HIP-graph replay (the fit() loop's default)")
     args = ap.parse_args()
     if args.no_graphs:
         os.environ["INTML_GRAPHS"] = "0"
@@ -87,24 +89,30 @@ def main():
     data = DeviceData(xs.reshape(n, -1), y, n)
     hvd.broadcast_global_variables(0, model=model)
 
-    nb = n // B
     state = {"pos": 0, "perm": torch.randperm(n, device=dev, generator=g)}
+    chunk = max(1, args.steps_per_graph)
 
-    def step():
-        if state["pos"] + B > n:
+    def run(k):
+        """k full training steps; a run of steps is one HIP-graph replay (the step's
+        bookkeeping is device-resident), re-shuffling when the epoch is exhausted."""
+        if state["pos"] + k * B > n:
             state["pos"] = 0
             state["perm"] = torch.randperm(n, device=dev, generator=g)
-        ex.train_step(data, state["perm"], state["pos"], B)
-        state["pos"] += B
+        ex.train_steps(data, state["perm"], state["pos"], B, k)
+        state["pos"] += k * B
+
+    def chunks(total):
+        return [chunk] * (total // chunk) + ([total % chunk] if total % chunk else [])
 
     ex.reset_metrics()
-    for _ in range(args.warmup):
-        step()
+    timed = chunks(args.steps)
+    for k in chunks(args.warmup) + sorted(set(timed)):   # every timed graph is captured here
+        run(k)
     hvd.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for k in timed:
+        run(k)
     torch.cuda.synchronize()
     hvd.barrier()
     t1 = time.perf_counter()
@@ -123,7 +131,8 @@ def main():
                "config": {"model": cfg_name, "global_batch": B * size, "per_gpu_batch": B,
                           "seq_len": None, "input": list(shape),
                           "optimizer": type(getattr(model.optimizer, "_base_optimizer", model.optimizer)).__name__,
-                          "parallelism": "dp%d" % size, "train_loss": round(loss, 5)}}
+                          "parallelism": "dp%d" % size, "steps_per_graph": chunk,
+                          "train_loss": round(loss, 5)}}
         print(json.dumps(out), flush=True)
     hvd.shutdown()
 

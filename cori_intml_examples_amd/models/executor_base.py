@@ -54,6 +54,11 @@ class Executor:
     def train_step(self, data: DeviceData, perm: torch.Tensor, pos: int, bs: int) -> None:
         raise NotImplementedError
 
+    def train_steps(self, data: DeviceData, perm: torch.Tensor, pos: int, bs: int, k: int) -> None:
+        """``k`` consecutive full batches starting at ``pos`` (backends may fuse them)."""
+        for i in range(k):
+            self.train_step(data, perm, pos + i * bs, bs)
+
     def eval_step(self, data: DeviceData, pos: int, bs: int) -> None:
         raise NotImplementedError
 

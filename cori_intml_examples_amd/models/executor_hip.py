@@ -336,14 +336,19 @@ class HipExecutor(Executor):
         return bp
 
     def train_step(self, data, perm, pos, bs):
+        self.train_steps(data, perm, pos, bs, 1)
+
+    def train_steps(self, data, perm, pos, bs, k):
+        """k consecutive full training steps over batches [pos, pos + k*bs) of ``perm``
+        (one graph replay; the caller guarantees no host-side change between them)."""
         self._sync_lr()
         self._bind_data(data, perm)
         if self._expected_pos != pos:
             self._st_i32[1] = pos
         bp = self._plan_for(bs, "train")
-        bp.run()
-        self._expected_pos = pos + bs
-        self.opt.iterations += 1
+        bp.run(k)
+        self._expected_pos = pos + k * bs
+        self.opt.iterations += k
 
     def _set_eval_pos(self, pos, bs):
         if getattr(self, "_expected_eval_pos", None) != pos:
@@ -401,6 +406,7 @@ class BatchPlan:
         K = ex.K
         dev = ex.device
         self.graph = None
+        self.multi_graphs: Dict[int, torch.cuda.CUDAGraph] = {}   # k -> graph of k steps
         self.dp_graphs = None
         self.side = torch.cuda.Stream(device=dev) if env_flag("INTML_TWO_STREAMS", False) else None
         # opt-in: per-bucket optimizer (+ weight re-pack) on its own stream as soon as the
@@ -1017,23 +1023,40 @@ class BatchPlan:
     def _run_segment(self, lo, hi, k):
         self._run_seq(lo, hi)
 
-    def run(self):
+    def run(self, k: int = 1):
+        """Run ``k`` consecutive steps.  Step bookkeeping (data cursor, iteration count, LR,
+        dropout counter) is device-resident, so k steps are ONE graph of k back-to-back step
+        bodies: the inter-graph launch gap is paid once per k steps."""
         ex = self.ex
         dp = self.training and ex.reducer is not None and ex.reducer.active
         if dp:
             ex.grad_scale = 1.0 / ex.reducer.size
         if not dp or self.comm_in_graph:
             # single launch sequence; with the native RCCL engine it includes the bucket
-            # all-reduces on the comm stream (one graph replay per DP step)
+            # all-reduces on the comm stream (one graph replay per DP step / k steps)
             if not ex.use_graphs:
-                self._body(with_optim=True)
-            else:
+                for _ in range(k):
+                    self._body(with_optim=True)
+            elif k == 1:
                 if self.graph is None:
                     self.graph = self._capture(lambda: self._body(with_optim=True))
                 self.graph.replay()
+            else:
+                g = self.multi_graphs.get(k)
+                if g is None:
+                    def body_k():
+                        for _ in range(k):
+                            self._body(with_optim=True)
+                    g = self.multi_graphs[k] = self._capture(body_k)
+                g.replay()
             if dp:
                 ex.reducer.after_step()
             return
+        for _ in range(k):
+            self._run_dp_segmented()
+
+    def _run_dp_segmented(self):
+        ex = self.ex
         # Data parallel, torch.distributed data plane: each bucket's all-reduce is issued
         # between graph segments as soon as its slab reduction is done, so RCCL moves the
         # dense bucket over xGMI while the conv backward runs; the fused optimizer (with the

@@ -3,7 +3,9 @@
 Differences from a naive port: the dataset is uploaded to the device once, the
 per-epoch shuffle is a device permutation, the per-batch step is one HIP-graph
 replay on GPU, and epoch metrics accumulate on the device (one D2H per epoch).
-Per-batch host syncs happen only when a callback actually consumes batch logs.
+Per-batch host syncs happen only when a callback actually consumes batch logs; without
+per-batch callbacks, runs of full batches are replayed ``INTML_STEPS_PER_GRAPH`` (8) steps
+per graph launch.
 
 Reference behaviour reproduced: ``validation_split`` takes the *last* fraction
 before shuffling (``DistHPO_mnist.ipynb:188,293``: 60000 -> 49800/10200), the final
@@ -11,6 +13,8 @@ partial batch is processed, ``Train on N samples, validate on M samples`` banner
 History keys ``loss, acc, val_loss, val_acc`` (+ ``lr`` from ReduceLROnPlateau).
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -67,6 +71,7 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
     model.stop_training = False
     need_batch_logs = cb.batch_logs_needed
     need_batch_begin = cb.batch_begin_needed
+    steps_per_replay = max(1, int(os.environ.get("INTML_STEPS_PER_GRAPH", "8")))
 
     if do_val and verbose:
         print("Train on %d samples, validate on %d samples" % (train.n, val.n))
@@ -85,21 +90,35 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
             perm = torch.arange(train.n, device=ex.device)
         ex.reset_metrics()
         nb = (train.n + batch_size - 1) // batch_size
-        for b in range(nb):
+        # Without per-batch callbacks, runs of full batches go to the device as chunks of
+        # `chunk` steps (one HIP-graph replay each); the partial tail batch runs alone.
+        chunk = 1 if (need_batch_logs or need_batch_begin) else steps_per_replay
+        b = 0
+        while b < nb:
             pos = b * batch_size
             bs = min(batch_size, train.n - pos)
-            if need_batch_begin:
-                cb.on_batch_begin(b, {"batch": b, "size": bs})
-            ex.train_step(train, perm, pos, bs)
-            if need_batch_logs:
-                l, a = ex.last_batch_metrics()
-                logs = {"batch": b, "size": bs, "loss": l}
-                if model.metrics:
-                    logs["acc"] = a
-                cb.on_batch_end(b, logs)
-            if progbar is not None and verbose == 1:
-                if need_batch_logs or b == nb - 1 or b % 50 == 0:
-                    progbar.progress(pos + bs, [])
+            k = 1
+            if chunk > 1 and bs == batch_size:
+                k = max(1, min(chunk, (train.n - pos) // batch_size))
+            if k > 1:
+                ex.train_steps(train, perm, pos, bs, k)
+                b += k
+                if progbar is not None and verbose == 1:
+                    progbar.progress(pos + k * bs, [])
+            else:
+                if need_batch_begin:
+                    cb.on_batch_begin(b, {"batch": b, "size": bs})
+                ex.train_step(train, perm, pos, bs)
+                if need_batch_logs:
+                    l, a = ex.last_batch_metrics()
+                    logs = {"batch": b, "size": bs, "loss": l}
+                    if model.metrics:
+                        logs["acc"] = a
+                    cb.on_batch_end(b, logs)
+                if progbar is not None and verbose == 1:
+                    if need_batch_logs or b == nb - 1 or b % 50 == 0:
+                        progbar.progress(pos + bs, [])
+                b += 1
             if farm_should_stop():      # Stop button / AsyncResult.abort on a farm engine
                 model.stop_training = True
             if model.stop_training:

@@ -233,3 +233,28 @@ def test_multiple_steps_track_reference():
     wg = g.store.master[:g.store.numel].cpu().numpy()
     wc = c.store.master[:c.store.numel].numpy()
     assert _rel(wg, wc) < 1e-2
+
+
+def test_multi_step_graph_matches_single_steps():
+    """train_steps(k) replays ONE graph of k step bodies (device-resident cursor, step
+    counter, LR, dropout counter): bit-identical to k single-step replays, including the
+    metric accumulators and a following single step."""
+    set_random_seed(21)
+    a = _build("rpv", "cuda", opt="Adam", drop=0.2, cin=3)
+    set_random_seed(21)
+    b = _build("rpv", "cuda", opt="Adam", drop=0.2, cin=3)
+    x, y = _data(a, 640, seed=4)
+    res = []
+    for m, chunks in ((a, [1, 1, 1, 1, 1]), (b, [4, 1])):
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(3)).to(ex.device)
+        ex.reset_metrics()
+        pos = 0
+        for k in chunks:
+            ex.train_steps(d, perm, pos, 128, k)
+            pos += 128 * k
+        torch.cuda.synchronize()
+        res.append((m.store.master[:m.store.numel].cpu().numpy(), ex.read_metrics(), int(m.optimizer.iterations)))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1] and res[0][2] == res[1][2] == 5
