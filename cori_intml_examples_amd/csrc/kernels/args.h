@@ -146,6 +146,19 @@ struct StepBeginArgs {
   float beta1 = 0.9f, beta2 = 0.999f, decay = 0.f, schedule_decay = 0.004f;
 };
 
+// One launch opening every step: batch gather (workgroups [0, gather_blocks)), weight
+// re-pack of the previous update (the rest; pack_mode 1 always, 2 only if st->packs_stale),
+// and the step bookkeeping (workgroup 0).
+struct PrologueArgs {
+  StepBeginArgs sb;
+  GatherArgs ga;
+  int gather_gx = 1;             // workgroups per batch row
+  int gather_blocks = 0;         // gather_gx * bs
+  int pack_mode = 0;             // 0 none, 1 always, 2 if stale
+  const float* master = nullptr;
+  bf16* arena = nullptr;
+};
+
 struct OptimArgs {
   float* p = nullptr;
   const float* g = nullptr;
@@ -153,12 +166,13 @@ struct OptimArgs {
   float* s1 = nullptr;
   int n = 0;                     // elements [lo, lo + n) are updated (lo need not be aligned)
   int lo = 0;
-  const StepState* st = nullptr;
+  StepState* st = nullptr;       // read: this step's scalars; written: packs_stale
   int kind = 0;
   float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-7f, rho = 0.95f, momentum = 0.f;
   int nesterov = 0;
   float grad_scale = 1.f;
   int pack_only = 0;
+  int defer_pack = 0;            // leave the re-pack to the next step's prologue (marks stale)
   bf16* arena = nullptr;
 };
 

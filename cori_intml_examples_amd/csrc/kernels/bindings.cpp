@@ -26,8 +26,8 @@ void launch_dense_epi(const DenseEpiArgs& a, hipStream_t s);
 int dense_groups(int M, int NT, int KS);
 bool dense_big(int NT, int KS);
 void launch_head(const HeadArgs& a, hipStream_t s);
-void launch_step_begin(const StepBeginArgs& a, hipStream_t s);
-void launch_gather(const GatherArgs& a, hipStream_t s);
+void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
+int gather_gx(int R);
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s);
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s);
 void launch_pack(const float* master, bf16* arena, const PackTable& tab, hipStream_t s);
@@ -109,12 +109,17 @@ PYBIND11_MODULE(_kernels, m) {
       RW(StepBeginArgs, beta1) RW(StepBeginArgs, beta2) RW(StepBeginArgs, decay)
       RW(StepBeginArgs, schedule_decay);
 
+  py::class_<PrologueArgs>(m, "PrologueArgs")
+      .def(py::init<>())
+      RW(PrologueArgs, sb) RW(PrologueArgs, ga) RW(PrologueArgs, gather_gx) RW(PrologueArgs, gather_blocks)
+      RW(PrologueArgs, pack_mode) PTR(PrologueArgs, master) PTR(PrologueArgs, arena);
+
   py::class_<OptimArgs>(m, "OptimArgs")
       .def(py::init<>())
       PTR(OptimArgs, p) PTR(OptimArgs, g) PTR(OptimArgs, s0) PTR(OptimArgs, s1) RW(OptimArgs, n) RW(OptimArgs, lo)
       PTR(OptimArgs, st) RW(OptimArgs, kind) RW(OptimArgs, beta1) RW(OptimArgs, beta2) RW(OptimArgs, eps)
       RW(OptimArgs, rho) RW(OptimArgs, momentum) RW(OptimArgs, nesterov) RW(OptimArgs, grad_scale)
-      RW(OptimArgs, pack_only) PTR(OptimArgs, arena);
+      RW(OptimArgs, pack_only) RW(OptimArgs, defer_pack) PTR(OptimArgs, arena);
 
   py::class_<PackTable>(m, "PackTable")
       .def(py::init([]() { PackTable t; memset(&t, 0, sizeof(t)); return t; }))
@@ -204,8 +209,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("dense_big", &dense_big, "dense_fwd uses the large-weight LDS path for (NT, KS)");
   m.def("dense_epi", [](const DenseEpiArgs& a, uintptr_t s) { launch_dense_epi(a, S(s)); check_last("dense_epi"); });
   m.def("head", [](const HeadArgs& a, uintptr_t s) { launch_head(a, S(s)); check_last("head"); });
-  m.def("step_begin", [](const StepBeginArgs& a, uintptr_t s) { launch_step_begin(a, S(s)); check_last("step_begin"); });
-  m.def("gather", [](const GatherArgs& a, uintptr_t s) { launch_gather(a, S(s)); check_last("gather"); });
+  m.def("prologue", [](const PrologueArgs& a, const PackTable& t, uintptr_t s) {
+    launch_prologue(a, t, S(s)); check_last("prologue"); });
+  m.def("gather_gx", &gather_gx);
   m.def("slab_reduce", [](uintptr_t grad, int lo, int hi, const RedTable& t, uintptr_t s) {
     launch_slab_reduce(reinterpret_cast<float*>(grad), lo, hi, t, S(s)); check_last("slab_reduce"); });
   m.def("optim", [](const OptimArgs& a, const PackTable& t, uintptr_t s) { launch_optim(a, t, S(s)); check_last("optim"); });

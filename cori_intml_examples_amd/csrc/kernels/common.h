@@ -142,7 +142,7 @@ __device__ __forceinline__ bool dropout_keep(uint32_t idx, uint32_t seed, uint32
 struct StepState {
   int t;          // optimizer iterations completed (Keras `iterations`)
   int pos;        // next data cursor
-  int cur_pos;    // cursor of the step in flight
+  int cur_pos;    // (unused; kept for the host-side field offsets)
   int eval_pos;   // cursor for eval / predict steps
   float lr;       // base learning rate (host-written)
   float lr_eff;   // lr after Keras `decay`
@@ -153,6 +153,9 @@ struct StepState {
   // are dataset-independent): x rows [n][R] bf16, targets [n][C] fp32, epoch permutation
   unsigned long long data_x, data_y, perm;
   int data_n, data_R, data_C, use_perm;
+  // "the optimizer updated the master since the weight packs were last written"
+  int packs_stale;
+  int pad_;
 };
 
 enum OptKind { OPT_SGD = 0, OPT_RMSPROP = 1, OPT_ADADELTA = 2, OPT_ADAM = 3, OPT_NADAM = 4 };

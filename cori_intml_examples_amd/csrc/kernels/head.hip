@@ -20,6 +20,14 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   const int N = a.N;
   const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
   const int row = row0 + wave;
+  if (a.st && blockIdx.x == 0 && tid == 0) {
+    // advance the data cursor the step prologue gathered from (it must not move while
+    // prologue workgroups read it) and mark the weight packs fresh (this step's prologue
+    // re-packed them if an optimizer ran; the next optimizer marks them stale again)
+    if (a.training) a.st->pos += a.M;
+    else a.st->eval_pos += a.M;
+    a.st->packs_stale = 0;
+  }
 
   float z[16];
 #pragma unroll

@@ -1,8 +1,9 @@
 // Step plumbing kernels:
-//   step_begin   (1 thread)  iteration counter, data cursor, LR decay and the optimizer's
-//                            bias-correction scalars for this step (race-free bookkeeping)
-//   gather_batch (K14)       batch rows from the device-resident dataset by the epoch's
-//                            device permutation (16-byte copies), targets alongside
+//   prologue     (K14)       ONE launch per step: batch rows from the device-resident
+//                            dataset by the epoch's device permutation (16-byte copies),
+//                            the bf16 re-pack of the previous update, and the step
+//                            bookkeeping (iteration counter, cursor, LR decay, optimizer
+//                            bias-correction scalars) by the last workgroup
 //   slab_reduce  (K6/K9 2nd) deterministic fixed-order sum of split partial slabs into the
 //                            flat fp32 gradient buffer, remapped to Keras layout
 //   optim_update (K13)       ONE multi-tensor launch over the flat buffer: Adam / Nadam /
@@ -11,17 +12,13 @@
 //                            packs the MFMA kernels read scattered out in the same pass
 #include "args.h"
 
-__global__ void step_begin_kernel(const StepBeginArgs a) {
-  if (threadIdx.x != 0) return;
+// Step bookkeeping (one thread): iteration counter, LR decay and the optimizer's
+// bias-correction scalars for this step.  (The data cursor is advanced by the head kernel,
+// after every prologue workgroup has read it.)
+__device__ void step_bookkeeping(const StepBeginArgs& a) {
   StepState* st = a.st;
-  if (!a.training) {
-    st->cur_pos = st->eval_pos;
-    st->eval_pos += a.bs;
-    return;
-  }
+  if (!a.training) return;
   st->t += 1;
-  st->cur_pos = st->pos;
-  st->pos += a.bs;
   const double t = (double)st->t;
   const double lr = (double)st->lr / (1.0 + (double)a.decay * (t - 1.0));
   st->lr_eff = (float)lr;
@@ -51,34 +48,23 @@ __global__ void step_begin_kernel(const StepBeginArgs a) {
   }
 }
 
-void launch_step_begin(const StepBeginArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(64), 0, s, a);
-}
-
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void gather_kernel(const GatherArgs a) {
-  const int row = blockIdx.y;
-  if (row >= a.bs) return;
-  const StepState* st = a.st;
+// Batch rows from the device-resident dataset by the epoch's permutation (16-byte copies),
+// targets alongside.  `pos0` is the step's cursor (read before the bookkeeping advances it).
+__device__ __forceinline__ void gather_block(const GatherArgs& a, const StepState* st, int pos0, int row, int bx,
+                                             int gx) {
   const bf16* xs = reinterpret_cast<const bf16*>(st->data_x);
   const float* ys = reinterpret_cast<const float*>(st->data_y);
   const int* perm = reinterpret_cast<const int*>(st->perm);
   const int R = st->data_R, C = st->data_C;
-  const int pos = st->cur_pos + row;
+  const int pos = pos0 + row;
   int src = (st->use_perm && perm) ? perm[pos] : pos;
   src = min(max(src, 0), st->data_n - 1);
   const int nvec = R / 8;   // 16-byte vectors per row
   const uint4* s = reinterpret_cast<const uint4*>(xs + (size_t)src * R);
   uint4* d = reinterpret_cast<uint4*>(a.xb + (size_t)row * R);
-  for (int v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) d[v] = s[v];
-  if (blockIdx.x == 0 && a.yb && ys)
+  for (int v = bx * 256 + threadIdx.x; v < nvec; v += gx * 256) d[v] = s[v];
+  if (bx == 0 && a.yb && ys)
     for (int c = threadIdx.x; c < C; c += 256) a.yb[(size_t)row * C + c] = ys[(size_t)src * C + c];
-}
-
-void launch_gather(const GatherArgs& a, hipStream_t s) {
-  const int nvec = a.R / 8;
-  const int gx = max(1, min(8, (nvec + 255) / 256));
-  hipLaunchKernelGGL(gather_kernel, dim3(gx, a.bs), dim3(256), 0, s, a);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -270,6 +256,39 @@ void launch_pack(const float* master, bf16* arena, const PackTable& tab, hipStre
 }
 
 // ---------------------------------------------------------------------------------------
+// Step prologue: ONE launch instead of bookkeeping + gather + pack (three kernel boundaries,
+// ~5 us each at this size).  Gather and pack workgroups are independent.  Nothing here
+// writes state another prologue workgroup reads: the cursors (st->pos / eval_pos) and the
+// stale flag are advanced / cleared by the head kernel later in the step, and workgroup 0
+// computes this step's iteration count and optimizer scalars (read only by later kernels).
+// (A completion counter instead cost ~15 us: ~1200 same-address atomics serialise.)
+__global__ __launch_bounds__(256) void prologue_kernel(const PrologueArgs a, const PackTable tab) {
+  __shared__ __attribute__((aligned(16))) bf16 tile[32][136];
+  StepState* st = a.sb.st;
+  const int b = (int)blockIdx.x;
+  if (b < a.gather_blocks) {
+    const int row = b / a.gather_gx, bx = b - row * a.gather_gx;
+    const int pos0 = a.sb.training ? st->pos : st->eval_pos;
+    gather_block(a.ga, st, pos0, row, bx, a.gather_gx);
+  } else if (a.pack_mode == 1 || (a.pack_mode == 2 && st->packs_stale)) {
+    const int pb = b - a.gather_blocks;
+    if (pb >= tab.nblocks) dense_pack_block(a.master, a.arena, tab, pb - tab.nblocks, tile);
+    else conv_pack_block(a.master, a.arena, tab, pb);
+  }
+  if (b == 0 && threadIdx.x == 0) step_bookkeeping(a.sb);
+}
+
+void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s) {
+  const int pack_blocks = a.pack_mode ? tab.nblocks + tab.dblocks : 0;
+  hipLaunchKernelGGL(prologue_kernel, dim3(a.gather_blocks + pack_blocks), dim3(256), 0, s, a, tab);
+}
+
+int gather_gx(int R) {
+  const int nvec = R / 8;
+  return max(1, min(8, (nvec + 255) / 256));
+}
+
+// ---------------------------------------------------------------------------------------
 // Multi-tensor optimizer update over the flat fp32 buffers, 4 elements per thread
 // (16-byte loads/stores; the buffers' capacity is a multiple of 64 elements).
 template <int KIND>
@@ -342,6 +361,7 @@ __global__ __launch_bounds__(256) void optim_kernel(const OptimArgs a) {
   *reinterpret_cast<float4*>(a.p + e) = p;
   if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
   if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
+  if (a.defer_pack && blockIdx.x == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
 }
 
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s) {
@@ -356,5 +376,6 @@ void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s) {
       default: hipLaunchKernelGGL(optim_kernel<OPT_SGD>, grid, dim3(256), 0, s, a); break;
     }
   }
-  launch_pack(a.p, a.arena, tab, s);      // the MFMA kernels read the bf16 packs
+  if (!a.defer_pack || a.pack_only)
+    launch_pack(a.p, a.arena, tab, s);    // the MFMA kernels read the bf16 packs
 }

@@ -3,9 +3,9 @@
 One training step is a fixed sequence of ~15-20 launches (SURVEY.md §2.7 "fused op
 boundaries"), captured once per batch size into a HIP graph and replayed:
 
-  step_begin -> gather -> conv_mm(fwd) x C -> [dense split-K + epilogue] x D -> head
+  prologue(gather + re-pack + bookkeeping) -> conv_mm(fwd) x C -> [dense split-K + epilogue] x D -> head
   -> [wgrad(dense) + conv_mm(dX, bwd-through)] x D -> [wgrad(conv) + conv_mm(dgrad,
-  bwd-through)] x C -> slab_reduce (per DP bucket) -> [RCCL all-reduce] -> optim(+pack)
+  bwd-through)] x C -> slab_reduce (per DP bucket) -> [RCCL all-reduce] -> optim
 
 Activations are bf16 NHWC with channel strides padded to 8 (input: 4); weights live in
 ONE fp32 master buffer (Keras layout) and are mirrored into bf16 fragment-major packs by
@@ -233,7 +233,7 @@ class HipExecutor(Executor):
         self.arena = torch.zeros(max(off, 8), dtype=BF16, device=self.device)
 
     # ------------------------------------------------------------------ params / optimizer
-    def _optim_args(self, pack_only: bool):
+    def _optim_args(self, pack_only: bool, defer_pack: bool = False):
         K = self.K
         a = K.OptimArgs()
         a.p = self.store.master.data_ptr()
@@ -254,6 +254,7 @@ class HipExecutor(Executor):
         a.nesterov = int(getattr(o, "nesterov", False))
         a.grad_scale = self.grad_scale
         a.pack_only = int(pack_only)
+        a.defer_pack = int(defer_pack)
         a.arena = self.arena.data_ptr()
         return a
 
@@ -513,15 +514,23 @@ class BatchPlan:
         sb.beta2 = getattr(o, "beta_2", 0.999)
         sb.decay = getattr(o, "initial_decay", 0.0)
         sb.schedule_decay = getattr(o, "schedule_decay", 0.004)
-        self.launches.append(("step_begin", lambda s, a=sb: K.step_begin(a, s)))
-
         ga = K.GatherArgs()
         ga.st = st_ptr
         ga.bs = bs
         ga.R = self.xb.shape[1]
         ga.xb = self.xb.data_ptr()
         ga.yb = self.yb.data_ptr()
-        self.launches.append(("gather", lambda s, a=ga: K.gather(a, s)))
+        # one prologue launch: gather + the previous update's weight re-pack (training: always,
+        # except with per-bucket optimizers that pack themselves; eval/predict: only if an
+        # optimizer ran since the last pack) + the step bookkeeping
+        pa = K.PrologueArgs()
+        pa.sb, pa.ga = sb, ga
+        pa.gather_gx = K.gather_gx(ga.R)
+        pa.gather_blocks = pa.gather_gx * bs
+        pa.pack_mode = (0 if self.early_optim else 1) if training else 2
+        pa.master = store.master.data_ptr()
+        pa.arena = ex.arena.data_ptr()
+        self.launches.append(("prologue", lambda s, a=pa: K.prologue(a, ex.pack_table, s)))
 
         # ---------------- forward convs
         x_buf, H, W, Cs = self.xb, ex.in_H, ex.in_W, ex.in_Cs
@@ -996,7 +1005,8 @@ class BatchPlan:
 
     def _launch_optim(self):
         ex = self.ex
-        ex.K.optim(ex._optim_args(False), ex.pack_table, torch.cuda.current_stream().cuda_stream)
+        # the re-pack of the updated weights is done by the next step's prologue launch
+        ex.K.optim(ex._optim_args(False, defer_pack=True), ex.pack_table, torch.cuda.current_stream().cuda_stream)
 
     def _body(self, with_optim: bool):
         self._run_seq()
