@@ -55,6 +55,41 @@ struct ConvMMArgs {
   int dbg = 0;   // ablation (timing only, wrong results): 1 skip staging, 2 skip MFMA, 4 skip stores
 };
 
+// Layer-fused forward of a conv stack (conv_stack.hip): one workgroup per image, all
+// stages' activations in LDS.  Stride-1 convs with optional 2x2 max-pool.
+#define MAX_STACK 4
+#define MAX_STACK_SPLIT 4
+struct StackLayer {
+  int H = 0, W = 0, Cs_in = 0;        // input grid and channel stride
+  int Ho = 0, Wo = 0, Cout = 0, Cs_out = 0;
+  int KH = 3, KW = 3, pad_t = 0, pad_l = 0;
+  int KS = 0, NT = 0;                 // k-steps / n-tiles of the forward pack
+  int pool = 0, relu = 0;
+  int Hp = 0, Wp = 0;                 // stage output grid (pooled, or = Ho, Wo)
+  uint32_t drop_thr = 0;
+  float drop_scale = 1.f;
+  uint32_t stream_id = 0;
+  const bf16* wpk = nullptr;          // forward fragment pack (global)
+  const float* bias = nullptr;
+  bf16* out = nullptr;                // stage output [B][Hp][Wp][Cs_out]
+  uint8_t* code = nullptr;            // pool argmax codes, same shape (or null)
+  int w_lds = 0;                      // bf16 element offset of the pack inside the LDS weights
+};
+
+struct ConvStackArgs {
+  const bf16* x = nullptr;            // network input [B][H][W][Cs]
+  int B = 0, n = 0;
+  uint32_t seed = 0;
+  const StepState* st = nullptr;
+  int off_w = 0, off_buf[2] = {0, 0}, off_codes = 0, lds_bytes = 0;   // LDS layout (bytes)
+  int dbg = 0;   // ablation (timing only, wrong results): 1 no MFMA loop, 2 no epilogue, 4 no global stores, 8 no staging
+  int splits = 1;                     // workgroups (row bands) per image
+  // per layer, per band: conv-output rows [c0, c1) computed, stage-output rows [own0, own1)
+  // stored, input halo image = input rows [ib, ib + ih)
+  int rows[MAX_STACK][MAX_STACK_SPLIT][6] = {};
+  StackLayer L[MAX_STACK];
+};
+
 // Weight gradient: dW[k][n] = sum_pixels im2col(x)[p][k] * dY[p][n]  (split over pixels)
 struct WgradArgs {
   const bf16* x = nullptr;

@@ -26,6 +26,7 @@ void launch_dense_epi(const DenseEpiArgs& a, hipStream_t s);
 int dense_groups(int M, int NT, int KS);
 bool dense_big(int NT, int KS);
 void launch_head(const HeadArgs& a, hipStream_t s);
+void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s);
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
 int gather_gx(int R);
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s);
@@ -108,6 +109,31 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(StepBeginArgs, st) RW(StepBeginArgs, training) RW(StepBeginArgs, bs) RW(StepBeginArgs, opt_kind)
       RW(StepBeginArgs, beta1) RW(StepBeginArgs, beta2) RW(StepBeginArgs, decay)
       RW(StepBeginArgs, schedule_decay);
+
+  py::class_<StackLayer>(m, "StackLayer")
+      .def(py::init<>())
+      RW(StackLayer, H) RW(StackLayer, W) RW(StackLayer, Cs_in) RW(StackLayer, Ho) RW(StackLayer, Wo)
+      RW(StackLayer, Cout) RW(StackLayer, Cs_out) RW(StackLayer, KH) RW(StackLayer, KW) RW(StackLayer, pad_t)
+      RW(StackLayer, pad_l) RW(StackLayer, KS) RW(StackLayer, NT) RW(StackLayer, pool) RW(StackLayer, relu)
+      RW(StackLayer, Hp) RW(StackLayer, Wp) RW(StackLayer, drop_thr) RW(StackLayer, drop_scale)
+      RW(StackLayer, stream_id) PTR(StackLayer, wpk) PTR(StackLayer, bias) PTR(StackLayer, out)
+      PTR(StackLayer, code) RW(StackLayer, w_lds);
+
+  py::class_<ConvStackArgs>(m, "ConvStackArgs")
+      .def(py::init<>())
+      PTR(ConvStackArgs, x) RW(ConvStackArgs, B) RW(ConvStackArgs, n) RW(ConvStackArgs, seed)
+      PTR(ConvStackArgs, st) RW(ConvStackArgs, dbg) RW(ConvStackArgs, off_w) RW(ConvStackArgs, off_codes) RW(ConvStackArgs, lds_bytes)
+      .def("set_buf_offsets", [](ConvStackArgs& a, int b0, int b1) { a.off_buf[0] = b0; a.off_buf[1] = b1; })
+      RW(ConvStackArgs, splits)
+      .def("set_rows", [](ConvStackArgs& a, int l, int sp, int c0, int c1, int o0, int o1, int ib, int ih) {
+        if (l < 0 || l >= MAX_STACK || sp < 0 || sp >= MAX_STACK_SPLIT) throw std::out_of_range("conv stack rows");
+        const int v[6] = {c0, c1, o0, o1, ib, ih};
+        for (int i = 0; i < 6; ++i) a.rows[l][sp][i] = v[i];
+      })
+      .def("set_layer", [](ConvStackArgs& a, int i, const StackLayer& l) {
+        if (i < 0 || i >= MAX_STACK) throw std::out_of_range("conv stack layer index");
+        a.L[i] = l;
+      });
 
   py::class_<PrologueArgs>(m, "PrologueArgs")
       .def(py::init<>())
@@ -212,6 +238,10 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("prologue", [](const PrologueArgs& a, const PackTable& t, uintptr_t s) {
     launch_prologue(a, t, S(s)); check_last("prologue"); });
   m.def("gather_gx", &gather_gx);
+  m.attr("MAX_STACK") = MAX_STACK;
+  m.attr("MAX_STACK_SPLIT") = MAX_STACK_SPLIT;
+  m.def("conv_stack_fwd", [](const ConvStackArgs& a, uintptr_t s) {
+    launch_conv_stack_fwd(a, S(s)); check_last("conv_stack_fwd"); });
   m.def("slab_reduce", [](uintptr_t grad, int lo, int hi, const RedTable& t, uintptr_t s) {
     launch_slab_reduce(reinterpret_cast<float*>(grad), lo, hi, t, S(s)); check_last("slab_reduce"); });
   m.def("optim", [](const OptimArgs& a, const PackTable& t, uintptr_t s) { launch_optim(a, t, S(s)); check_last("optim"); });

@@ -533,8 +533,14 @@ class BatchPlan:
         self.launches.append(("prologue", lambda s, a=pa: K.prologue(a, ex.pack_table, s)))
 
         # ---------------- forward convs
+        stack = self._conv_stack_args(training) if env_flag("INTML_CONV_STACK", True) else None
+        if stack is not None:
+            self.stack_args = stack
+            self.launches.append(("conv_stack_fwd", lambda s, a=stack: K.conv_stack_fwd(a, s)))
         x_buf, H, W, Cs = self.xb, ex.in_H, ex.in_W, ex.in_Cs
         for g, cs in zip(ex.convs, ex.plan.convs):
+            if stack is not None:
+                break
             a = K.ConvMMArgs()
             a.x = x_buf.data_ptr()
             a.B, a.H, a.W, a.Cs_in = bs, g.H, g.W, g.Cs_in
@@ -701,6 +707,129 @@ class BatchPlan:
                 self.launches.append(("dgrad_conv%d" % g.i, self._conv_launch(a, g.NTd, False)))
                 self.pack_readers.append(("dgrad_conv%d" % g.i, sp.offset, sp.offset + sp.numel))
         self._build_reduce()
+
+    LDS_LIMIT = 160 * 1024
+
+    def _conv_stack_args(self, training: bool):
+        """ConvStackArgs for the layer-fused forward (one workgroup per image, activations in
+        LDS), or None when the conv stack does not qualify: stride-1 convs, <= 64 output
+        channels, <= MAX_STACK layers, and the per-image working set within the LDS."""
+        ex, K = self.ex, self.ex.K
+        convs = ex.convs
+        if not convs or len(convs) > K.MAX_STACK:
+            return None
+        for g in convs:
+            if g.stride != 1 or g.NT > 4 or g.Cs_out % 8 or (g.Cs_in != 4 and g.Cs_in % 8):
+                return None
+
+        # row bands per image: enough workgroups to cover the 256 CUs at small batches
+        want = int(os.environ.get("INTML_STACK_SPLITS", "0")) or cdiv(256, self.bs)
+        splits = max(1, min(K.MAX_STACK_SPLIT, want))
+        while splits > 1 and self._stack_rows(convs, splits) is None:
+            splits -= 1
+        rows = self._stack_rows(convs, splits)
+        if rows is None:
+            return None
+        layout = self._stack_layout(convs, rows, splits)
+        if layout is None:
+            return None
+        off_w, w_off, off_b0, off_b1, off_codes, lds = layout
+        n = len(convs)
+        a = K.ConvStackArgs()
+        a.x = self.xb.data_ptr()
+        a.B, a.n, a.seed, a.st = self.bs, n, ex.seed, ex.state.data_ptr()
+        a.off_w, a.off_codes, a.lds_bytes = off_w, off_codes, lds
+        a.dbg = int(os.environ.get("INTML_STACK_DBG", "0"))
+        a.set_buf_offsets(off_b0, off_b1)
+        a.splits = splits
+        for l in range(n):
+            for sp in range(splits):
+                a.set_rows(l, sp, *rows[l][sp])
+        store = ex.store
+        for i, (g, cs) in enumerate(zip(convs, ex.plan.convs)):
+            L = K.StackLayer()
+            L.H, L.W, L.Cs_in = g.H, g.W, g.Cs_in
+            L.Ho, L.Wo, L.Cout, L.Cs_out = g.Ho, g.Wo, g.Cout, g.Cs_out
+            L.KH, L.KW, L.pad_t, L.pad_l = g.KH, g.KW, g.pad_t, g.pad_l
+            L.KS, L.NT = g.KS, g.NT
+            L.pool, L.relu = int(g.pool), int(g.relu)
+            L.Hp, L.Wp = g.Hp, g.Wp
+            if training and g.rate > 0:
+                L.drop_thr = keep_threshold(g.rate)
+                L.drop_scale = 1.0 / (1.0 - g.rate)
+            L.stream_id = g.stream
+            L.wpk = ex.arena.data_ptr() + 2 * g.pack_fwd
+            L.bias = store.view(cs.conv, "bias").data_ptr() if cs.conv.use_bias else 0
+            L.out = self.conv_out[i].data_ptr()
+            if g.pool:
+                L.code = self.conv_code[i].data_ptr()
+            L.w_lds = w_off[i]
+            a.set_layer(i, L)
+        self.stack_splits = splits
+        return a
+
+    @staticmethod
+    def _stack_rows(convs, splits):
+        """Per layer, per row band: (c0, c1, own0, own1, ib, ih) = conv-output rows computed,
+        stage-output rows stored, and the input halo image's first input row and row count.
+        Bands own an even partition of every layer's stage rows; each band computes its
+        owned rows plus what the next layer's computed rows read (halo), walking the stack
+        backwards.  A layer's input image spans both the rows its conv reads and the rows the
+        previous layer stores from it.  None if a band would own no rows."""
+        n = len(convs)
+        rows = [[None] * splits for _ in range(n)]
+        for sp in range(splits):
+            need = None                       # stage-output rows of layer l needed downstream
+            for l in range(n - 1, -1, -1):
+                g = convs[l]
+                P = 2 if g.pool else 1
+                own = (sp * g.Hp // splits, (sp + 1) * g.Hp // splits)
+                if own[1] <= own[0]:
+                    return None
+                lo, hi = own
+                if need is not None:
+                    lo, hi = min(lo, need[0]), max(hi, need[1])
+                lo, hi = max(lo, 0), min(hi, g.Hp)
+                c0, c1 = lo * P, hi * P
+                rows[l][sp] = [c0, c1, own[0], own[1], c0 - g.pad_t, c1 - c0 + g.KH - 1]
+                need = (max(c0 - g.pad_t, 0), min(c1 - 1 - g.pad_t + g.KH, g.H))
+            for l in range(1, n):             # image of layer l also holds layer l-1's stored rows
+                r, o0, o1 = rows[l][sp], rows[l - 1][sp][2], rows[l - 1][sp][3]
+                ib0, ie0 = r[4], r[4] + r[5]
+                r[4] = min(ib0, o0)
+                r[5] = max(ie0, o1) - r[4]
+        return [[tuple(r) for r in layer] for layer in rows]
+
+    def _stack_layout(self, convs, rows, splits):
+        """LDS byte layout: zeros + k-offset table | all weight packs | two ping-pong halo
+        images | code plane.  None if it exceeds the CU's LDS."""
+        def a16(v):
+            return (v + 15) & ~15
+
+        n = len(convs)
+        ntab = max((g.KS * 8 if g.Cs_in == 4 else g.KS * 4) for g in convs)
+        off_w = 32 + a16(4 * ntab)
+        w_off, welems = [], 0
+        for g in convs:
+            w_off.append(welems)
+            welems += g.KS * g.NT * 64 * 8
+        bufs, codes = [0, 0], 16
+        for l, g in enumerate(convs):
+            P = 2 if g.pool else 1
+            for sp in range(splits):
+                c0, c1, _, _, _, ih = rows[l][sp]
+                bufs[l & 1] = max(bufs[l & 1], ih * (g.Wo + g.KW - 1) * g.Cs_in)
+                if g.pool:
+                    codes = max(codes, (c1 - c0) // 2 * g.Wp * g.Cs_out)
+                if l == n - 1:
+                    bufs[n & 1] = max(bufs[n & 1], (c1 - c0) // P * g.Wp * g.Cs_out)
+        off_b0 = off_w + a16(2 * welems)
+        off_b1 = off_b0 + a16(2 * bufs[0])
+        off_codes = off_b1 + a16(2 * bufs[1])
+        lds = off_codes + a16(codes)
+        if lds > self.LDS_LIMIT:
+            return None
+        return off_w, w_off, off_b0, off_b1, off_codes, lds
 
     @staticmethod
     def _wide(Cs_in: int, KS: int, NT: int) -> bool:

@@ -258,3 +258,34 @@ def test_multi_step_graph_matches_single_steps():
         res.append((m.store.master[:m.store.numel].cpu().numpy(), ex.read_metrics(), int(m.optimizer.iterations)))
     np.testing.assert_array_equal(res[0][0], res[1][0])
     assert res[0][1] == res[1][1] and res[0][2] == res[1][2] == 5
+
+
+@pytest.mark.parametrize("kind,drop,cin,hw", [("rpv", 0.2, 3, 64), ("rpv", 0.0, 1, 16), ("mnist", 0.4, 1, 28),
+                                              ("odd", 0.25, 2, 16)])
+def test_conv_stack_forward_matches_per_layer(kind, drop, cin, hw, monkeypatch):
+    """The layer-fused forward (one workgroup per image, activations in LDS) produces the
+    per-layer kernels' stage outputs and argmax codes bit for bit (same k order, bf16
+    rounding points and dropout counters), and hence the same training step."""
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("INTML_CONV_STACK", flag)
+        set_random_seed(33)
+        m = _build(kind, "cuda", opt="Adam", drop=drop, cin=cin, hw=hw)
+        x, y = _data(m, 96, seed=8)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.arange(d.n, device=ex.device)
+        ex.train_step(d, perm, 0, 96)
+        torch.cuda.synchronize()
+        bp = ex._plans[(96, "train")]
+        names = [it[0] for it in bp.launches]
+        outs.append(([t.clone() for t in bp.conv_out], [c.clone() if c is not None else None for c in bp.conv_code],
+                     m.store.master[:m.store.numel].clone(), names))
+    (o1, c1, w1, n1), (o0, c0, w0, n0) = outs
+    assert "conv_stack_fwd" in n1 and "conv_stack_fwd" not in n0
+    for i, (a, b) in enumerate(zip(o1, o0)):
+        assert torch.equal(a, b), "stage %d output differs (max %g)" % (i, (a.float() - b.float()).abs().max())
+    for a, b in zip(c1, c0):
+        if a is not None:
+            assert torch.equal(a, b)
+    assert torch.equal(w1, w0)
