@@ -26,6 +26,8 @@ void launch_dense_epi(const DenseEpiArgs& a, hipStream_t s);
 int dense_groups(int M, int NT, int KS);
 bool dense_big(int NT, int KS);
 void launch_head(const HeadArgs& a, hipStream_t s);
+bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits,
+                      hipStream_t s);
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s);
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
 int gather_gx(int R);
@@ -238,6 +240,11 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("prologue", [](const PrologueArgs& a, const PackTable& t, uintptr_t s) {
     launch_prologue(a, t, S(s)); check_last("prologue"); });
   m.def("gather_gx", &gather_gx);
+  m.def("dual_halo", [](const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits, uintptr_t s) {
+    const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, S(s));
+    check_last("dual_halo");
+    return ok;
+  });
   m.attr("MAX_STACK") = MAX_STACK;
   m.attr("MAX_STACK_SPLIT") = MAX_STACK_SPLIT;
   m.def("conv_stack_fwd", [](const ConvStackArgs& a, uintptr_t s) {

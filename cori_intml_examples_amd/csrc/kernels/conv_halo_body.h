@@ -1,0 +1,282 @@
+// Body of the halo-staged implicit-GEMM conv kernel (see conv_halo.hip for the design),
+// as a device function of the block index so dual_halo.hip can co-schedule it with
+// the weight-gradient body in one launch.
+#pragma once
+#include "bwd_through.h"
+
+// NTC n-tiles of the weight slice, TM m-tiles per wave per pass (each A fragment feeds NTC
+// MFMAs and each weight fragment TM), KCH k-steps per batch of independent reads.
+template <int NTC, int TM, int KCH, bool CS4>
+__device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx, const int by, char* smem) {
+  const int KS = a.KS, R = a.R, s = a.stride, dil = a.in_dil, Cs = a.Cs_in;
+  const int ntab = CS4 ? KS * 8 : KS * 4;
+  int* tab = reinterpret_cast<int*>(smem);
+  const int tab_bytes = (ntab * 4 + 15) & ~15;
+  bf16* zl = reinterpret_cast<bf16*>(smem + tab_bytes);      // 32 B of zeros
+  bf16* wl = zl + 16;
+  bf16* xl = wl + (size_t)KS * NTC * 64 * 8;
+  const int W_in = (a.Wo - 1) * s + a.KW;
+  const int R_in = (R - 1) * s + a.KH;
+  const int tid = threadIdx.x;
+  const int nrb = (a.Ho + R - 1) / R;
+  const int b = bx / nrb;
+  const int oy0 = (bx - b * nrb) * R;
+  const int nt0 = by * NTC;
+
+  if (tid < 8) reinterpret_cast<uint32_t*>(zl)[tid] = 0u;
+  const bool dbg_stage = !(a.dbg & 1), dbg_mfma = !(a.dbg & 2), dbg_store = !(a.dbg & 4);
+  // weights -> LDS
+  if (dbg_stage) staged_copy<8, bf16x8>(
+      KS * NTC * 64, tid, 256,
+      [&](int i) {
+        const int ks = i / (NTC * 64);   // compile-time power of two
+        const int rem = i - ks * NTC * 64;
+        const int nt = nt0 + (rem >> 6);
+        const bool ok = nt < a.NT;
+        return load_bf16x8_if(ok, a.wpk + ((size_t)(ks * a.NT + nt) * 64 + (rem & 63)) * 8, a.wpk);
+      },
+      [&](int i, const bf16x8& v) { *reinterpret_cast<bf16x8*>(wl + (size_t)i * 8) = v; });
+  // k-chunk -> halo offset table
+  {
+    const int KHW = a.KH * a.KW;
+    const int cw = CS4 ? 4 : 8;
+    for (int c = tid; c < ntab; c += 256) {
+      const int k0 = c * cw;
+      const int tap = k0 / Cs;
+      int e = -1;
+      if (tap < KHW) {
+        const int ky = tap / a.KW;
+        e = (ky * W_in + (tap - ky * a.KW)) * Cs + (k0 - tap * Cs);
+      }
+      tab[c] = e;
+    }
+  }
+  // input halo -> LDS
+  if (dbg_stage) {
+    const int cw = CS4 ? 4 : 8;
+    const int cpp = Cs / cw;
+    const int nch = R_in * W_in * cpp;
+    const int yb = oy0 * s - a.pad_t, xb0 = -a.pad_l;
+    const bf16* xbase = a.in_code ? a.x + (size_t)b * a.in_pH * a.in_pW * Cs : a.x + (size_t)b * a.H * a.W * Cs;
+    const uint8_t* cbase = a.in_code ? a.in_code + (size_t)b * a.in_pH * a.in_pW * Cs : nullptr;
+    const FastDiv fcpp(cpp), fwin(W_in);
+    auto coords = [&](int i, int& c, int& iy, int& ix) -> bool {
+      const int pix = fcpp.div(i);
+      c = (i - pix * cpp) * cw;
+      const int r = fwin.div(pix);
+      iy = yb + r;
+      ix = xb0 + (pix - r * W_in);
+      bool ok = iy >= 0 && ix >= 0;
+      if (dil > 1) {
+        ok = ok && (iy % dil == 0) && (ix % dil == 0);
+        iy /= dil;
+        ix /= dil;
+      }
+      return ok && iy < a.H && ix < a.W;
+    };
+    if (CS4) {
+      staged_copy<8, bf16x4>(
+          nch, tid, 256,
+          [&](int i) {
+            int c, iy, ix;
+            const bool ok = coords(i, c, iy, ix);
+            return load_bf16x4_if(ok, xbase + ((size_t)iy * a.W + ix) * 4, xbase);
+          },
+          [&](int i, const bf16x4& v) { *reinterpret_cast<bf16x4*>(xl + (size_t)i * 4) = v; });
+    } else {
+      staged_copy<8, bf16x8>(
+          nch, tid, 256,
+          [&](int i) {
+            int c, iy, ix;
+            const bool ok = coords(i, c, iy, ix);
+            if (cbase) return unpool_load8(xbase, cbase, a.in_pH, a.in_pW, Cs, iy, ix, c, ok);
+            return load_bf16x8_if(ok, xbase + ((size_t)iy * a.W + ix) * Cs + c, xbase);
+          },
+          [&](int i, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + (size_t)i * 8) = v; });
+    }
+  }
+  __syncthreads();
+
+  const int wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const int rows = min(R, a.Ho - oy0);
+  const int nwin = a.pool ? (rows >> 1) * a.Wp : 0;
+  const int npix = rows * a.Wo;
+  const int ntiles = a.pool ? (nwin + 3) / 4 : (npix + 15) / 16;
+  const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
+
+  const FastDiv fwp(a.Wp > 0 ? a.Wp : 1), fwo(a.Wo);
+  // per-wave epilogue scratch [16 rows][NTC*16] fp32, after the 16-B aligned halo image
+  constexpr int EPW = TM * 16 * 2 * NTC * 16 / 4;   // floats per wave: TM*16 rows x LDC bf16
+  float* ep = reinterpret_cast<float*>(xl + (((size_t)R_in * W_in * Cs + 7) & ~(size_t)7)) + wave * EPW;
+  const size_t qbase = ((size_t)b * a.Hp + (oy0 >> 1)) * a.Wp;
+  for (int tb = wave * TM; tb < ntiles; tb += 4 * TM) {
+    bool rv[TM];
+    const bf16* xrow[TM];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      const int tile = tb + t;
+      int ry, rx;
+      if (a.pool) {
+        const int w = tile * 4 + (r >> 2);
+        rv[t] = w < nwin;
+        const int wi = rv[t] ? w : 0;
+        const int pyl = fwp.div(wi);
+        ry = 2 * pyl + ((r >> 1) & 1);
+        rx = 2 * (wi - pyl * a.Wp) + (r & 1);
+      } else {
+        const int p = tile * 16 + r;
+        rv[t] = p < npix;
+        const int pi = rv[t] ? p : 0;
+        ry = fwo.div(pi);
+        rx = pi - ry * a.Wo;
+      }
+      xrow[t] = xl + ((size_t)(ry * s) * W_in + rx * s) * Cs;
+    }
+    f32x4 acc[TM][NTC];
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int nt = 0; nt < NTC; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < (dbg_mfma ? KS : 0); kc += KCH) {
+      int e0[KCH], e1[KCH];
+#pragma unroll
+      for (int u = 0; u < KCH; ++u) {
+        const bool in = kc + u < KS;
+        if (CS4) {
+          e0[u] = in ? tab[((kc + u) * 4 + g) * 2] : -1;
+          e1[u] = in ? tab[((kc + u) * 4 + g) * 2 + 1] : -1;
+        } else {
+          e0[u] = in ? tab[(kc + u) * 4 + g] : -1;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < KCH; ++u) {
+        if (kc + u < KS) {   // wave-uniform
+          bf16x8 af[TM];
+#pragma unroll
+          for (int t = 0; t < TM; ++t) {
+            if (!CS4) {
+              af[t] = *reinterpret_cast<const bf16x8*>((rv[t] && e0[u] >= 0) ? xrow[t] + e0[u] : zl);
+            } else {
+              const bf16x4 v0 = *reinterpret_cast<const bf16x4*>((rv[t] && e0[u] >= 0) ? xrow[t] + e0[u] : zl);
+              const bf16x4 v1 = *reinterpret_cast<const bf16x4*>((rv[t] && e1[u] >= 0) ? xrow[t] + e1[u] : zl);
+              af[t] = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+          }
+#pragma unroll
+          for (int nt = 0; nt < NTC; ++nt) {
+            const bf16x8 bfr =
+                *reinterpret_cast<const bf16x8*>(wl + ((size_t)((kc + u) * NTC + nt) * 64 + lane) * 8);
+#pragma unroll
+            for (int t = 0; t < TM; ++t) acc[t][nt] = mfma16(af[t], bfr, acc[t][nt]);
+          }
+        }
+      }
+    }
+
+    if (!dbg_store) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int nt = 0; nt < NTC; ++nt)
+          asm volatile("" ::"v"(acc[t][nt][0]), "v"(acc[t][nt][1]), "v"(acc[t][nt][2]), "v"(acc[t][nt][3]));
+      continue;
+    }
+    // Epilogue through the wave's LDS scratch: lanes write their MFMA-layout results, then
+    // re-read them as 8-channel vectors so every global store is 16 bytes.  The forward
+    // epilogue stages all TM tiles of the pass first (final bf16 values + pool codes), so
+    // one copy loop writes TM*16 pixels / TM*4 windows with all lanes busy.
+    const int LDC = NTC * 16;
+    const int csh = (a.mode == 1 ? a.bt.pCs : a.Cs_out) - nt0 * 16;   // channels this WG owns
+    const int C = csh < LDC ? csh : LDC;
+    const int cch = C >> 3;                                            // 8-channel chunks
+    const FastDiv fcch(cch > 0 ? cch : 1);
+    if (a.mode == 0 && a.pool) {
+      bf16* epb = reinterpret_cast<bf16*>(ep);                // [TM*4 windows][LDC]
+      uint8_t* epc = reinterpret_cast<uint8_t*>(epb + TM * 4 * LDC);
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const size_t q = qbase + (tb + t) * 4 + g;
+#pragma unroll
+        for (int nt = 0; nt < NTC; ++nt) {
+          const int n = (nt0 + nt) * 16 + r;
+          float best = 0.f;
+          int code = 0;
+          if (n < a.N) {
+            const float bv = a.bias ? a.bias[n] : 0.f;
+            best = -3.4e38f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float v = acc[t][nt][j] + bv;
+              if (a.relu) v = fmaxf(v, 0.f);
+              if (v > best) { best = v; code = j; }
+            }
+            if (a.drop_thr)
+              best = dropout_keep((uint32_t)(q * a.N + n), a.seed, a.stream_id, step, a.drop_thr) ? best * a.drop_scale
+                                                                                                 : 0.f;
+          }
+          epb[(t * 4 + g) * LDC + nt * 16 + r] = f2bf(best);
+          epc[(t * 4 + g) * LDC + nt * 16 + r] = (uint8_t)code;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int nw = max(0, min(TM * 4, nwin - tb * 4));
+      for (int c = lane; c < nw * cch; c += 64) {
+        const int win = fcch.div(c), c8 = c - win * cch;
+        const size_t o = (qbase + tb * 4 + win) * a.Cs_out + nt0 * 16 + c8 * 8;
+        *reinterpret_cast<uint4*>(a.out + o) = *reinterpret_cast<const uint4*>(epb + win * LDC + c8 * 8);
+        *reinterpret_cast<uint2*>(a.code + o) = *reinterpret_cast<const uint2*>(epc + win * LDC + c8 * 8);
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      // unpooled forward and dgrad (mode 1): stage the TM tiles as bf16, then one copy loop
+      bf16* epb = reinterpret_cast<bf16*>(ep);                // [TM*16 pixels][LDC]
+      const bool fwd = a.mode == 0;
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int p = (tb + t) * 16 + g * 4 + j;
+          const int pc = p < npix ? p : 0;
+          const int pyl = fwo.div(pc);
+          const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (pc - pyl * a.Wo);
+#pragma unroll
+          for (int nt = 0; nt < NTC; ++nt) {
+            const int n = (nt0 + nt) * 16 + r;
+            float x = acc[t][nt][j];
+            if (fwd) {
+              x = 0.f;
+              if (n < a.N) {
+                x = acc[t][nt][j] + (a.bias ? a.bias[n] : 0.f);
+                if (a.relu) x = fmaxf(x, 0.f);
+                if (a.drop_thr)
+                  x = dropout_keep((uint32_t)(m * a.N + n), a.seed, a.stream_id, step, a.drop_thr) ? x * a.drop_scale
+                                                                                                 : 0.f;
+              }
+            }
+            epb[(t * 16 + g * 4 + j) * LDC + nt * 16 + r] = f2bf(x);
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int np = max(0, min(TM * 16, npix - tb * 16));
+      for (int c = lane; c < np * cch; c += 64) {
+        const int pr = fcch.div(c), c8 = c - pr * cch;
+        const int p = tb * 16 + pr;
+        const int pyl = fwo.div(p);
+        const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (p - pyl * a.Wo);
+        const bf16x8 val = *reinterpret_cast<const bf16x8*>(epb + pr * LDC + c8 * 8);
+        if (fwd) {
+          *reinterpret_cast<bf16x8*>(a.out + m * a.Cs_out + nt0 * 16 + c8 * 8) = val;
+        } else {
+          float v[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = bf2f(val[k]);
+          bwd_through_store8(a.bt, m, nt0 * 16 + c8 * 8, v, step);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+

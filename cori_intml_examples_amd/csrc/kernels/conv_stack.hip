@@ -267,9 +267,10 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       obase = A.rows[l + 1][sp][4], OH = A.rows[l + 1][sp][5], ol = N.pad_l, OW = N.Wo + N.KW - 1;
     }
     {
-      LDS uint4* z = (LDS uint4*)out;
+      LDS bf16x8* z = (LDS bf16x8*)out;
       const int nz = (OH * OW * L.Cs_out) >> 3;   // Cs_out % 8 == 0
-      for (int i = tid; i < nz; i += STACK_THREADS) z[i] = uint4{0u, 0u, 0u, 0u};
+      const bf16x8 zero8 = zero_bf16x8();
+      for (int i = tid; i < nz; i += STACK_THREADS) z[i] = zero8;
       const int Wi = L.Wo + L.KW - 1, KHW = L.KH * L.KW, cw = L.Cs_in == 4 ? 4 : 8;
       const int ntab = L.Cs_in == 4 ? L.KS * 8 : L.KS * 4;
       for (int c = tid; c < ntab; c += STACK_THREADS) {
@@ -311,13 +312,14 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       for (int i = tid; i < n; i += STACK_THREADS) {
         const int pix = fc.div(i), c = (i - pix * cch) * 8;
         const int pyo = fw.div(pix), px = pix - pyo * L.Wp;
-        *reinterpret_cast<uint4*>(gout + pix * L.Cs_out + c) =
-            *reinterpret_cast<const LDS uint4*>(out + ((own0 + pyo - obase) * OW + px + ol) * L.Cs_out + c);
+        *reinterpret_cast<bf16x8*>(gout + pix * L.Cs_out + c) =
+            *reinterpret_cast<const LDS bf16x8*>(out + ((own0 + pyo - obase) * OW + px + ol) * L.Cs_out + c);
       }
       if (L.pool && L.code) {
         const int nb = ((own1 - own0) * L.Wp * L.Cs_out) >> 3;
-        uint2* gc = reinterpret_cast<uint2*>(L.code + ((size_t)b * L.Hp + own0) * L.Wp * L.Cs_out);
-        const LDS uint2* lc = (const LDS uint2*)(codes + (own0 - p0) * L.Wp * L.Cs_out);
+        unsigned long long* gc =
+            reinterpret_cast<unsigned long long*>(L.code + ((size_t)b * L.Hp + own0) * L.Wp * L.Cs_out);
+        const LDS unsigned long long* lc = (const LDS unsigned long long*)(codes + (own0 - p0) * L.Wp * L.Cs_out);
         for (int i = tid; i < nb; i += STACK_THREADS) gc[i] = lc[i];
       }
     }
@@ -327,6 +329,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
 
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s) {
   auto k = conv_stack_fwd_kernel;
-  if (a.lds_bytes > 65536) hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, a.lds_bytes);
+  if (a.lds_bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, a.lds_bytes);
   hipLaunchKernelGGL(k, dim3(a.B * a.splits), dim3(STACK_THREADS), a.lds_bytes, s, a);
 }

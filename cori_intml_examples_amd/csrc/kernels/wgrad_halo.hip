@@ -11,195 +11,12 @@
 // of "its" pixel row, with the tap shift folded into the per-lane address (im2col without
 // materialising it).  The bias gradient is one extra MFMA tile with an all-ones A operand.
 // Partials: one fp32 slab per split, summed in fixed order by slab_reduce (deterministic).
-#include "bwd_through.h"
+#include "wgrad_halo_body.h"
 
-__device__ __forceinline__ bf16x4 tr_read_h(const bf16* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, p));
-}
-
-// Each wave owns MTW m-tiles (w, w+4, ...) x all NTT n-tiles of the workgroup, so per
-// k-step it reads NTT B fragments + MTW A fragments for MTW*NTT MFMAs.
 template <int MTW, int NTT, bool CS4>
 __global__ __launch_bounds__(256) void wgrad_halo_kernel(const WgradArgs a, const int MT) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int R = a.R, s = a.stride, Cs = a.Cs_in;
-  const int W_in = (a.Wo - 1) * s + a.KW;
-  const int R_in = (R - 1) * s + a.KH;
-  const int npb = R * a.Wo;                         // pixels per full block
-  const int npb32 = (npb + 31) & ~31;
-  const int ldb = NTT * 16 + 8;                     // dY LDS row stride (elements)
-  bf16* xl = reinterpret_cast<bf16*>(smem);
-  const int x_elems = ((R_in * W_in * Cs) + 7) & ~7;
-  bf16* dyl = xl + x_elems;
-  bf16* zl = dyl + (size_t)npb32 * ldb;             // 64 B of zeros
-  int* ktab = reinterpret_cast<int*>(zl + 32);      // [MT*4] halo offsets of k column blocks
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, g = lane >> 4;
-  const int mt0 = blockIdx.z * MT;
-  const int nt0 = blockIdx.y * NTT;
-  const int KHW = a.KH * a.KW;
-  const bool do_bias = a.bslab != nullptr && blockIdx.z == 0;
-  const int MTb = MT + (do_bias ? 1 : 0);          // pseudo m-tile MT = bias (ones operand)
-
-  if (tid < 32) reinterpret_cast<uint32_t*>(zl)[tid] = 0u;
-  for (int c = tid; c < MT * 4; c += 256) {
-    const int k = (mt0 + c / 4) * 16 + 4 * (c & 3);
-    const int tap = k / Cs;
-    int e = -1;
-    if (tap < KHW && mt0 + c / 4 < a.Ktiles) {
-      const int ky = tap / a.KW;
-      e = (ky * W_in + (tap - ky * a.KW)) * Cs + (k - tap * Cs);
-    }
-    ktab[c] = e;
-  }
-  __syncthreads();
-
-  // per-wave m-tile descriptors (constant over blocks and k-steps)
-  int ko[MTW];
-  bool tbias[MTW], tval[MTW];
-#pragma unroll
-  for (int u = 0; u < MTW; ++u) {
-    const int mt = wave + 4 * u;
-    tval[u] = mt < MTb;
-    tbias[u] = mt == MT && do_bias;
-    ko[u] = (mt < MT) ? ktab[mt * 4 + (i & 3)] : -1;
-  }
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = f2bf(1.f);
-
-  f32x4 acc[MTW][NTT];
-#pragma unroll
-  for (int u = 0; u < MTW; ++u)
-#pragma unroll
-    for (int v = 0; v < NTT; ++v) acc[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nrb = (a.Ho + R - 1) / R;
-  const int nblocks = a.B * nrb;
-  const int blk0 = blockIdx.x * a.blocks_per_split;
-  const int blk1 = min(nblocks, blk0 + a.blocks_per_split);
-  const int cw = CS4 ? 4 : 8;
-  const int cpp = Cs / cw;
-  const FastDiv fcpp(cpp), fwin(W_in), fcpr(NTT * 2), fwo(a.Wo);
-
-  for (int blk = blk0; blk < blk1; ++blk) {
-    const int b = blk / nrb;
-    const int oy0 = (blk - b * nrb) * R;
-    const int rows = min(R, a.Ho - oy0);
-    const int npix = rows * a.Wo;
-    if (blk != blk0) __syncthreads();   // previous block's readers are done
-    const bool dbg_stage = !(a.dbg & 1);
-    if (dbg_stage) {   // X halo
-      const int nch = R_in * W_in * cpp;
-      const int yb = oy0 * s - a.pad_t, xb0 = -a.pad_l;
-      const bf16* xbase = a.x + (size_t)b * a.H * a.W * Cs;
-      auto coords = [&](int idx, int& c, int& iy, int& ix) -> bool {
-        const int pix = fcpp.div(idx);
-        c = (idx - pix * cpp) * cw;
-        const int r = fwin.div(pix);
-        iy = yb + r;
-        ix = xb0 + (pix - r * W_in);
-        return iy >= 0 && ix >= 0 && iy < a.H && ix < a.W;
-      };
-      if (CS4) {
-        staged_copy<8, bf16x4>(
-            nch, tid, 256,
-            [&](int idx) {
-              int c, iy, ix;
-              const bool ok = coords(idx, c, iy, ix);
-              return load_bf16x4_if(ok, xbase + ((size_t)iy * a.W + ix) * 4, xbase);
-            },
-            [&](int idx, const bf16x4& v) { *reinterpret_cast<bf16x4*>(xl + (size_t)idx * 4) = v; });
-      } else {
-        staged_copy<8, bf16x8>(
-            nch, tid, 256,
-            [&](int idx) {
-              int c, iy, ix;
-              const bool ok = coords(idx, c, iy, ix);
-              return load_bf16x8_if(ok, xbase + ((size_t)iy * a.W + ix) * Cs + c, xbase);
-            },
-            [&](int idx, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + (size_t)idx * 8) = v; });
-      }
-    }
-    if (dbg_stage) {   // dY rows (rebuilt from pooled dP + codes when the conv is pooled)
-      const int cpr = NTT * 2;
-      const int nch = npb32 * cpr;
-      const size_t boff = (size_t)b * a.dHp * a.dWp * a.Cs_dy;
-      staged_copy<8, bf16x8>(
-          nch, tid, 256,
-          [&](int idx) {
-            const int p = fcpr.div(idx);
-            const int n0 = nt0 * 16 + (idx - p * cpr) * 8;
-            const bool ok = p < npix && n0 < a.Cs_dy;
-            const int pp = ok ? p : 0;
-            const int pyl = fwo.div(pp);
-            const int oy = oy0 + pyl, ox = pp - pyl * a.Wo;
-            if (a.dy_code) return unpool_load8(a.dy + boff, a.dy_code + boff, a.dHp, a.dWp, a.Cs_dy, oy, ox, n0, ok);
-            return load_bf16x8_if(ok, a.dy + (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.Cs_dy + n0, a.dy);
-          },
-          [&](int idx, const bf16x8& v) {
-            const int p = fcpr.div(idx);
-            *reinterpret_cast<bf16x8*>(dyl + (size_t)p * ldb + (idx - p * cpr) * 8) = v;
-          });
-    }
-    __syncthreads();
-    const int nks = (a.dbg & 2) ? 0 : (npix + 31) >> 5;
-    for (int ks = 0; ks < nks; ++ks) {
-      // per-lane pixel rows of the two transposed reads (h = 0, 1)
-      const int P0 = ks * 32 + 8 * g + (i >> 2);
-      const int q0 = min(P0, npix - 1), q1 = min(P0 + 4, npix - 1);
-      const int y0 = fwo.div(q0), y1 = fwo.div(q1);
-      const int off0 = ((y0 * s) * W_in + (q0 - y0 * a.Wo) * s) * Cs;
-      const int off1 = ((y1 * s) * W_in + (q1 - y1 * a.Wo) * s) * Cs;
-      const bf16* pbrow = dyl + (size_t)P0 * ldb + 4 * (i & 3);
-      bf16x8 bfr[NTT], afr[MTW];
-#pragma unroll
-      for (int v = 0; v < NTT; ++v) {
-        const bf16* pb = pbrow + v * 16;
-        bfr[v] = __builtin_shufflevector(tr_read_h(pb), tr_read_h(pb + 4 * ldb), 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int u = 0; u < MTW; ++u) {
-        const bf16* pa0 = ko[u] >= 0 ? xl + off0 + ko[u] : zl;
-        const bf16* pa1 = ko[u] >= 0 ? xl + off1 + ko[u] : zl;
-        afr[u] = tbias[u] ? ones : __builtin_shufflevector(tr_read_h(pa0), tr_read_h(pa1), 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int u = 0; u < MTW; ++u)
-        if (tval[u]) {
-#pragma unroll
-          for (int v = 0; v < NTT; ++v) acc[u][v] = mfma16(afr[u], bfr[v], acc[u][v]);
-        }
-    }
-  }
-
-  const int ld = a.NT * 16;
-  float* slab = a.slab + (size_t)blockIdx.x * a.Ktiles * 16 * ld;
-  if (a.dbg & 4) {
-#pragma unroll
-    for (int u = 0; u < MTW; ++u)
-#pragma unroll
-      for (int v = 0; v < NTT; ++v)
-        asm volatile("" ::"v"(acc[u][v][0]), "v"(acc[u][v][1]), "v"(acc[u][v][2]), "v"(acc[u][v][3]));
-    return;
-  }
-#pragma unroll
-  for (int u = 0; u < MTW; ++u) {
-    const int mt = wave + 4 * u;
-    if (!tval[u]) continue;
-#pragma unroll
-    for (int v = 0; v < NTT; ++v) {
-      if (nt0 + v >= a.NT) continue;
-      if (tbias[u]) {   // bias tile: every row holds the column sums; row 0 lives in lanes 0..15
-        if (g == 0) a.bslab[(size_t)blockIdx.x * ld + (nt0 + v) * 16 + i] = acc[u][v][0];
-        continue;
-      }
-      if (mt0 + mt >= a.Ktiles) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        slab[(size_t)((mt0 + mt) * 16 + g * 4 + j) * ld + (nt0 + v) * 16 + i] = acc[u][v][j];
-    }
-  }
+  wgrad_halo_body<MTW, NTT, CS4>(a, MT, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT) {

@@ -676,6 +676,7 @@ class BatchPlan:
                 wa, cfg, slab, bslab = self._wgrad_halo_args(xin, g, bs, cs.conv.use_bias)
                 self.launches.append(("wgrad_conv%d" % g.i,
                                       lambda s, a=wa, c=cfg: K.wgrad_halo(a, c[0], c[1], c[2], s), "side"))
+            w_at = len(self.launches) - 1
             sp = store.spec(cs.conv, "kernel")
             S, ld = cfg[2], g.NT * 16
             descs = [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel, RED_CONVW,
@@ -704,8 +705,18 @@ class BatchPlan:
                 a.mode, a.flat_out = 1, 0
                 a.st = st_ptr
                 a.bt = self._bt_for(Src("conv", prev.i, prev.Cout, prev.Cs_out, prev.Hp, prev.Wp))
-                self.launches.append(("dgrad_conv%d" % g.i, self._conv_launch(a, g.NTd, False)))
-                self.pack_readers.append(("dgrad_conv%d" % g.i, sp.offset, sp.offset + sp.numel))
+                dname = "dgrad_conv%d" % g.i
+                dual = (self.side is None and env_flag("INTML_DUAL_HALO", True)
+                        and not self._wide(g.Cs_in, g.KS, g.NT) and not self._wide(a.Cs_in, a.KS, g.NTd))
+                if dual:
+                    # one launch for the layer's wgrad and dgrad (independent GEMMs sharing dY):
+                    # replaces the wgrad launch in place (its slabs are final after it)
+                    ntc = self._halo_cfg(a, g.NTd, False)
+                    dname = "wgrad_dgrad_conv%d" % g.i
+                    self.launches[w_at] = (dname, lambda s, a=a, n=ntc, w=wa, c=cfg: self._dual(a, n, w, c, s), "main")
+                else:
+                    self.launches.append((dname, self._conv_launch(a, g.NTd, False)))
+                self.pack_readers.append((dname, sp.offset, sp.offset + sp.numel))
         self._build_reduce()
 
     LDS_LIMIT = 160 * 1024
@@ -854,6 +865,12 @@ class BatchPlan:
             return lambda s, a=a, n=ntc: K.conv_tile(a, n, s)
         ntc = self._halo_cfg(a, NT, pool)
         return lambda s, a=a, n=ntc: K.conv_halo(a, n, s)
+
+    def _dual(self, a, ntc, wa, cfg, s):
+        K = self.ex.K
+        if not K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s):   # unsupported combination
+            K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
+            K.conv_halo(a, ntc, s)
 
     def _halo_cfg(self, a, NT, pool):
         """Pick n-tiles per workgroup (weight LDS slice) and R output rows per block."""
