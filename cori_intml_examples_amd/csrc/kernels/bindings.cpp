@@ -28,6 +28,8 @@ bool dense_big(int NT, int KS);
 void launch_head(const HeadArgs& a, hipStream_t s);
 bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits,
                       hipStream_t s);
+bool launch_dense_bwd_dual(const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da,
+                           hipStream_t s);
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s);
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
 int gather_gx(int R);
@@ -240,6 +242,11 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("prologue", [](const PrologueArgs& a, const PackTable& t, uintptr_t s) {
     launch_prologue(a, t, S(s)); check_last("prologue"); });
   m.def("gather_gx", &gather_gx);
+  m.def("dense_bwd_dual", [](const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da, uintptr_t s) {
+    const bool ok = launch_dense_bwd_dual(wa, ktw, ntt, splits, da, S(s));
+    check_last("dense_bwd_dual");
+    return ok;
+  });
   m.def("dual_halo", [](const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits, uintptr_t s) {
     const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, S(s));
     check_last("dual_halo");

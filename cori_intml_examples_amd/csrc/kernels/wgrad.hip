@@ -13,19 +13,19 @@
 // (grid.y, 4 waves each own k-tiles w, w+4, ...) and over n-tile groups (grid.z).
 // Also used for dense layers (1x1 conv over a 1x1 image, pixels = batch rows).
 // Bias gradient = column sums of the staged dY tile (grid.y == 0 workgroups).
-#include "args.h"
+#include "dense_body.h"
 
 __device__ __forceinline__ bf16x4 tr_read(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, p));
 }
 
 template <int KTW, int NTT, bool CS4>
-__global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void wgrad_body(const WgradArgs& a, const int bx, const int by, const int bz,
+                                           char* smem) {
   const int KT = a.KT;
-  const int kt0 = blockIdx.y * KT;
+  const int kt0 = by * KT;
   const int ktn = min(KT, a.Ktiles - kt0);
-  const int ntb = blockIdx.z * NTT;
+  const int ntb = bz * NTT;
   const int lda = KT * 16 + 16;
   const int ldb = NTT * 16 + 16;
   bf16* As = reinterpret_cast<bf16*>(smem);
@@ -41,9 +41,9 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 #pragma unroll
     for (int v = 0; v < NTT; ++v) acc[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc = 0.f;
-  const bool do_bias = a.bslab != nullptr && blockIdx.y == 0;
+  const bool do_bias = a.bslab != nullptr && by == 0;
 
-  const long long p_begin = (long long)blockIdx.x * a.px_per_split;
+  const long long p_begin = (long long)bx * a.px_per_split;
   const long long p_end = min((long long)a.P, p_begin + a.px_per_split);
   const int cpr = KT * 2;
   const int cpb = NTT * 2;
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
   }
 
   const int ld = NTtot * 16;
-  float* slab = a.slab + (size_t)blockIdx.x * a.Ktiles * 16 * ld;
+  float* slab = a.slab + (size_t)bx * a.Ktiles * 16 * ld;
 #pragma unroll
   for (int u = 0; u < KTW; ++u) {
     const int kt = wave + 4 * u;
@@ -142,7 +142,13 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
       }
     }
   }
-  if (do_bias && tid < NTT * 16 && ntb * 16 + tid < ld) a.bslab[(size_t)blockIdx.x * ld + ntb * 16 + tid] = bacc;
+  if (do_bias && tid < NTT * 16 && ntb * 16 + tid < ld) a.bslab[(size_t)bx * ld + ntb * 16 + tid] = bacc;
+}
+
+template <int KTW, int NTT, bool CS4>
+__global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  wgrad_body<KTW, NTT, CS4>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 size_t wgrad_lds_bytes(int KT, int NTT) {
@@ -171,4 +177,52 @@ void launch_wgrad(const WgradArgs& a, int ktw, int ntt, int splits, hipStream_t 
   C2(2, 1) C2(2, 2) C2(2, 4) C2(2, 8)
   C2(4, 1) C2(4, 2) C2(4, 4)
 #undef C2
+}
+
+// Dense backward as ONE launch: the dense wgrad (dW = X^T dH, split over the batch) and the
+// dense dX = dH W^T routed through the previous stage's masks are independent GEMMs over
+// the same dH, so workgroups [0, n_w) run the wgrad body and the rest the split-K body
+// (one kernel boundary instead of two, and the 64 long wgrad workgroups no longer leave
+// most CUs idle).
+template <int KTW, int NTT>
+__global__ __launch_bounds__(256) void dense_bwd_dual_kernel(const WgradArgs wa, const DenseFwdArgs da, const int n_w,
+                                                             const int wgx, const int wgy) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int id = blockIdx.x;
+  if (id < n_w) {
+    const int bx = id % wgx;
+    id /= wgx;
+    wgrad_body<KTW, NTT, false>(wa, bx, id % wgy, id / wgy, smem);
+  } else {
+    dense_splitk_body(da, id - n_w);
+  }
+}
+
+bool dense_big(int NT, int KS);
+
+template <int KTW, int NTT>
+static void dd_t(const WgradArgs& wa, const DenseFwdArgs& da, dim3 wg, size_t lds, hipStream_t s) {
+  const int n_w = wg.x * wg.y * wg.z;
+  const long long waves = (long long)((da.M + 15) / 16) * da.NT * da.splits;
+  const int n_d = (int)((waves + 3) / 4);
+  hipLaunchKernelGGL((dense_bwd_dual_kernel<KTW, NTT>), dim3(n_w + n_d), dim3(256), lds, s, wa, da, n_w,
+                     (int)wg.x, (int)wg.y);
+}
+
+// false = unsupported combination (nothing launched): the caller launches both separately
+bool launch_dense_bwd_dual(const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da,
+                           hipStream_t s) {
+  if (wa.Cs_in == 4 || dense_big(da.NT, da.KS) || da.mode != 1) return false;
+  const dim3 wg(splits, (wa.Ktiles + wa.KT - 1) / wa.KT, (wa.NT + ntt - 1) / ntt);
+  const size_t lds = wgrad_lds_bytes(wa.KT, ntt);
+#define C2(KW_, NT_)                              \
+  if (ktw == KW_ && ntt == NT_) {                 \
+    dd_t<KW_, NT_>(wa, da, wg, lds, s);           \
+    return true;                                  \
+  }
+  C2(1, 1) C2(1, 2) C2(1, 4) C2(1, 8)
+  C2(2, 1) C2(2, 2) C2(2, 4) C2(2, 8)
+  C2(4, 1) C2(4, 2) C2(4, 4)
+#undef C2
+  return false;
 }

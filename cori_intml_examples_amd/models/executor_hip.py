@@ -643,6 +643,7 @@ class BatchPlan:
                 ds.dense.use_bias, direct=(store.grad.data_ptr() + 4 * sp.offset) if direct else None)
             self.launches.append(("wgrad_dense%d" % g.j, lambda s, a=wa, c=cfg: K.wgrad(a, c[0], c[1], c[2], s),
                                   "side"))
+            w_at = len(self.launches) - 1
             S, ld = cfg[2], g.NT * 16
             descs = [] if direct else [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel,
                                         RED_FLATW, 0, 0, g.src.C, g.N, g.src.Cs)]
@@ -663,8 +664,15 @@ class BatchPlan:
                 a.mode = 1
                 a.st = st_ptr
                 a.bt = self._bt_for(g.src)
-                self.launches.append(("dense_dx%d" % g.j, lambda s, a=a: K.dense_fwd(a, s)))
-                self.pack_readers.append(("dense_dx%d" % g.j, sp.offset, sp.offset + sp.numel))
+                dname = "dense_dx%d" % g.j
+                if self.side is None and env_flag("INTML_DUAL_DENSE", True):
+                    # one launch for the dense wgrad and dX (independent GEMMs over dH), in the
+                    # wgrad's slot (its slabs are final after it)
+                    dname = "dense_bwd%d" % g.j
+                    self.launches[w_at] = (dname, lambda s, a=a, w=wa, c=cfg: self._dense_dual(w, c, a, s), "main")
+                else:
+                    self.launches.append((dname, lambda s, a=a: K.dense_fwd(a, s)))
+                self.pack_readers.append((dname, sp.offset, sp.offset + sp.numel))
 
         for g, cs in reversed(list(zip(ex.convs, ex.plan.convs))):
             xin = self.xb if g.i == 0 else self.conv_out[g.i - 1]
@@ -866,6 +874,12 @@ class BatchPlan:
         ntc = self._halo_cfg(a, NT, pool)
         return lambda s, a=a, n=ntc: K.conv_halo(a, n, s)
 
+    def _dense_dual(self, wa, cfg, da, s):
+        K = self.ex.K
+        if not K.dense_bwd_dual(wa, cfg[0], cfg[1], cfg[2], da, s):   # unsupported combination
+            K.wgrad(wa, cfg[0], cfg[1], cfg[2], s)
+            K.dense_fwd(da, s)
+
     def _dual(self, a, ntc, wa, cfg, s):
         K = self.ex.K
         if not K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s):   # unsupported combination
@@ -961,7 +975,8 @@ class BatchPlan:
         groups = cdiv(NT, NTT) * cdiv(a.Ktiles, MT)
         per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
         s_budget = max(1, (8 << 20) // per_split_bytes)
-        S = max(1, min(nblocks, s_budget, max(1, 2048 // groups)))
+        cap = int(os.environ.get("INTML_WGRAD_SPLITS", "1024"))
+        S = max(1, min(nblocks, s_budget, max(1, cap // groups)))
         bps = cdiv(nblocks, S)
         S = cdiv(nblocks, bps)
         a.blocks_per_split = bps
@@ -1028,7 +1043,11 @@ class BatchPlan:
         if reducer is not None:
             bucket_groups = reducer.configure(groups)
         else:
-            limit = int(os.environ.get("INTML_BUCKET_BYTES", 1 << 20))
+            # single stream, no all-reduce to overlap: ONE reduction launch at the end of the
+            # backward (each launch boundary costs ~5 us here), if the descriptors fit a table
+            ndesc = sum(len(d) for _, _, d in self.red_groups)
+            one = self.side is None and ndesc <= 16
+            limit = 1 << 62 if one else int(os.environ.get("INTML_BUCKET_BYTES", 1 << 20))
             bucket_groups, cur, nb = [], [], 0
             for gi, (lo, hi) in enumerate(groups):
                 cur.append(gi)

@@ -23,6 +23,29 @@ _DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64:
 _OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
 
 
+class _stdout_to_stderr:
+    """Route fd 1 to fd 2 for the duration (library banners must not mix with a program's
+    machine-readable stdout, e.g. bench.py's single JSON line)."""
+
+    def __enter__(self):
+        import ctypes
+        import sys
+        self._libc = ctypes.CDLL(None)
+        sys.stdout.flush()
+        self._libc.fflush(None)
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        import sys
+        sys.stdout.flush()
+        self._libc.fflush(None)
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        return False
+
+
 def _module():
     from .. import _comm          # built in-tree by _build.build_comm
     return _comm
@@ -49,15 +72,16 @@ class NativeComm:
             if size > 1:
                 tdist.broadcast_object_list(box, src=0)    # over the gloo control plane
             uid = box[0]
-        self._c = m.Comm(uid, size, rank, device.index if device.index is not None else 0)
-        self.timeout_s = timeout_s
-        if timeout_s and timeout_s > 0:
-            self._c.start_watchdog(float(timeout_s))
-        # one-time connection setup outside any graph capture (RCCL connects lazily on the
-        # first collective, which must not happen inside a capture)
-        t = torch.zeros(256, dtype=torch.float32, device=device)
-        self.all_reduce(t)
-        torch.cuda.current_stream(device).synchronize()
+        with _stdout_to_stderr():      # RCCL prints a version banner on stdout at init
+            self._c = m.Comm(uid, size, rank, device.index if device.index is not None else 0)
+            self.timeout_s = timeout_s
+            if timeout_s and timeout_s > 0:
+                self._c.start_watchdog(float(timeout_s))
+            # one-time connection setup outside any graph capture (RCCL connects lazily on
+            # the first collective, which must not happen inside a capture)
+            t = torch.zeros(256, dtype=torch.float32, device=device)
+            self.all_reduce(t)
+            torch.cuda.current_stream(device).synchronize()
 
     # ------------------------------------------------------------------ collectives
     @staticmethod
