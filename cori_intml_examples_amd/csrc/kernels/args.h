@@ -161,6 +161,10 @@ struct HeadArgs {
   float* bslab = nullptr;        // [nblocks][N]
   // gradient wrt the previous stage (hidden dense or flattened conv); bt.dy == null: skip
   BwdThrough bt;
+  // fused epilogue of the previous dense layer (epi.part != null): the head's workgroup
+  // reduces the split-K partials of its rows itself (bias, ReLU, dropout), writes that
+  // layer's bf16 output and uses it as h -- one launch instead of two
+  DenseEpiArgs epi;
 };
 
 struct GatherArgs {

@@ -19,6 +19,7 @@ size_t wgrad_tile_lds_bytes(int ntc);
 void launch_wgrad_halo(const WgradArgs& a, int MT, int NTT, int splits, hipStream_t s);
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT);
 int head_rows_per_block();
+int head_epi_max();
 void launch_wgrad(const WgradArgs& a, int ktw, int ntt, int splits, hipStream_t s);
 size_t wgrad_lds_bytes(int KT, int NTT);
 void launch_dense_fwd(const DenseFwdArgs& a, hipStream_t s);
@@ -34,6 +35,7 @@ void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s);
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
 int gather_gx(int R);
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s);
+void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, hipStream_t s);
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s);
 void launch_pack(const float* master, bf16* arena, const PackTable& tab, hipStream_t s);
 
@@ -100,7 +102,7 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(HeadArgs, h) RW(HeadArgs, M) RW(HeadArgs, K) RW(HeadArgs, Ks) RW(HeadArgs, N)
       RW(HeadArgs, flat_C) RW(HeadArgs, flat_Cs) PTR(HeadArgs, w) PTR(HeadArgs, bias) PTR(HeadArgs, y)
       RW(HeadArgs, act) RW(HeadArgs, training) RW(HeadArgs, inv_bs) PTR(HeadArgs, st) PTR(HeadArgs, probs)
-      PTR(HeadArgs, wslab) PTR(HeadArgs, bslab) RW(HeadArgs, bt);
+      PTR(HeadArgs, wslab) PTR(HeadArgs, bslab) RW(HeadArgs, bt) RW(HeadArgs, epi);
 
   py::class_<GatherArgs>(m, "GatherArgs")
       .def(py::init<>())
@@ -242,6 +244,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("prologue", [](const PrologueArgs& a, const PackTable& t, uintptr_t s) {
     launch_prologue(a, t, S(s)); check_last("prologue"); });
   m.def("gather_gx", &gather_gx);
+  m.def("head_epi_max", &head_epi_max);
+  m.def("reduce_optim", [](uintptr_t grad, const RedTable& t, const OptimArgs& a, uintptr_t s) {
+    launch_reduce_optim(reinterpret_cast<float*>(grad), t, a, S(s)); check_last("reduce_optim"); });
   m.def("dense_bwd_dual", [](const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da, uintptr_t s) {
     const bool ok = launch_dense_bwd_dual(wa, ktw, ntt, splits, da, S(s));
     check_last("dense_bwd_dual");

@@ -249,8 +249,8 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   }
 
   for (int l = 0; l < A.n; ++l) {
-    const StackLayer& L = A.L[l];
-    const bool last = l + 1 == A.n;
+    const StackLayer L = A.L[l];      // by value: one batch of scalar loads per layer instead of
+    const bool last = l + 1 == A.n;   // a kernarg reload of every field after each barrier
     const int c0 = A.rows[l][sp][0], c1 = A.rows[l][sp][1];
     const int own0 = A.rows[l][sp][2], own1 = A.rows[l][sp][3];
     const int p0 = L.pool ? c0 >> 1 : c0;

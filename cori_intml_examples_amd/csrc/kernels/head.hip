@@ -11,15 +11,56 @@
 #include "bwd_through.h"
 
 #define HEAD_RB 4
+#define HEAD_EPI_MAX 1024   // widest previous dense whose epilogue the head absorbs
+
+// dense_epilogue_kernel's value for (m, n): the same 4-way interleaved split order
+// (bit-identical), then bias, ReLU, dropout.
+__device__ __forceinline__ float dense_epi_value(const DenseEpiArgs& e, int m, int n, uint32_t step) {
+  const size_t stride = (size_t)e.M * e.ldp;
+  const float* p = e.part + (size_t)m * e.ldp + n;
+  float r4[4];
+#pragma unroll
+  for (int sg = 0; sg < 4; ++sg) {
+    float a0 = 0.f, a1 = 0.f;
+    int s = sg;
+    for (; s + 4 < e.splits; s += 8) {
+      a0 += p[(size_t)s * stride];
+      a1 += p[(size_t)(s + 4) * stride];
+    }
+    for (; s < e.splits; s += 4) a0 += p[(size_t)s * stride];
+    r4[sg] = a0 + a1;
+  }
+  float v = (r4[0] + r4[1]) + (r4[2] + r4[3]);
+  if (e.bias) v += e.bias[n];
+  if (e.relu) v = fmaxf(v, 0.f);
+  if (e.drop_thr)
+    v = dropout_keep((uint32_t)(m * e.N + n), e.seed, e.stream_id, step, e.drop_thr) ? v * e.drop_scale : 0.f;
+  return v;
+}
 
 __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   __shared__ float dz_s[HEAD_RB][16];
   __shared__ float met[HEAD_RB][2];
+  __shared__ bf16 hs[HEAD_RB][HEAD_EPI_MAX];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int row0 = blockIdx.x * HEAD_RB;
   const int N = a.N;
   const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
   const int row = row0 + wave;
+  const bool fused = a.epi.part != nullptr;
+  if (fused) {   // previous dense layer's epilogue for this workgroup's rows
+    const DenseEpiArgs& e = a.epi;
+    const int nr = min(HEAD_RB, a.M - row0);
+    for (int idx = tid; idx < nr * e.Ns; idx += 256) {
+      const int rl = idx / e.Ns, n = idx - rl * e.Ns;
+      const int m = row0 + rl;
+      const bf16 hb = f2bf(n < e.N ? dense_epi_value(e, m, n, step) : 0.f);
+      hs[rl][n] = hb;
+      e.out[(size_t)m * e.Ns + n] = hb;     // saved activation (ReLU mask of the backward)
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
   if (a.st && blockIdx.x == 0 && tid == 0) {
     // advance the data cursor the step prologue gathered from (it must not move while
     // prologue workgroups read it) and mark the weight packs fresh (this step's prologue
@@ -36,7 +77,7 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
     const bf16* hr = a.h + (size_t)row * a.Ks;
     for (int k = lane; k < a.K; k += 64) {
       const int kp = a.flat_C ? flat_keras_to_padded(k, a.flat_C, a.flat_Cs) : k;
-      const float hv = bf2f(hr[kp]);
+      const float hv = fused ? bf2f(hs[wave][kp]) : bf2f(hr[kp]);
       const float* wr = a.w + (size_t)k * N;
 #pragma unroll
       for (int n = 0; n < 16; ++n)
@@ -133,7 +174,8 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
     const int k = idx / N, n = idx - (idx / N) * N;
     const int kp = a.flat_C ? flat_keras_to_padded(k, a.flat_C, a.flat_Cs) : k;
     float s = 0.f;
-    for (int rl = 0; rl < rows_here; ++rl) s += bf2f(a.h[(size_t)(row0 + rl) * a.Ks + kp]) * dz_s[rl][n];
+    for (int rl = 0; rl < rows_here; ++rl)
+      s += (fused ? bf2f(hs[rl][kp]) : bf2f(a.h[(size_t)(row0 + rl) * a.Ks + kp])) * dz_s[rl][n];
     ws[idx] = s;
   }
   if (tid < N && a.bslab) {
@@ -166,3 +208,4 @@ void launch_head(const HeadArgs& a, hipStream_t s) {
 }
 
 int head_rows_per_block() { return HEAD_RB; }
+int head_epi_max() { return HEAD_EPI_MAX; }

@@ -73,8 +73,8 @@ __device__ __forceinline__ void gather_block(const GatherArgs& a, const StepStat
 // addresses of one slab: coalesced) and split-lane t / E (the tpe split-lanes of an
 // element sum interleaved subsets of the S slabs with independent unrolled loads).  The tpe
 // partials are combined through LDS in a fixed order -> bitwise reproducible.
-__global__ __launch_bounds__(256) void slab_reduce_kernel(float* __restrict__ grad, const RedTable tab) {
-  __shared__ float red[256];
+// Returns true on the thread that holds the final sum of element `dst` (in `val`).
+__device__ __forceinline__ bool slab_reduce_elem(const RedTable& tab, float* red, int& dst, float& val) {
   int di = 0;
   while (di + 1 < tab.n && (int)blockIdx.x >= tab.d[di + 1].blk0) ++di;
   const RedDesc& d = tab.d[di];
@@ -113,17 +113,25 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(float* __restrict__ gr
     for (; s < d.S; s += tpe) a0 += p[(size_t)s * st];
     acc = (a0 + a1) + (a2 + a3);
   }
+  dst = d.dst_off + le;
   if (tpe == 1) {
-    if (in) grad[d.dst_off + le] = acc;
-    return;
+    val = acc;
+    return in;
   }
   red[threadIdx.x] = acc;
   __syncthreads();
-  if (lane == 0 && in) {
-    float sum = 0.f;
-    for (int k = 0; k < tpe; ++k) sum += red[k * E + el];
-    grad[d.dst_off + le] = sum;
-  }
+  if (lane != 0 || !in) return false;
+  float sum = 0.f;
+  for (int k = 0; k < tpe; ++k) sum += red[k * E + el];
+  val = sum;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void slab_reduce_kernel(float* __restrict__ grad, const RedTable tab) {
+  __shared__ float red[256];
+  int e;
+  float v;
+  if (slab_reduce_elem(tab, red, e, v)) grad[e] = v;
 }
 
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s) {
@@ -378,4 +386,39 @@ void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s) {
   }
   if (!a.defer_pack || a.pack_only)
     launch_pack(a.p, a.arena, tab, s);    // the MFMA kernels read the bf16 packs
+}
+
+// ---------------------------------------------------------------------------------------
+// Final slab reduction fused with the optimizer (single GPU: nothing sits between them).
+// The thread that produces an element's gradient applies the Keras update to it at once:
+// the optimizer's own launch and its re-read of the gradient go away.  Used only when the
+// reduction table covers every parameter (no gradient written directly by its kernel).
+template <int KIND>
+__global__ __launch_bounds__(256) void reduce_optim_kernel(float* __restrict__ grad, const RedTable tab,
+                                                           const OptimArgs a) {
+  __shared__ float red[256];
+  int e;
+  float g;
+  if (slab_reduce_elem(tab, red, e, g)) {
+    grad[e] = g;
+    float p = a.p[e];
+    float s0 = a.s0 ? a.s0[e] : 0.f, s1 = a.s1 ? a.s1[e] : 0.f;
+    opt_update<KIND>(a, a.st, p, g * a.grad_scale, &s0, &s1);
+    a.p[e] = p;
+    if (a.s0) a.s0[e] = s0;
+    if (a.s1) a.s1[e] = s1;
+  }
+  if (a.defer_pack && blockIdx.x == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
+}
+
+void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, hipStream_t s) {
+  if (tab.nblocks <= 0) return;
+  const dim3 g(tab.nblocks), b(256);
+  switch (a.kind) {
+    case OPT_ADAM: hipLaunchKernelGGL(reduce_optim_kernel<OPT_ADAM>, g, b, 0, s, grad, tab, a); break;
+    case OPT_NADAM: hipLaunchKernelGGL(reduce_optim_kernel<OPT_NADAM>, g, b, 0, s, grad, tab, a); break;
+    case OPT_ADADELTA: hipLaunchKernelGGL(reduce_optim_kernel<OPT_ADADELTA>, g, b, 0, s, grad, tab, a); break;
+    case OPT_RMSPROP: hipLaunchKernelGGL(reduce_optim_kernel<OPT_RMSPROP>, g, b, 0, s, grad, tab, a); break;
+    default: hipLaunchKernelGGL(reduce_optim_kernel<OPT_SGD>, g, b, 0, s, grad, tab, a); break;
+  }
 }

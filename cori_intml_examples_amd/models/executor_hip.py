@@ -418,6 +418,7 @@ class BatchPlan:
         self.early_optim = self.training and env_flag("INTML_EARLY_OPTIM", False)
         self.opt_stream = torch.cuda.Stream(device=dev) if self.early_optim else None
         self.opt_at = []
+        self.optim_fused = False           # set by _build_reduce
         # Native RCCL data plane: the bucket all-reduces are part of the launch sequence (on
         # their own comm stream) and captured with the rest of the step into ONE HIP graph.
         red = ex.reducer
@@ -565,6 +566,7 @@ class BatchPlan:
             x_buf = self.conv_out[g.i]
 
         # ---------------- forward denses
+        head_epi = None
         for g, ds in zip(ex.denses, ex.plan.denses):
             splits, kps = self.dense_splits[g.j]
             a = K.DenseFwdArgs()
@@ -585,7 +587,13 @@ class BatchPlan:
                 e.drop_thr = keep_threshold(g.rate)
                 e.drop_scale = 1.0 / (1.0 - g.rate)
             e.seed, e.stream_id, e.st = ex.seed, g.stream, st_ptr
-            self.launches.append(("dense_epi%d" % g.j, lambda s, e=e: K.dense_epi(e, s)))
+            if (g.j == len(ex.denses) - 1 and ex.head_src.kind == "dense" and g.Ns <= K.head_epi_max()
+                    and env_flag("INTML_FUSE_HEAD", False)):
+                # opt-in: measured slower at batch 128 (the head's 32 workgroups then serialise
+                # the split-K reduction the 256-workgroup epilogue spreads over the chip)
+                head_epi = e          # the head launch reduces this layer's partials itself
+            else:
+                self.launches.append(("dense_epi%d" % g.j, lambda s, e=e: K.dense_epi(e, s)))
 
         # ---------------- head
         hd = ex.plan.head
@@ -598,6 +606,8 @@ class BatchPlan:
         h.bias = store.view(hd.dense, "bias").data_ptr() if hd.dense.use_bias else 0
         h.y = self.yb.data_ptr() if self.mode != "predict" else 0
         h.act = ex.head_act
+        if head_epi is not None:
+            h.epi = head_epi
         h.training = int(training)
         h.inv_bs = 1.0 / bs
         h.st = st_ptr
@@ -1048,6 +1058,10 @@ class BatchPlan:
             ndesc = sum(len(d) for _, _, d in self.red_groups)
             one = self.side is None and ndesc <= 16
             limit = 1 << 62 if one else int(os.environ.get("INTML_BUCKET_BYTES", 1 << 20))
+            # ... with the optimizer fused into it when its table covers every parameter
+            covered = sum(d[5] for _, _, ds in self.red_groups for d in ds)
+            self.optim_fused = (one and not self.early_optim and covered == ex.store.numel
+                                and env_flag("INTML_FUSE_OPTIM", True))
             bucket_groups, cur, nb = [], [], 0
             for gi, (lo, hi) in enumerate(groups):
                 cur.append(gi)
@@ -1166,7 +1180,11 @@ class BatchPlan:
 
     def _launch_bucket_reduce(self, k, s):
         lo, hi, tab = self.bucket_tables[k]
-        self.ex.K.slab_reduce(self.ex.store.grad.data_ptr(), lo, hi, tab, s)
+        ex = self.ex
+        if self.optim_fused:     # gradient reduction + Keras update in one launch (re-pack deferred)
+            ex.K.reduce_optim(ex.store.grad.data_ptr(), tab, ex._optim_args(False, defer_pack=True), s)
+        else:
+            ex.K.slab_reduce(ex.store.grad.data_ptr(), lo, hi, tab, s)
 
     def _launch_optim(self):
         ex = self.ex
@@ -1175,7 +1193,7 @@ class BatchPlan:
 
     def _body(self, with_optim: bool):
         self._run_seq()
-        if self.training and with_optim and not self.early_optim:
+        if self.training and with_optim and not self.early_optim and not self.optim_fused:
             self._launch_optim()
 
     def _dp_segments(self):

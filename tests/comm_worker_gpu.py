@@ -73,6 +73,8 @@ def main(out):
         results[name]["comm_in_graph"] = bool(plan.comm_in_graph)
         results[name]["n_comm_launches"] = sum(1 for it in plan.launches if len(it) > 2 and it[2] == "comm")
         results[name]["max_abs_diff"] = float(np.abs(w - wb).max())
+        results[name]["w"] = w
+    results["captured_vs_segmented"] = float(np.abs(results["captured"].pop("w") - results["segmented"].pop("w")).max())
     os.environ["INTML_COMM_CAPTURE"] = "1"
     opt = hvd.DistributedOptimizer("Adam", compression=hvd.Compression.fp16)
     m = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw)

@@ -58,7 +58,10 @@ def test_native_comm_engine_gpu(tmp_path):
     cap, seg = rep["train"]["captured"], rep["train"]["segmented"]
     assert cap["reducer"] == "NativeGradReducer" and cap["comm_in_graph"]
     assert cap["n_comm_launches"] == len(cap["buckets"]) == 2
-    assert cap["max_abs_diff"] == 0.0, cap           # size-1 all-reduce in the graph is exact
-    assert not seg["comm_in_graph"] and seg["max_abs_diff"] == 0.0, seg
+    # size-1 all-reduce is exact: both DP modes agree bit for bit; against the single-GPU
+    # step (whose optimizer is fused into the gradient reduction) only fp contraction differs
+    assert rep["train"]["captured_vs_segmented"] == 0.0, rep["train"]
+    assert cap["max_abs_diff"] < 1e-4, cap
+    assert not seg["comm_in_graph"] and seg["max_abs_diff"] < 1e-4, seg
     assert rep["train"]["bf16_wire"]["rel_diff"] < 0.05, rep["train"]["bf16_wire"]
     assert rep["abort_raises"] and rep["healthy"], rep
