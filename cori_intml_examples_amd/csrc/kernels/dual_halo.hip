@@ -25,7 +25,7 @@ __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, con
   if (id < n_w) {
     const int bx = id % wgx;
     id /= wgx;
-    wgrad_halo_body<MTW, NTT, false>(wa, MT, bx, id % wgy, id / wgy, smem);
+    wgrad_halo_body<MTW, NTT, false, true>(wa, MT, bx, id % wgy, id / wgy, smem);
   } else {
     id -= n_w;
     conv_halo_body<NTC, TM, 8, false>(ca, id % cgx, id / cgx, smem);

@@ -13,10 +13,10 @@
 // Partials: one fp32 slab per split, summed in fixed order by slab_reduce (deterministic).
 #include "wgrad_halo_body.h"
 
-template <int MTW, int NTT, bool CS4>
+template <int MTW, int NTT, bool CS4, bool PIPE>
 __global__ __launch_bounds__(256) void wgrad_halo_kernel(const WgradArgs a, const int MT) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  wgrad_halo_body<MTW, NTT, CS4>(a, MT, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  wgrad_halo_body<MTW, NTT, CS4, PIPE>(a, MT, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT) {
@@ -29,8 +29,11 @@ size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT) {
 
 template <int MTW, int NTT, bool CS4>
 static void wh_t(const WgradArgs& a, int MT, dim3 grid, size_t lds, hipStream_t s) {
-  auto k = wgrad_halo_kernel<MTW, NTT, CS4>;
-  if (lds > 65536) hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  // few workgroups streaming several blocks each: pipeline their staging; a large grid
+  // already hides it with resident workgroups (and keeps the lower VGPR count)
+  const bool pipe = grid.x * grid.y * grid.z < 512 && a.blocks_per_split > 1;
+  auto k = pipe ? wgrad_halo_kernel<MTW, NTT, CS4, true> : wgrad_halo_kernel<MTW, NTT, CS4, false>;
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a, MT);
 }
 

@@ -9,7 +9,9 @@ __device__ __forceinline__ bf16x4 tr_read_h(const bf16* p) {
 
 // Each wave owns MTW m-tiles (w, w+4, ...) x all NTT n-tiles of the workgroup, so per
 // k-step it reads NTT B fragments + MTW A fragments for MTW*NTT MFMAs.
-template <int MTW, int NTT, bool CS4>
+// PIPE: software-pipelined block loop (more VGPRs; pays off for workgroups that stream many
+// blocks, not for grids that already hide the latency with many resident workgroups).
+template <int MTW, int NTT, bool CS4, bool PIPE>
 __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT, const int bx, const int by,
                                                 const int bz, char* smem) {
   const int R = a.R, s = a.stride, Cs = a.Cs_in;
@@ -70,96 +72,199 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   const int blk1 = min(nblocks, blk0 + a.blocks_per_split);
   const int cw = CS4 ? 4 : 8;
   const int cpp = Cs / cw;
-  const FastDiv fcpp(cpp), fwin(W_in), fcpr(NTT * 2), fwo(a.Wo);
+  const int cpr = NTT * 2;
+  const int nch_x = R_in * W_in * cpp;              // X-halo chunks per block
+  const int nch_y = npb32 * cpr;                    // dY chunks per block
+  const FastDiv fcpp(cpp), fwin(W_in), fcpr(cpr), fwo(a.Wo);
+  const bool dbg_stage = !(a.dbg & 1);
 
-  for (int blk = blk0; blk < blk1; ++blk) {
-    const int b = blk / nrb;
-    const int oy0 = (blk - b * nrb) * R;
-    const int rows = min(R, a.Ho - oy0);
-    const int npix = rows * a.Wo;
-    if (blk != blk0) __syncthreads();   // previous block's readers are done
-    const bool dbg_stage = !(a.dbg & 1);
-    if (dbg_stage) {   // X halo
-      const int nch = R_in * W_in * cpp;
+  // MFMA reduction over the staged block's npix pixels
+  auto mma_block = [&](const int npix) {
+      const int nks = (a.dbg & 2) ? 0 : (npix + 31) >> 5;
+      for (int ks = 0; ks < nks; ++ks) {
+        // per-lane pixel rows of the two transposed reads (h = 0, 1)
+        const int P0 = ks * 32 + 8 * g + (i >> 2);
+        const int q0 = min(P0, npix - 1), q1 = min(P0 + 4, npix - 1);
+        const int y0 = fwo.div(q0), y1 = fwo.div(q1);
+        const int off0 = ((y0 * s) * W_in + (q0 - y0 * a.Wo) * s) * Cs;
+        const int off1 = ((y1 * s) * W_in + (q1 - y1 * a.Wo) * s) * Cs;
+        const bf16* pbrow = dyl + (size_t)P0 * ldb + 4 * (i & 3);
+        bf16x8 bfr[NTT], afr[MTW];
+  #pragma unroll
+        for (int v = 0; v < NTT; ++v) {
+          const bf16* pb = pbrow + v * 16;
+          bfr[v] = __builtin_shufflevector(tr_read_h(pb), tr_read_h(pb + 4 * ldb), 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+  #pragma unroll
+        for (int u = 0; u < MTW; ++u) {
+          const bf16* pa0 = ko[u] >= 0 ? xl + off0 + ko[u] : zl;
+          const bf16* pa1 = ko[u] >= 0 ? xl + off1 + ko[u] : zl;
+          afr[u] = tbias[u] ? ones : __builtin_shufflevector(tr_read_h(pa0), tr_read_h(pa1), 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+  #pragma unroll
+        for (int u = 0; u < MTW; ++u)
+          if (tval[u]) {
+  #pragma unroll
+            for (int v = 0; v < NTT; ++v) acc[u][v] = mfma16(afr[u], bfr[v], acc[u][v]);
+          }
+      }
+  };
+
+  // Software pipeline over the workgroup's blocks (when one block's staging fits WH_PX + WH_PY
+  // chunks per thread): block blk+1's X-halo and dY chunks are loaded into registers while
+  // block blk's MFMAs run, and go to LDS after the barrier that retires blk's readers --
+  // the staging loads' latency, not the MFMAs, was the per-block cost.
+  constexpr int WH_PX = 4, WH_PY = 4;
+  if (PIPE && dbg_stage && nch_x <= WH_PX * 256 && nch_y <= WH_PY * 256) {
+    uint4 xr[WH_PX], yr[WH_PY];
+    uint2 yc[WH_PY];
+    uint32_t yp[WH_PY];
+    auto fetch = [&](const int blk) {
+      const int b = blk / nrb, oy0 = (blk - b * nrb) * R;
+      const int npix = min(R, a.Ho - oy0) * a.Wo;
       const int yb = oy0 * s - a.pad_t, xb0 = -a.pad_l;
       const bf16* xbase = a.x + (size_t)b * a.H * a.W * Cs;
-      auto coords = [&](int idx, int& c, int& iy, int& ix) -> bool {
-        const int pix = fcpp.div(idx);
-        c = (idx - pix * cpp) * cw;
+#pragma unroll
+      for (int u = 0; u < WH_PX; ++u) {
+        const int idx = min(tid + u * 256, nch_x - 1);
+        const int pix = fcpp.div(idx), c = (idx - pix * cpp) * cw;
         const int r = fwin.div(pix);
-        iy = yb + r;
-        ix = xb0 + (pix - r * W_in);
-        return iy >= 0 && ix >= 0 && iy < a.H && ix < a.W;
-      };
-      if (CS4) {
-        staged_copy<8, bf16x4>(
-            nch, tid, 256,
-            [&](int idx) {
-              int c, iy, ix;
-              const bool ok = coords(idx, c, iy, ix);
-              return load_bf16x4_if(ok, xbase + ((size_t)iy * a.W + ix) * 4, xbase);
-            },
-            [&](int idx, const bf16x4& v) { *reinterpret_cast<bf16x4*>(xl + (size_t)idx * 4) = v; });
-      } else {
-        staged_copy<8, bf16x8>(
-            nch, tid, 256,
-            [&](int idx) {
-              int c, iy, ix;
-              const bool ok = coords(idx, c, iy, ix);
-              return load_bf16x8_if(ok, xbase + ((size_t)iy * a.W + ix) * Cs + c, xbase);
-            },
-            [&](int idx, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + (size_t)idx * 8) = v; });
-      }
-    }
-    if (dbg_stage) {   // dY rows (rebuilt from pooled dP + codes when the conv is pooled)
-      const int cpr = NTT * 2;
-      const int nch = npb32 * cpr;
-      const size_t boff = (size_t)b * a.dHp * a.dWp * a.Cs_dy;
-      staged_copy<8, bf16x8>(
-          nch, tid, 256,
-          [&](int idx) {
-            const int p = fcpr.div(idx);
-            const int n0 = nt0 * 16 + (idx - p * cpr) * 8;
-            const bool ok = p < npix && n0 < a.Cs_dy;
-            const int pp = ok ? p : 0;
-            const int pyl = fwo.div(pp);
-            const int oy = oy0 + pyl, ox = pp - pyl * a.Wo;
-            if (a.dy_code) return unpool_load8(a.dy + boff, a.dy_code + boff, a.dHp, a.dWp, a.Cs_dy, oy, ox, n0, ok);
-            return load_bf16x8_if(ok, a.dy + (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.Cs_dy + n0, a.dy);
-          },
-          [&](int idx, const bf16x8& v) {
-            const int p = fcpr.div(idx);
-            *reinterpret_cast<bf16x8*>(dyl + (size_t)p * ldb + (idx - p * cpr) * 8) = v;
-          });
-    }
-    __syncthreads();
-    const int nks = (a.dbg & 2) ? 0 : (npix + 31) >> 5;
-    for (int ks = 0; ks < nks; ++ks) {
-      // per-lane pixel rows of the two transposed reads (h = 0, 1)
-      const int P0 = ks * 32 + 8 * g + (i >> 2);
-      const int q0 = min(P0, npix - 1), q1 = min(P0 + 4, npix - 1);
-      const int y0 = fwo.div(q0), y1 = fwo.div(q1);
-      const int off0 = ((y0 * s) * W_in + (q0 - y0 * a.Wo) * s) * Cs;
-      const int off1 = ((y1 * s) * W_in + (q1 - y1 * a.Wo) * s) * Cs;
-      const bf16* pbrow = dyl + (size_t)P0 * ldb + 4 * (i & 3);
-      bf16x8 bfr[NTT], afr[MTW];
-#pragma unroll
-      for (int v = 0; v < NTT; ++v) {
-        const bf16* pb = pbrow + v * 16;
-        bfr[v] = __builtin_shufflevector(tr_read_h(pb), tr_read_h(pb + 4 * ldb), 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int u = 0; u < MTW; ++u) {
-        const bf16* pa0 = ko[u] >= 0 ? xl + off0 + ko[u] : zl;
-        const bf16* pa1 = ko[u] >= 0 ? xl + off1 + ko[u] : zl;
-        afr[u] = tbias[u] ? ones : __builtin_shufflevector(tr_read_h(pa0), tr_read_h(pa1), 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int u = 0; u < MTW; ++u)
-        if (tval[u]) {
-#pragma unroll
-          for (int v = 0; v < NTT; ++v) acc[u][v] = mfma16(afr[u], bfr[v], acc[u][v]);
+        const int iy = yb + r, ix = xb0 + (pix - r * W_in);
+        const bool ok = iy >= 0 && ix >= 0 && iy < a.H && ix < a.W;
+        const bf16* src = ok ? xbase + ((size_t)iy * a.W + ix) * Cs + c : xbase;
+        if (CS4) {
+          const uint2 v = *reinterpret_cast<const uint2*>(src);
+          xr[u] = uint4{ok ? v.x : 0u, ok ? v.y : 0u, 0u, 0u};
+        } else {
+          const uint4 v = *reinterpret_cast<const uint4*>(src);
+          xr[u] = ok ? v : uint4{0u, 0u, 0u, 0u};
         }
+      }
+      const size_t boff = (size_t)b * a.dHp * a.dWp * a.Cs_dy;
+#pragma unroll
+      for (int u = 0; u < WH_PY; ++u) {
+        const int idx = min(tid + u * 256, nch_y - 1);
+        const int p = fcpr.div(idx);
+        const int n0 = nt0 * 16 + (idx - p * cpr) * 8;
+        bool ok = p < npix && n0 < a.Cs_dy;
+        const int pp = ok ? p : 0;
+        const int pyl = fwo.div(pp);
+        const int oy = oy0 + pyl, ox = pp - pyl * a.Wo;
+        size_t o;
+        if (a.dy_code) {   // pooled: dP + argmax code of the window (unpool on commit)
+          const int wy = oy >> 1, wx = ox >> 1;
+          ok = ok && wy < a.dHp && wx < a.dWp;
+          o = ok ? boff + ((size_t)wy * a.dWp + wx) * a.Cs_dy + n0 : 0;
+          yc[u] = *reinterpret_cast<const uint2*>(a.dy_code + o);
+          yp[u] = ok ? (uint32_t)(((oy & 1) << 1) | (ox & 1)) : 0xFFu;
+        } else {
+          o = ok ? (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.Cs_dy + n0 : 0;
+          yc[u] = uint2{0u, 0u};
+          yp[u] = ok ? 0u : 0xFFu;
+        }
+        yr[u] = *reinterpret_cast<const uint4*>(a.dy + o);
+      }
+    };
+    auto commit = [&]() {
+#pragma unroll
+      for (int u = 0; u < WH_PX; ++u) {
+        const int idx = tid + u * 256;
+        if (idx >= nch_x) continue;
+        if (CS4) reinterpret_cast<uint2*>(xl)[idx] = uint2{xr[u].x, xr[u].y};
+        else reinterpret_cast<uint4*>(xl)[idx] = xr[u];
+      }
+#pragma unroll
+      for (int u = 0; u < WH_PY; ++u) {
+        const int idx = tid + u * 256;
+        if (idx >= nch_y) continue;
+        uint4 v = yr[u];
+        const uint32_t pos = yp[u];
+        if (a.dy_code) {   // keep element j iff its argmax code is this pixel's window position
+          uint32_t m[4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t w = h ? yc[u].y : yc[u].x;
+            m[2 * h] = (((w & 0xFF) == pos) ? 0x0000FFFFu : 0u) | ((((w >> 8) & 0xFF) == pos) ? 0xFFFF0000u : 0u);
+            m[2 * h + 1] =
+                ((((w >> 16) & 0xFF) == pos) ? 0x0000FFFFu : 0u) | ((((w >> 24) & 0xFF) == pos) ? 0xFFFF0000u : 0u);
+          }
+          v = uint4{v.x & m[0], v.y & m[1], v.z & m[2], v.w & m[3]};
+        } else if (pos) {
+          v = uint4{0u, 0u, 0u, 0u};
+        }
+        const int p = fcpr.div(idx);
+        *reinterpret_cast<uint4*>(dyl + (size_t)p * ldb + (idx - p * cpr) * 8) = v;
+      }
+    };
+    fetch(blk0);
+    for (int blk = blk0; blk < blk1; ++blk) {
+      const int b = blk / nrb, oy0 = (blk - b * nrb) * R;
+      const int npix = min(R, a.Ho - oy0) * a.Wo;
+      if (blk != blk0) __syncthreads();   // previous block's readers are done
+      commit();
+      __syncthreads();
+      fetch(min(blk + 1, blk1 - 1));      // next block's loads fly during this block's MFMAs
+      mma_block(npix);
+    }
+  } else {
+    for (int blk = blk0; blk < blk1; ++blk) {
+      const int b = blk / nrb;
+      const int oy0 = (blk - b * nrb) * R;
+      const int rows = min(R, a.Ho - oy0);
+      const int npix = rows * a.Wo;
+      if (blk != blk0) __syncthreads();   // previous block's readers are done
+      if (dbg_stage) {   // X halo
+        const int yb = oy0 * s - a.pad_t, xb0 = -a.pad_l;
+        const bf16* xbase = a.x + (size_t)b * a.H * a.W * Cs;
+        auto coords = [&](int idx, int& c, int& iy, int& ix) -> bool {
+          const int pix = fcpp.div(idx);
+          c = (idx - pix * cpp) * cw;
+          const int r = fwin.div(pix);
+          iy = yb + r;
+          ix = xb0 + (pix - r * W_in);
+          return iy >= 0 && ix >= 0 && iy < a.H && ix < a.W;
+        };
+        if (CS4) {
+          staged_copy<8, bf16x4>(
+              nch_x, tid, 256,
+              [&](int idx) {
+                int c, iy, ix;
+                const bool ok = coords(idx, c, iy, ix);
+                return load_bf16x4_if(ok, xbase + ((size_t)iy * a.W + ix) * 4, xbase);
+              },
+              [&](int idx, const bf16x4& v) { *reinterpret_cast<bf16x4*>(xl + (size_t)idx * 4) = v; });
+        } else {
+          staged_copy<8, bf16x8>(
+              nch_x, tid, 256,
+              [&](int idx) {
+                int c, iy, ix;
+                const bool ok = coords(idx, c, iy, ix);
+                return load_bf16x8_if(ok, xbase + ((size_t)iy * a.W + ix) * Cs + c, xbase);
+              },
+              [&](int idx, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + (size_t)idx * 8) = v; });
+        }
+      }
+      if (dbg_stage) {   // dY rows (rebuilt from pooled dP + codes when the conv is pooled)
+        const size_t boff = (size_t)b * a.dHp * a.dWp * a.Cs_dy;
+        staged_copy<8, bf16x8>(
+            nch_y, tid, 256,
+            [&](int idx) {
+              const int p = fcpr.div(idx);
+              const int n0 = nt0 * 16 + (idx - p * cpr) * 8;
+              const bool ok = p < npix && n0 < a.Cs_dy;
+              const int pp = ok ? p : 0;
+              const int pyl = fwo.div(pp);
+              const int oy = oy0 + pyl, ox = pp - pyl * a.Wo;
+              if (a.dy_code) return unpool_load8(a.dy + boff, a.dy_code + boff, a.dHp, a.dWp, a.Cs_dy, oy, ox, n0, ok);
+              return load_bf16x8_if(ok, a.dy + (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.Cs_dy + n0, a.dy);
+            },
+            [&](int idx, const bf16x8& v) {
+              const int p = fcpr.div(idx);
+              *reinterpret_cast<bf16x8*>(dyl + (size_t)p * ldb + (idx - p * cpr) * 8) = v;
+            });
+      }
+      __syncthreads();
+      mma_block(npix);
     }
   }
 
