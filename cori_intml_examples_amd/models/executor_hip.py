@@ -975,9 +975,25 @@ class BatchPlan:
         mt_cap = (8 if NTT == 8 else 16) - (1 if bias else 0)
         MT = max(1, min(a.Ktiles, mt_cap))
         MT = cdiv(a.Ktiles, cdiv(a.Ktiles, MT))        # balance the m-groups
-        # rows per block: ~128 pixels (4 k-steps), bounded LDS
+        # rows per block: ~256 pixels, at most 8 rows (measured best at batch 128 for the
+        # RPV and MNIST stacks), bounded LDS
         W_in = (g.Wo - 1) * g.stride + g.KW
-        R = max(1, min(g.Ho, 128 // max(1, g.Wo)))
+        pxs = os.environ.get("INTML_WGRAD_BLOCK_PX", "256").split(",")
+        px = int(pxs[min(g.i, len(pxs) - 1)])
+        R = max(1, min(g.Ho, px // max(1, g.Wo), int(os.environ.get("INTML_WGRAD_MAX_ROWS", "8"))))
+        # prefer the largest R whose block staging fits the kernel's register pipeline
+        # (<= 4 X-halo and 4 dY chunks per thread, wgrad_halo_body.h WH_PX / WH_PY)
+        cpp = g.Cs_in // (4 if g.Cs_in == 4 else 8)
+
+        def fits(r):
+            w_in = (g.Wo - 1) * g.stride + g.KW
+            nch_x = ((r - 1) * g.stride + g.KH) * w_in * cpp
+            nch_y = cdiv(r * g.Wo, 32) * 32 * NTT * 2
+            return nch_x <= 1024 and nch_y <= 1024
+        for r in range(R, 0, -1):
+            if fits(r):
+                R = r
+                break
         while R > 1 and (((R - 1) * g.stride + g.KH) * W_in * g.Cs_in * 2 > 64 * 1024):
             R -= 1
         a.R = R
