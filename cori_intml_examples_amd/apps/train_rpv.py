@@ -22,8 +22,10 @@ import sys
 
 
 def build_parser():
-    p = argparse.ArgumentParser(description="Distributed RPV classifier training")
-    p.add_argument("--input-dir", default=os.environ.get("RPV_DATA_DIR", "/global/cscratch1/sd/sfarrell/atlas-rpv-images"))
+    p = argparse.ArgumentParser(description="RPV calorimeter-image CNN: data-parallel training on MI355X "
+                                            "(one rank per GPU), prints the HPO figure of merit")
+    # no site-specific default: $RPV_DATA_DIR, else ./data/atlas-rpv-images (synthetic if absent)
+    p.add_argument("--input-dir", default=os.environ.get("RPV_DATA_DIR", os.path.join("data", "atlas-rpv-images")))
     p.add_argument("--n-train", type=int, default=64000)
     p.add_argument("--n-valid", type=int, default=32000)
     p.add_argument("--n-test", type=int, default=0)
@@ -55,9 +57,10 @@ def main(argv=None):
     from ..utils import set_random_seed
     from .rpv import build_model, load_dataset, train_model
 
-    print("Distributed RPV classifier training")
-    hvd.init(shard_data=args.shard)
-    print("MPI rank %i, local rank %i, host %s" % (hvd.rank(), hvd.local_rank(), socket.gethostname()))
+    st = hvd.init(shard_data=args.shard)
+    print("[train_rpv] rank %d/%d (local %d) on %s, data plane %s" % (
+        hvd.rank(), hvd.size(), hvd.local_rank(), socket.gethostname(),
+        "rccl" if st.comm is not None else st.backend))
     if args.seed is not None:
         set_random_seed(args.seed + hvd.rank())
 
@@ -80,7 +83,7 @@ def main(argv=None):
     if hvd.rank() == 0:
         model.summary()
 
-    print("Begin training")
+    print("[train_rpv] %d epochs, batch %d per rank, lr %g" % (args.n_epochs, args.batch_size, lr))
     history = train_model(model, train_input=train_input, train_labels=train_labels, valid_input=valid_input,
                           valid_labels=valid_labels, batch_size=args.batch_size, n_epochs=args.n_epochs,
                           verbose=args.verbose, use_horovod=True)

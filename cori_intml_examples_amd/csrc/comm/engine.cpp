@@ -27,6 +27,7 @@
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -92,24 +93,28 @@ class Comm {
   int device() const { return device_; }
 
   void all_reduce(uintptr_t send, uintptr_t recv, size_t count, int dtype, int op, uintptr_t stream) {
+    std::shared_lock<std::shared_timed_mutex> use(comm_mu_);   // abort cannot free comm_ meanwhile
     check();
     call(ncclAllReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
                        dtype_of(dtype), op_of(op), comm_, S(stream)), "ncclAllReduce");
   }
 
   void broadcast(uintptr_t send, uintptr_t recv, size_t count, int dtype, int root, uintptr_t stream) {
+    std::shared_lock<std::shared_timed_mutex> use(comm_mu_);
     check();
     call(ncclBroadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
                        dtype_of(dtype), root, comm_, S(stream)), "ncclBroadcast");
   }
 
   void reduce_scatter(uintptr_t send, uintptr_t recv, size_t recvcount, int dtype, int op, uintptr_t stream) {
+    std::shared_lock<std::shared_timed_mutex> use(comm_mu_);
     check();
     call(ncclReduceScatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), recvcount,
                            dtype_of(dtype), op_of(op), comm_, S(stream)), "ncclReduceScatter");
   }
 
   void all_gather(uintptr_t send, uintptr_t recv, size_t sendcount, int dtype, uintptr_t stream) {
+    std::shared_lock<std::shared_timed_mutex> use(comm_mu_);
     check();
     call(ncclAllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), sendcount,
                        dtype_of(dtype), comm_, S(stream)), "ncclAllGather");
@@ -209,6 +214,12 @@ class Comm {
       std::lock_guard<std::mutex> g(err_mu_);
       error_ = why;
     }
+    // exclusive: no enqueue or async-error query is between its check() and its RCCL call.
+    // A caller BLOCKED inside RCCL (e.g. connecting to a dead peer) holds the shared lock
+    // indefinitely; after a bounded wait abort anyway -- unblocking such a call from another
+    // thread is what ncclCommAbort is for, and failed_ already stops any new use.
+    std::unique_lock<std::shared_timed_mutex> own(comm_mu_, std::defer_lock);
+    own.try_lock_for(std::chrono::seconds(2));
     if (comm_ != nullptr && !aborted_.exchange(true)) ncclCommAbort(comm_);
   }
 
@@ -232,8 +243,13 @@ class Comm {
         }
       }
       ncclResult_t async = ncclSuccess;
-      if (!aborted_.load() && ncclCommGetAsyncError(comm_, &async) == ncclSuccess &&
-          async != ncclSuccess && async != ncclInProgress) {
+      bool async_failed = false;
+      {
+        std::shared_lock<std::shared_timed_mutex> use(comm_mu_);
+        async_failed = !aborted_.load() && ncclCommGetAsyncError(comm_, &async) == ncclSuccess &&
+                       async != ncclSuccess && async != ncclInProgress;
+      }
+      if (async_failed) {
         lk.unlock();
         fail(std::string("async error: ") + ncclGetErrorString(async));
         lk.lock();
@@ -252,6 +268,9 @@ class Comm {
   }
 
   ncclComm_t comm_ = nullptr;
+  // shared by every user of comm_ (collective enqueues, the async-error poll); exclusive in
+  // fail() around ncclCommAbort, so the communicator is never used after it is freed
+  std::shared_timed_mutex comm_mu_;
   int nranks_, rank_, device_;
   std::atomic<bool> failed_{false}, aborted_{false};
   mutable std::mutex err_mu_;

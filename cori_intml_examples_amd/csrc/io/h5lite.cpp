@@ -17,6 +17,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -99,8 +100,9 @@ std::vector<std::string> split_path(const std::string& p) {
 // Read string attribute/dataset contents (fixed or variable length, scalar or 1-D).
 py::object read_strings(hid_t obj, hid_t ftype, hid_t space, bool is_attr) {
   const int nd = H5Sget_simple_extent_ndims(space);
-  hsize_t dims[8] = {1};
-  if (nd > 0) H5Sget_simple_extent_dims(space, dims, nullptr);
+  if (nd < 0) throw std::runtime_error("h5lite: cannot read the dataspace rank of a string object");
+  std::vector<hsize_t> dims(std::max(nd, 1), 1);
+  if (nd > 0) H5Sget_simple_extent_dims(space, dims.data(), nullptr);
   size_t count = 1;
   for (int i = 0; i < nd; ++i) count *= dims[i];
   std::vector<std::string> vals;

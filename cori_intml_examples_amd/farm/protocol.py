@@ -26,9 +26,38 @@ from typing import Any, Dict
 import cloudpickle
 
 
+class InsecurePathError(PermissionError):
+    """A runtime directory / connection file another user could have planted or modified."""
+
+
+def _check_private(path: str, want_dir: bool) -> None:
+    """Refuse ``path`` unless it is a real (non-symlink) file/directory owned by this user
+    with no group/other permission bits: the connection file carries the authkey and the
+    socket address whose payloads are unpickled."""
+    st = os.lstat(path)
+    import stat as _stat
+    kind_ok = _stat.S_ISDIR(st.st_mode) if want_dir else _stat.S_ISREG(st.st_mode)
+    if not kind_ok:
+        raise InsecurePathError("%s is not a regular %s (symlink?)" % (path, "directory" if want_dir else "file"))
+    if st.st_uid != os.getuid():
+        raise InsecurePathError("%s is owned by uid %d, not %d" % (path, st.st_uid, os.getuid()))
+    if st.st_mode & 0o077:
+        raise InsecurePathError("%s has mode %o: group/other access is not allowed" % (path, st.st_mode & 0o777))
+
+
 def runtime_dir() -> str:
-    d = os.environ.get("INTML_FARM_DIR") or os.path.join(tempfile.gettempdir(), "intml-farm-%d" % os.getuid())
+    """Per-user private directory for connection files and sockets: ``$INTML_FARM_DIR``,
+    else ``$XDG_RUNTIME_DIR/intml-farm``, else ``/tmp/intml-farm-<uid>``; checked to be
+    ours and private (a pre-created world-writable dir is refused)."""
+    d = os.environ.get("INTML_FARM_DIR")
+    if not d:
+        xdg = os.environ.get("XDG_RUNTIME_DIR")
+        if xdg and os.path.isdir(xdg):
+            d = os.path.join(xdg, "intml-farm")
+        else:
+            d = os.path.join(tempfile.gettempdir(), "intml-farm-%d" % os.getuid())
     os.makedirs(d, mode=0o700, exist_ok=True)
+    _check_private(d, want_dir=True)
     return d
 
 
@@ -55,6 +84,7 @@ def write_connection_file(info: Dict[str, Any]) -> str:
 
 def read_connection_file(cluster_id: str = None, path: str = None) -> Dict[str, Any]:
     path = path or connection_file(cluster_id)
+    _check_private(path, want_dir=False)
     with open(path) as f:
         return json.load(f)
 

@@ -35,6 +35,37 @@ def parse_fom(text: str) -> Optional[float]:
     return float(m[-1]) if m else None
 
 
+def run_group(cmd: Sequence[str], env=None, timeout: Optional[float] = None, cwd=None,
+              grace: float = 10.0):
+    """Run ``cmd`` in its OWN session / process group; returns (stdout, stderr, rc).
+
+    On timeout the whole group gets SIGTERM, then SIGKILL after ``grace`` seconds: a
+    ``torch.distributed.run`` launcher cannot forward a SIGKILL to its worker ranks, which
+    would otherwise stay alive holding the slot's GPUs, RCCL communicators and port."""
+    import signal
+    p = subprocess.Popen(cmd, env=env, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+        return out, err, p.returncode
+    except subprocess.TimeoutExpired:
+        pgid = p.pid           # start_new_session: the child leads its own group
+
+        def _kill(sig):
+            try:
+                os.killpg(pgid, sig)
+            except ProcessLookupError:
+                pass
+        _kill(signal.SIGTERM)
+        try:
+            out, _ = p.communicate(timeout=grace)    # EOF only once every group member is gone
+        except subprocess.TimeoutExpired:
+            _kill(signal.SIGKILL)
+            out, _ = p.communicate()
+        _kill(signal.SIGKILL)      # a straggler that closed its pipes but ignored SIGTERM
+        return out or "", "timeout after %ss" % timeout, -9
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -123,13 +154,7 @@ class Evaluator:
             tmp = tempfile.mkdtemp(prefix="intml-eval-") if self.per_eval > 1 else None
             cmd = self.command_for(args, slot, tmp)
             t0 = time.time()
-            try:
-                r = subprocess.run(cmd, env=self._env_for(slot), capture_output=True, text=True,
-                                   timeout=self.timeout, cwd=self.cwd)
-                out, err, rc = r.stdout, r.stderr, r.returncode
-            except subprocess.TimeoutExpired as e:
-                out = e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
-                err, rc = "timeout after %ss" % self.timeout, -9
+            out, err, rc = run_group(cmd, env=self._env_for(slot), timeout=self.timeout, cwd=self.cwd)
             if tmp is not None:
                 import shutil
                 out = self._rank_output(tmp, 0) + out

@@ -165,6 +165,12 @@ class RefExecutor(Executor):
             loss, dz, corr = self._head_loss(z, y)
             self._backward(dz / bs, a_head, saved)
             if self.reducer is not None:
+                if not getattr(self, "_buckets_configured", False):
+                    # same bucketing as the GPU executor: per-layer flat ranges in backward
+                    # order (last layer first), merged up to the reducer's bucket size
+                    ranges = sorted(self.store.layer_ranges().values(), key=lambda r: -r[0])
+                    self.reducer.configure(ranges)
+                    self._buckets_configured = True
                 self.reducer.reduce_all(self.store.grad)
             self._apply_update()
         self._accumulate(loss, corr, bs)

@@ -39,10 +39,14 @@ def main(out_dir):
     hvd.broadcast_model_state(m, 0)
     w0 = [w.copy() for w in m.get_weights()]
 
-    # one DP step: rank r trains on its own half of a 32-sample batch
-    x, y, _ = synthetic_rpv(32, size=16, seed=5)
-    xs, ys = x[r * 16:(r + 1) * 16], y[r * 16:(r + 1) * 16]
+    # one DP step: rank r trains on its own 8-sample slice of an 8*n-sample batch
+    per = 8
+    x, y, _ = synthetic_rpv(per * n, size=16, seed=5)
+    xs, ys = x[r * per:(r + 1) * per], y[r * per:(r + 1) * per]
     m.train_on_batch(xs, ys)
+    red = m._executor.reducer
+    rep["buckets"] = [list(b) for b in red.buckets]
+    rep["numel"] = m.store.numel
     w1 = np.concatenate([w.reshape(-1) for w in m.get_weights()])
     rep["w1_digest"] = [float(w1.sum()), float(np.abs(w1).sum())]
     if r == 0:

@@ -20,32 +20,45 @@ def _free_port():
     return p
 
 
-def _torchrun(nproc, args, timeout=300):
+def _torchrun(nproc, args, timeout=300, extra_env=None):
     env = dict(os.environ)
-    env.update({"INTML_DEVICE": "cpu", "PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2"})
+    env.update({"INTML_DEVICE": "cpu", "PYTHONPATH": ROOT, "OMP_NUM_THREADS": "1" if nproc > 2 else "2"})
+    env.update(extra_env or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
     return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
 
 
-def test_dp_invariants(tmp_path):
-    r = _torchrun(2, [os.path.join(ROOT, "tests", "dp_worker.py"), str(tmp_path)])
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_dp_invariants(tmp_path, n):
+    """n gloo ranks (the driver runs the same path with RCCL on 2/4/8 MI355X); a 256-byte
+    bucket cap splits the gradient into many backward-ordered buckets."""
+    r = _torchrun(n, [os.path.join(ROOT, "tests", "dp_worker.py"), str(tmp_path)],
+                  extra_env={"INTML_BUCKET_BYTES": "256"}, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    reps = [json.load(open(tmp_path / ("rank%d.json" % i))) for i in range(2)]
+    reps = [json.load(open(tmp_path / ("rank%d.json" % i))) for i in range(n)]
+    tri = n * (n + 1) / 2
     for rep in reps:
-        assert rep["size"] == 2
-        assert rep["allreduce_sum"] == 3.0 and rep["allreduce_avg"] == 1.5
-        assert rep["allgather"] == [0, 10]
+        assert rep["size"] == n
+        assert rep["allreduce_sum"] == tri and rep["allreduce_avg"] == tri / n
+        assert rep["allgather"] == [10 * i for i in range(n)]
         assert rep["broadcast"] == [1.0] * 4
         assert rep["broadcast_object"] == {"from": 0}
         assert rep["history_keys"] == ["acc", "loss", "lr", "val_acc", "val_loss"]
-    assert reps[1]["init_differs"] > 0            # seeds differed before the broadcast
-    assert reps[0]["w1_digest"] == reps[1]["w1_digest"]
+        # buckets: backward order (descending offsets), disjoint, covering [0, numel) exactly
+        b = rep["buckets"]
+        assert len(b) > 2
+        assert all(b[i][0] == b[i + 1][1] for i in range(len(b) - 1))
+        assert b[0][1] == rep["numel"] and b[-1][0] == 0
+        assert b == reps[0]["buckets"]
+    assert all(rep["init_differs"] > 0 for rep in reps[1:])     # seeds differed before the broadcast
+    for rep in reps[1:]:
+        assert rep["w1_digest"] == reps[0]["w1_digest"]
+        assert rep["wf_digest"] == reps[0]["wf_digest"]
+        # MetricAverageCallback: every rank reports the same (averaged) epoch metrics
+        assert rep["val_loss"] == reps[0]["val_loss"]
+        assert rep["loss"] == reps[0]["loss"]
     assert reps[0]["dp_vs_single_maxdiff"] < 1e-5
-    assert reps[0]["wf_digest"] == reps[1]["wf_digest"]
-    # MetricAverageCallback: every rank reports the same (averaged) epoch metrics
-    assert reps[0]["val_loss"] == reps[1]["val_loss"]
-    assert reps[0]["loss"] == reps[1]["loss"]
 
 
 def test_train_rpv_cli_two_ranks(tmp_path):
@@ -62,5 +75,5 @@ def test_train_rpv_cli_two_ranks(tmp_path):
         outs.append(open(found[0]).read())
     foms = [[l for l in o.splitlines() if l.startswith("FoM:")] for o in outs]
     assert len(foms[0]) == 1 and foms[0] == foms[1]     # weights + averaged metrics agree
-    assert "MPI rank 0" in outs[0] and "MPI rank 1" in outs[1]
+    assert "rank 0/2" in outs[0] and "rank 1/2" in outs[1]
     assert "Total params" in outs[0] and "Total params" not in outs[1]   # rank-0 summary only

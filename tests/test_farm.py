@@ -187,3 +187,28 @@ def test_ipcluster_arg_parsing():
     assert a["num_engines"] == 4 and a["modules"] == ["numpy", "json"] and a["name"] == "mycluster"
     d = magics.parse_ipcluster_args("")
     assert d["name"] == "ipyparallel" and d["num_nodes"] == 1 and d["queue"] == "interactive"
+
+
+def test_runtime_dir_rejects_foreign_permissions(tmp_path, monkeypatch):
+    """A pre-created group/world-accessible runtime dir (another local user could plant a
+    connection file there) and a world-readable connection file are refused."""
+    from cori_intml_examples_amd.farm import protocol as P
+    d = tmp_path / "farm"
+    d.mkdir()
+    os.chmod(d, 0o777)
+    monkeypatch.setenv("INTML_FARM_DIR", str(d))
+    with pytest.raises(P.InsecurePathError):
+        P.runtime_dir()
+    os.chmod(d, 0o700)
+    assert P.runtime_dir() == str(d)
+    link = tmp_path / "link"
+    link.symlink_to(d)
+    monkeypatch.setenv("INTML_FARM_DIR", str(link))
+    with pytest.raises(P.InsecurePathError):
+        P.runtime_dir()
+    monkeypatch.setenv("INTML_FARM_DIR", str(d))
+    path = P.write_connection_file(P.new_connection_info("sec"))
+    assert P.read_connection_file("sec")["cluster_id"] == "sec"
+    os.chmod(path, 0o644)
+    with pytest.raises(P.InsecurePathError):
+        P.read_connection_file("sec")

@@ -148,3 +148,33 @@ def test_random_search_on_farm():
             assert (rs.runtime_seconds(ars) > 0).all()
     finally:
         cl.stop()
+
+
+def test_evaluator_timeout_kills_whole_process_group(tmp_path):
+    """A timed-out evaluation takes its children with it (a torchrun launcher cannot
+    forward SIGKILL to its ranks): no grandchild survives the timeout."""
+    import signal
+    import time
+    from cori_intml_examples_amd.hpo.evaluator import run_group
+    pidfile = tmp_path / "child.pid"
+    script = ("import subprocess, sys, time\n"
+              "p = subprocess.Popen([sys.executable, '-c', 'import signal, time; "
+              "signal.signal(signal.SIGTERM, signal.SIG_IGN); time.sleep(600)'])\n"
+              "open(%r, 'w').write(str(p.pid))\n"
+              "time.sleep(600)\n" % str(pidfile))
+    t0 = time.time()
+    out, err, rc = run_group([sys.executable, "-c", script], timeout=3, grace=1.0)
+    assert rc == -9 and "timeout" in err and time.time() - t0 < 30
+    pid = int(pidfile.read_text())
+    for _ in range(50):            # the SIGKILLed grandchild is reaped by init shortly
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            break
+        with open("/proc/%d/stat" % pid) as f:
+            if f.read().split()[2] == "Z":
+                break
+        time.sleep(0.1)
+    else:
+        os.kill(pid, signal.SIGKILL)
+        raise AssertionError("grandchild %d survived the evaluation timeout" % pid)
