@@ -9,20 +9,159 @@ batch 128 per rank (DistTrain_rpv.ipynb:267-285), 64x64x3 input.
 
 Each timed step is a FULL training step: device-side batch gather from the resident
 (synthetic) dataset by the epoch permutation, forward, loss, backward, bucketed RCCL
-gradient all-reduce (N > 1), Adam update + weight re-pack.  Weak scaling: per-GPU batch
-fixed.  Launch: ``python bench.py`` (1 GPU) or
+gradient all-reduce (N > 1) with each bucket's Adam update behind it, weight re-pack.
+Weak scaling: per-GPU batch fixed.  Launch: ``python bench.py`` (1 GPU) or
 ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
+
+Self-check at N > 1 (the multi-GPU path is never run by the builder; the run proves
+itself): the line reports the rank count the RCCL communicator reports, the gradient
+bucket sizes, per-rank step-time p50/max, a cross-rank checksum of the trained weights
+and the exposed communication time (the same step without DP, same N, timed right after);
+the process exits with status 3 if the checksums differ or RCCL saw the wrong rank count.
+
+``--via-fit`` times what users run instead: ``apps.rpv.train_model(...)`` epochs
+(Keras fit loop, Horovod callbacks, optional ``--lr-warmup-epochs``), training images only.
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
 import time
 
-BASELINE_IMG_PER_S = 1240.0   # BASELINE.md: RPV single-GPU reference, Train_rpv.ipynb:304-312
+BASELINE_LEGACY_IMG_PER_S = 1240.0   # BASELINE.md: RPV legacy CNN (34.5M params), 1 GPU, Train_rpv.ipynb:304-312
 BASELINE_MNIST_IMG_PER_S = 43600.0   # BASELINE.md: MNIST DP aggregate, 8 Haswell nodes, DistTrain_mnist.ipynb:341-357
+
+
+@contextlib.contextmanager
+def _quiet_stdout():
+    """fit() banners / callback prints go to stderr: stdout carries ONE JSON line."""
+    old = sys.stdout
+    sys.stdout = sys.stderr
+    try:
+        yield
+    finally:
+        sys.stdout = old
+
+
+def build(args, size, dp, dev):
+    from cori_intml_examples_amd.apps import zoo
+    if args.model == "rpv":
+        model = zoo.rpv_cnn((64, 64, args.channels), conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.2,
+                            optimizer="Adam", lr=0.001 * size, use_horovod=dp, device=dev)
+        shape, ncls = (64, 64, args.channels), 1
+        cfg = "RPV CNN conv[16,32,64] fc[128] 64x64x%d (DistTrain_rpv)" % args.channels
+        # no reference throughput exists for this 547,841-param model (BASELINE.md: the
+        # DistTrain_rpv training cell's timing was not saved) -> vs_baseline null
+        metric, baseline = "images/sec (whole node) RPV CNN training", None
+    elif args.model == "mnist":
+        model = zoo.mnist_cnn(32, 64, 128, 0.25, 0.5, lr=1.0 * size, use_horovod=dp, device=dev)
+        shape, ncls = (28, 28, 1), 10
+        cfg = "MNIST CNN 32-64-128 (DistTrain_mnist)"
+        metric, baseline = "images/sec (whole node) MNIST CNN training", BASELINE_MNIST_IMG_PER_S
+    else:
+        model = zoo.rpv_legacy_cnn((64, 64, args.channels), device=dev, use_horovod=dp)
+        shape, ncls = (64, 64, args.channels), 1
+        cfg = "RPV legacy CNN 34.5M (Train_rpv)"
+        metric, baseline = "images/sec (whole node) RPV legacy CNN training", BASELINE_LEGACY_IMG_PER_S
+    return model, shape, ncls, cfg, metric, baseline
+
+
+def synthetic(n, shape, ncls, ex, dev, g):
+    import torch
+    from cori_intml_examples_amd.models.executor_base import DeviceData
+    x = torch.rand((n,) + shape, generator=g, device=dev)
+    xs = torch.zeros(n, shape[0], shape[1], ex.in_Cs, dtype=torch.bfloat16, device=dev)
+    xs[..., :shape[2]] = x.to(torch.bfloat16)
+    del x
+    if ncls == 1:
+        y = (torch.rand(n, 1, generator=g, device=dev) > 0.5).float()
+    else:
+        y = torch.nn.functional.one_hot(torch.randint(0, ncls, (n,), generator=g, device=dev), ncls).float()
+    return DeviceData(xs.reshape(n, -1), y, n)
+
+
+def time_steps(model, data, B, steps, warmup, chunk, g, dev):
+    """Warmup (captures every graph the timed loop replays), then time `steps` full training
+    steps as graph replays of `chunk` steps.  Returns (elapsed seconds on this rank, per-step
+    ms of each replay from HIP events)."""
+    import torch
+    from cori_intml_examples_amd.parallel import hvd
+    ex = model._executor
+    n = data.n
+    state = {"pos": 0, "perm": torch.randperm(n, device=dev, generator=g)}
+
+    def run(k):
+        if state["pos"] + k * B > n:
+            state["pos"] = 0
+            state["perm"] = torch.randperm(n, device=dev, generator=g)
+        ex.train_steps(data, state["perm"], state["pos"], B, k)
+        state["pos"] += k * B
+
+    def chunks(total):
+        return [chunk] * (total // chunk) + ([total % chunk] if total % chunk else [])
+
+    ex.reset_metrics()
+    timed = chunks(steps)
+    for k in chunks(warmup) + sorted(set(timed)):
+        run(k)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(timed) + 1)]
+    hvd.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs[0].record()
+    for i, k in enumerate(timed):
+        run(k)
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    hvd.barrier()
+    t1 = time.perf_counter()
+    per_step = [evs[i].elapsed_time(evs[i + 1]) / k for i, k in enumerate(timed)]
+    return t1 - t0, per_step
+
+
+def weight_checksum(model):
+    import torch
+    m = model.store.master[:model.store.numel].double()
+    return [float(m.sum()), float(m.abs().sum()), float((m * m).sum())]
+
+
+def run_fit(args, model, shape, ncls, size, dp):
+    """Time `apps.rpv.train_model` epochs (the recipe path: Keras fit loop + Horovod
+    callbacks); the first epoch (graph capture) is untimed."""
+    import numpy as np
+    import torch
+    from cori_intml_examples_amd.apps.rpv import train_model
+    from cori_intml_examples_amd.train import callbacks as cbks
+    rs = np.random.RandomState(1234)
+    n = max(args.samples // 2, args.batch * 8) // args.batch * args.batch
+    x = rs.rand(n, *shape).astype(np.float32)
+    y = (rs.rand(n) > 0.5).astype(np.float32) if ncls == 1 else rs.randint(0, ncls, n)
+    marks = []
+
+    class EpochClock(cbks.Callback):
+        needs_batch_logs = False
+
+        def on_epoch_begin(self, epoch, logs=None):
+            torch.cuda.synchronize()
+            marks.append([time.perf_counter(), None])
+
+        def on_epoch_end(self, epoch, logs=None):
+            torch.cuda.synchronize()       # (the loop already synced reading the epoch metrics)
+            marks[-1][1] = time.perf_counter()
+
+    epochs = max(2, args.fit_epochs)
+    with _quiet_stdout():
+        train_model(model, x, y, None, None, batch_size=args.batch, n_epochs=epochs,
+                    lr_warmup_epochs=args.lr_warmup_epochs, use_horovod=dp, verbose=0,
+                    callbacks=[EpochClock()])
+    per_rank = n // size if (dp and size > 1) else n      # fit() shards the data set per rank
+    timed = marks[1:]
+    elapsed = sum(b - a for a, b in timed)
+    steps = len(timed) * (per_rank // args.batch)
+    return elapsed, steps, [(b - a) / (per_rank // args.batch) * 1e3 for a, b in timed]
 
 
 def main():
@@ -37,17 +176,19 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--steps-per-graph", type=int, default=int(os.environ.get("INTML_STEPS_PER_GRAPH", 8)),
                     help="full training steps per HIP-graph replay (the fit() loop's default)")
+    ap.add_argument("--no-dp-delta", action="store_true",
+                    help="skip the DP-off re-run that measures the exposed communication time")
+    ap.add_argument("--via-fit", action="store_true", help="time apps.rpv.train_model epochs (Keras fit path)")
+    ap.add_argument("--fit-epochs", type=int, default=4)
+    ap.add_argument("--lr-warmup-epochs", type=int, default=0)
     args = ap.parse_args()
     if args.no_graphs:
         os.environ["INTML_GRAPHS"] = "0"
 
     import torch
     from cori_intml_examples_amd.parallel import hvd
-    from cori_intml_examples_amd.apps import zoo
-    from cori_intml_examples_amd.models.executor_base import DeviceData
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    hvd.init()
+    st = hvd.init()
     rank, size = hvd.rank(), hvd.size()
     local = hvd.local_rank()
     torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
@@ -57,84 +198,79 @@ def main():
     B = args.batch
     # INTML_DP_FORCE=1 runs the full data-parallel step (RCCL all-reduces in the graph) at N=1
     dp = size > 1 or os.environ.get("INTML_DP_FORCE", "0") not in ("0", "")
-    if args.model == "rpv":
-        model = zoo.rpv_cnn((64, 64, args.channels), conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.2,
-                            optimizer="Adam", lr=0.001 * size, use_horovod=dp, device=dev)
-        shape, ncls = (64, 64, args.channels), 1
-        cfg_name = "RPV CNN conv[16,32,64] fc[128] 64x64x%d (DistTrain_rpv)" % args.channels
-        metric, baseline = "images/sec (whole node) RPV CNN training", BASELINE_IMG_PER_S
-    elif args.model == "mnist":
-        model = zoo.mnist_cnn(32, 64, 128, 0.25, 0.5, lr=1.0 * size, use_horovod=dp, device=dev)
-        shape, ncls = (28, 28, 1), 10
-        cfg_name = "MNIST CNN 32-64-128 (DistTrain_mnist)"
-        metric, baseline = "images/sec (whole node) MNIST CNN training", BASELINE_MNIST_IMG_PER_S
-    else:
-        model = zoo.rpv_legacy_cnn((64, 64, args.channels), device=dev, use_horovod=dp)
-        shape, ncls = (64, 64, args.channels), 1
-        cfg_name = "RPV legacy CNN 34.5M (Train_rpv)"
-        metric, baseline = "images/sec (whole node) RPV legacy CNN training", BASELINE_IMG_PER_S
-
+    model, shape, ncls, cfg_name, metric, baseline = build(args, size, dp, dev)
     ex = model._executor
-    # synthetic, device-resident dataset (no network / files here)
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    n = max(args.samples, B * 4)
-    x = torch.rand((n,) + shape, generator=g, device=dev)
-    xs = torch.zeros(n, shape[0], shape[1], ex.in_Cs, dtype=torch.bfloat16, device=dev)
-    xs[..., :shape[2]] = x.to(torch.bfloat16)
-    del x
-    if ncls == 1:
-        y = (torch.rand(n, 1, generator=g, device=dev) > 0.5).float()
-    else:
-        y = torch.nn.functional.one_hot(torch.randint(0, ncls, (n,), generator=g, device=dev), ncls).float()
-    data = DeviceData(xs.reshape(n, -1), y, n)
-    hvd.broadcast_global_variables(0, model=model)
-
-    state = {"pos": 0, "perm": torch.randperm(n, device=dev, generator=g)}
     chunk = max(1, args.steps_per_graph)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
 
-    def run(k):
-        """k full training steps; a run of steps is one HIP-graph replay (the step's
-        bookkeeping is device-resident), re-shuffling when the epoch is exhausted."""
-        if state["pos"] + k * B > n:
-            state["pos"] = 0
-            state["perm"] = torch.randperm(n, device=dev, generator=g)
-        ex.train_steps(data, state["perm"], state["pos"], B, k)
-        state["pos"] += k * B
+    if args.via_fit:
+        elapsed, steps, per_step = run_fit(args, model, shape, ncls, size, dp)
+        warmup_note = "1 epoch (untimed)"
+    else:
+        data = synthetic(max(args.samples, B * 4), shape, ncls, ex, dev, g)
+        hvd.broadcast_global_variables(0, model=model)
+        elapsed, per_step = time_steps(model, data, B, args.steps, args.warmup, chunk, g, dev)
+        steps = args.steps
+        warmup_note = args.warmup
+    loss = ex.read_metrics()[0]
 
-    def chunks(total):
-        return [chunk] * (total // chunk) + ([total % chunk] if total % chunk else [])
-
-    ex.reset_metrics()
-    timed = chunks(args.steps)
-    for k in chunks(args.warmup) + sorted(set(timed)):   # every timed graph is captured here
-        run(k)
-    hvd.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in timed:
-        run(k)
-    torch.cuda.synchronize()
-    hvd.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    # ---------------------------------------------------------------- self-check (DP)
+    selfcheck, ok = None, True
+    stats = {"p50": sorted(per_step)[len(per_step) // 2], "max": max(per_step)}
     if size > 1:
         elapsed = max(hvd.allgather(elapsed))   # MAX over ranks
-    loss, acc, cnt = ex.read_metrics()
-    ms = elapsed / args.steps * 1e3
-    value = size * B * args.steps / elapsed
+        steps = min(hvd.allgather(steps))
+    if dp:
+        comm = st.comm
+        red = ex.reducer
+        sums = hvd.allgather(weight_checksum(model)) if size > 1 else [weight_checksum(model)]
+        rstats = hvd.allgather(stats) if size > 1 else [stats]
+        selfcheck = {
+            "data_plane": "rccl-native" if comm is not None else ("torch-" + str(st.backend)),
+            "rccl_nranks": comm.nranks if comm is not None else None,
+            "world_size": size,
+            "bucket_bytes": [4 * (hi - lo) for lo, hi in red.buckets] if red is not None else None,
+            "weights_identical": all(s == sums[0] for s in sums),
+            "weight_checksum": sums[0],
+            "step_ms_p50_per_rank": [round(r["p50"], 4) for r in rstats],
+            "step_ms_max_per_rank": [round(r["max"], 4) for r in rstats],
+        }
+        ok = selfcheck["weights_identical"] and (comm is None or selfcheck["rccl_nranks"] == size)
+        if not args.no_dp_delta and not args.via_fit:
+            # the same step without the data-parallel machinery, same N, right after
+            ref, *_ = build(args, size, False, dev)
+            data2 = synthetic(max(args.samples, B * 4), shape, ncls, ref._executor, dev, g)
+            e2, _ = time_steps(ref, data2, B, args.steps, args.warmup, chunk, g, dev)
+            if size > 1:
+                e2 = max(hvd.allgather(e2))
+            selfcheck["nodp_ms_per_step"] = round(e2 / args.steps * 1e3, 4)
+            selfcheck["exposed_comm_us_per_step"] = round((elapsed - e2) / args.steps * 1e6, 2)
+
+    ms = elapsed / steps * 1e3
+    value = size * B * steps / elapsed
     if rank == 0:
         out = {"metric": metric,
-               "value": round(value, 1), "unit": "images/s", "n_gpus": size, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": round(value / baseline, 2),
+               "value": round(value, 1), "unit": "images/s", "n_gpus": size, "steps": steps,
+               "warmup": warmup_note, "ms_per_step": round(ms, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": round(value / baseline, 2) if baseline else None,
                "dtype": "bf16", "data": "synthetic (device-resident, random-init weights)",
                "config": {"model": cfg_name, "global_batch": B * size, "per_gpu_batch": B,
                           "seq_len": None, "input": list(shape),
                           "optimizer": type(getattr(model.optimizer, "_base_optimizer", model.optimizer)).__name__,
                           "parallelism": "dp%d" % size, "steps_per_graph": chunk,
+                          "path": "fit" if args.via_fit else "train_steps",
+                          "step_ms_p50": round(stats["p50"], 4), "step_ms_max": round(stats["max"], 4),
                           "train_loss": round(loss, 5)}}
+        if args.via_fit:
+            out["data"] = "synthetic (host numpy uploaded by fit(), random-init weights)"
+            out["config"]["lr_warmup_epochs"] = args.lr_warmup_epochs
+        if selfcheck is not None:
+            out["selfcheck"] = selfcheck
         print(json.dumps(out), flush=True)
     hvd.shutdown()
+    if not ok:
+        print("bench self-check FAILED: %s" % json.dumps(selfcheck), file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -88,6 +88,22 @@ class Comm {
     }
   }
 
+  // what the RCCL communicator itself reports (not what we asked for)
+  int comm_count() {
+    std::shared_lock<std::shared_timed_mutex> use(comm_mu_);
+    check();
+    int n = -1;
+    call(ncclCommCount(comm_, &n), "ncclCommCount");
+    return n;
+  }
+  int comm_rank() {
+    std::shared_lock<std::shared_timed_mutex> use(comm_mu_);
+    check();
+    int r = -1;
+    call(ncclCommUserRank(comm_, &r), "ncclCommUserRank");
+    return r;
+  }
+
   int rank() const { return rank_; }
   int size() const { return nranks_; }
   int device() const { return device_; }
@@ -308,6 +324,8 @@ PYBIND11_MODULE(_comm, m) {
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("size", &Comm::size)
       .def_property_readonly("device", &Comm::device)
+      .def("comm_count", &Comm::comm_count)
+      .def("comm_rank", &Comm::comm_rank)
       .def("all_reduce", &Comm::all_reduce, py::arg("send"), py::arg("recv"), py::arg("count"),
            py::arg("dtype"), py::arg("op"), py::arg("stream"))
       .def("broadcast", &Comm::broadcast, py::arg("send"), py::arg("recv"), py::arg("count"),

@@ -217,6 +217,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("STEP_STATE_METRICS_OFFSET") = (int)offsetof(StepState, metrics);
   m.attr("STEP_STATE_MSCHED_OFFSET") = (int)offsetof(StepState, m_schedule);
   m.attr("STEP_STATE_LR_OFFSET") = (int)offsetof(StepState, lr);
+  m.attr("STEP_STATE_WARM_OFFSET") = (int)offsetof(StepState, warm_t0);
   m.attr("STEP_STATE_DATA_OFFSET") = (int)offsetof(StepState, data_x);
   m.attr("STEP_STATE_DATAN_OFFSET") = (int)offsetof(StepState, data_n);
 

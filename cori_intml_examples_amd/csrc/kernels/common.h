@@ -156,6 +156,13 @@ struct StepState {
   // "the optimizer updated the master since the weight packs were last written"
   int packs_stale;
   int pad_;
+  // device-side LR warmup (Goyal et al. gradual warmup, the Horovod warmup callback's
+  // schedule): for 0-based step g = t - warm_t0 - 1 < warm_steps the base LR is
+  //   warm_base / size * ((g + 1) / warm_spe * (size - 1) / warm_epochs + 1)
+  // instead of the host-written `lr` -- so warmup needs no per-batch host write and runs
+  // inside multi-step graph replays.  warm_steps = 0: off.
+  int warm_t0, warm_steps, warm_spe, warm_size;
+  float warm_base, warm_epochs;
 };
 
 enum OptKind { OPT_SGD = 0, OPT_RMSPROP = 1, OPT_ADADELTA = 2, OPT_ADAM = 3, OPT_NADAM = 4 };

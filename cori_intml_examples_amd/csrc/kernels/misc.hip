@@ -20,7 +20,13 @@ __device__ void step_bookkeeping(const StepBeginArgs& a) {
   if (!a.training) return;
   st->t += 1;
   const double t = (double)st->t;
-  const double lr = (double)st->lr / (1.0 + (double)a.decay * (t - 1.0));
+  double base = (double)st->lr;
+  const int g = st->t - st->warm_t0 - 1;
+  if (g >= 0 && g < st->warm_steps) {
+    const double n = (double)st->warm_size;
+    base = (double)st->warm_base / n * ((double)(g + 1) / st->warm_spe * (n - 1.0) / st->warm_epochs + 1.0);
+  }
+  const double lr = base / (1.0 + (double)a.decay * (t - 1.0));
   st->lr_eff = (float)lr;
   switch (a.opt_kind) {
     case OPT_ADAM: {

@@ -34,6 +34,13 @@ def prepare_targets(y: np.ndarray, plan: Plan) -> np.ndarray:
     return np.ascontiguousarray(y)
 
 
+def warmup_lr(g: int, spe: int, size: int, epochs: float, base: float) -> float:
+    """LR of 0-based warmup step g: ramps linearly from ~base/size to base over
+    ``epochs * spe`` steps (Goyal et al. 2017 gradual warmup; the same schedule the device
+    bookkeeping computes, misc.hip step_bookkeeping)."""
+    return base / size * ((g + 1) / spe * (size - 1) / epochs + 1.0)
+
+
 class Executor:
     """Runs training / evaluation steps of a compiled Plan on one device."""
 
@@ -45,6 +52,24 @@ class Executor:
         self.optimizer = optimizer
         self.seed = int(seed) & 0xFFFFFFFF
         self.reducer = None          # data-parallel gradient reducer (parallel.dist)
+        self.lr_warmup = None        # (t0, steps, spe, size, epochs, base) device LR schedule
+
+    # learning-rate schedule ---------------------------------------------------------------
+    def set_lr_warmup(self, t0: int, steps: int, spe: int, size: int, epochs: float, base: float) -> None:
+        """Gradual LR warmup evaluated per step by the executor itself (no per-batch host
+        write): optimizer step g = iterations - t0 - 1 < steps uses
+        ``warmup_lr(g, ...)`` as its base LR (``parallel.callbacks.LearningRateWarmupCallback``)."""
+        self.lr_warmup = (int(t0), int(steps), int(spe), int(size), float(epochs), float(base)) if steps > 0 else None
+
+    def base_lr_for_step(self, t: int, host_lr: float) -> float:
+        """Base LR of optimizer iteration ``t`` (1-based), before Keras ``decay``."""
+        w = self.lr_warmup
+        if w is not None:
+            t0, steps, spe, size, epochs, base = w
+            g = t - t0 - 1
+            if 0 <= g < steps:
+                return warmup_lr(g, spe, size, epochs, base)
+        return host_lr
 
     # data ---------------------------------------------------------------------------------
     def upload(self, x: np.ndarray, y: Optional[np.ndarray]) -> DeviceData:

@@ -112,6 +112,76 @@ class DenseGeo:
     pack_bwd: int = -1
 
 
+def splice_bucket_launches(launches, inserts, per_bucket):
+    """Insert each bucket's launches into the step's launch list.
+
+    ``inserts``: (launch index after which bucket k's partial slabs are final, k);
+    ``per_bucket``: [(name pattern, factory k -> fn(stream), stream tag)] appended, in
+    order, at that point (slab reduction, then all-reduce / optimizer on the comm stream).
+    Returns (new launch list, bucket_ready[k] = index just past bucket k's launches)."""
+    out, ready, pos = [], [0] * len(inserts), 0
+    for at, k in sorted(inserts):
+        out.extend(launches[pos:at])
+        pos = at
+        for pat, make, tag in per_bucket:
+            out.append((pat % k, make(k), tag))
+        ready[k] = len(out)
+    out.extend(launches[pos:])
+    return out, ready
+
+
+def stream_program(tags, side=False, opt=False):
+    """The stream schedule of a launch sequence, as a list of ops:
+    ("run", stream, i)  launch i on "main" / "side" / "opt" / "comm";
+    ("wait", dst, src)  make stream dst wait for everything issued so far on src.
+
+    'main' launches run in order on the current stream.  'side' launches (weight gradients,
+    slab reductions) run on the side stream when there is one (else on main), each after the
+    latest main launch before it.  'comm' launches fork the comm stream after everything
+    issued so far (main and side: the bucket's slab reduction) -- RCCL and the bucket's
+    optimizer run there while main continues the backward.  'opt' launches (early per-bucket
+    optimizer) wait for all three.  Every used stream is joined back into main at the end."""
+    ops, used = [], set()
+    main_moved = True
+    for i, tag in enumerate(tags):
+        if tag == "side" and side:
+            if main_moved:
+                ops.append(("wait", "side", "main"))
+                main_moved = False
+            ops.append(("run", "side", i))
+            used.add("side")
+        elif tag == "opt":
+            if not opt:
+                continue
+            ops.append(("wait", "opt", "main"))
+            for src in ("side", "comm"):
+                if src in used:
+                    ops.append(("wait", "opt", src))
+            ops.append(("run", "opt", i))
+            used.add("opt")
+        elif tag == "comm":
+            ops.append(("wait", "comm", "main"))
+            if "side" in used:
+                ops.append(("wait", "comm", "side"))
+            ops.append(("run", "comm", i))
+            used.add("comm")
+        else:
+            ops.append(("run", "main", i))
+            main_moved = True
+    for src in ("side", "opt", "comm"):
+        if src in used:
+            ops.append(("wait", "main", src))
+    return ops
+
+
+def check_bucket_cover(spans, numel):
+    """Bucket (lo, hi) spans must tile [0, numel) exactly: disjoint, no gap, nothing left
+    out (every gradient is reduced, all-reduced and updated exactly once)."""
+    sp = sorted(spans)
+    if not sp or sp[0][0] != 0 or sp[-1][1] != numel or any(a[1] != b[0] for a, b in zip(sp, sp[1:])):
+        raise AssertionError("gradient buckets %s do not tile [0, %d)" % (spans, numel))
+
+
 class HipExecutor(Executor):
     def __init__(self, plan: Plan, store, optimizer, seed: int):
         super().__init__(plan, store, optimizer, seed)
@@ -276,6 +346,13 @@ class HipExecutor(Executor):
     def set_m_schedule(self, v: float) -> None:
         self._st_f64[self.K.STEP_STATE_MSCHED_OFFSET // 8] = float(v)
 
+    def set_lr_warmup(self, t0, steps, spe, size, epochs, base):
+        super().set_lr_warmup(t0, steps, spe, size, epochs, base)
+        w = self.lr_warmup or (0, 0, 1, 1, 1.0, 0.0)
+        o = self.K.STEP_STATE_WARM_OFFSET
+        self._st_i32[o // 4:o // 4 + 4] = torch.tensor(w[:4], dtype=torch.int32)
+        self._st_f32[o // 4 + 4:o // 4 + 6] = torch.tensor(w[4:], dtype=torch.float32)
+
     def _sync_lr(self):
         lr = float(self.opt.lr)
         if lr != self._lr_host:
@@ -425,6 +502,11 @@ class BatchPlan:
         self.comm_in_graph = (self.training and red is not None and getattr(red, "capturable", False)
                               and red.active and env_flag("INTML_COMM_CAPTURE", True))
         self.comm_stream = torch.cuda.Stream(device=dev) if self.comm_in_graph else None
+        # ... and each bucket's optimizer update follows its all-reduce on the comm stream (the
+        # 1/size average folded in), so the dense bucket's update overlaps the conv backward and
+        # only the last bucket's (small) update is on the step's tail
+        self.optim_on_comm = (self.comm_in_graph and not self.early_optim
+                              and env_flag("INTML_DP_OPTIM_ON_COMM", True))
         z = lambda *s, dt=BF16: torch.zeros(*s, dtype=dt, device=dev)
         self.xb = z(bs, ex.in_H * ex.in_W * ex.in_Cs)
         self.yb = z(bs, ex.plan.head.N, dt=torch.float32)
@@ -1098,19 +1180,28 @@ class BatchPlan:
             hi = max(self.red_groups[i][1] for i in bg)
             self.bucket_tables.append((lo, hi, tab))
             inserts.append((max(self.red_ready[i] for i in bg), k))
-        launches, self.bucket_ready = [], [0] * len(bucket_groups)
-        pos = 0
-        for at, k in sorted(inserts):
-            launches.extend(self.launches[pos:at])
-            pos = at
-            launches.append(("reduce_b%d" % k, lambda s, k=k: self._launch_bucket_reduce(k, s), "side"))
-            if self.comm_in_graph:
-                launches.append(("allreduce_b%d" % k, lambda s, k=k: reducer.launch(k, ex.store.grad, s), "comm"))
-            self.bucket_ready[k] = len(launches)
-        launches.extend(self.launches[pos:])
-        self.launches = launches
+        extra = []
+        if self.comm_in_graph:
+            extra.append(("allreduce_b%d", lambda k: (lambda s: reducer.launch(k, ex.store.grad, s)), "comm"))
+            if self.optim_on_comm:
+                extra.append(("optim_b%d", lambda k: (lambda s: self._launch_optim_comm(k, s)), "comm"))
+        self.launches, self.bucket_ready = splice_bucket_launches(
+            self.launches, inserts,
+            [("reduce_b%d", lambda k: (lambda s: self._launch_bucket_reduce(k, s)), "side")] + extra)
+        check_bucket_cover([(lo, hi) for lo, hi, _ in self.bucket_tables], ex.store.numel)
         if self.early_optim:
             self._insert_optim()
+
+    def _launch_optim_comm(self, k, stream):
+        """Keras update of bucket k's parameters on the comm stream, right after its
+        all-reduce (re-pack deferred to the next prologue)."""
+        ex = self.ex
+        lo, hi, _ = self.bucket_tables[k]
+        a = ex._optim_args(False, defer_pack=True)   # built at capture time: grad_scale = 1/size
+        a.lo, a.n = lo, hi - lo
+        if getattr(self, "_no_packs", None) is None:
+            self._no_packs = ex.K.PackTable()
+        ex.K.optim(a, self._no_packs, stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
 
     def _insert_optim(self):
         """One ("optim_b<k>", ..., "opt") launch per bucket at the first point where the
@@ -1150,49 +1241,20 @@ class BatchPlan:
 
     # ---------------------------------------------------------------- execution
     def _run_seq(self, lo: int = 0, hi: Optional[int] = None):
-        """Launch [lo, hi): 'main' launches in order on the current stream; 'side' launches
-        (weight gradients, slab reductions) on the side stream, each after the latest main
-        launch before it -- the two chains run concurrently and join at the end."""
-        main = torch.cuda.current_stream()
-        side_used = opt_used = comm_used = False
-        main_moved = True
-        for item in self.launches[lo:hi]:
-            name, fn = item[0], item[1]
-            tag = item[2] if len(item) > 2 else "main"
-            if tag == "side" and self.side is not None:
-                if main_moved:
-                    self.side.wait_stream(main)
-                    main_moved = False
-                fn(self.side.cuda_stream)
-                side_used = True
-            elif tag == "opt":
-                if self.opt_stream is None:
-                    continue
-                self.opt_stream.wait_stream(main)
-                if side_used:
-                    self.opt_stream.wait_stream(self.side)
-                if comm_used:
-                    self.opt_stream.wait_stream(self.comm_stream)
-                fn(self.opt_stream.cuda_stream)
-                opt_used = True
-            elif tag == "comm":
-                # fork: the comm stream follows everything issued so far (the bucket's slab
-                # reduction), RCCL runs there while the main stream continues the backward
-                cs = self.comm_stream
-                cs.wait_stream(main)
-                if side_used:
-                    cs.wait_stream(self.side)
-                fn(cs)
-                comm_used = True
-            else:
-                fn(main.cuda_stream)
-                main_moved = True
-        if side_used:
-            main.wait_stream(self.side)
-        if opt_used:
-            main.wait_stream(self.opt_stream)
-        if comm_used:
-            main.wait_stream(self.comm_stream)
+        """Launch [lo, hi) on the streams ``stream_program`` assigns (concurrent chains that
+        join main at the end)."""
+        items = self.launches[lo:hi]
+        tags = [it[2] if len(it) > 2 else "main" for it in items]
+        streams = {"main": torch.cuda.current_stream(), "side": self.side, "opt": self.opt_stream,
+                   "comm": self.comm_stream}
+        for op in stream_program(tags, side=self.side is not None, opt=self.opt_stream is not None):
+            if op[0] == "wait":
+                streams[op[1]].wait_stream(streams[op[2]])
+                continue
+            _, sname, i = op
+            st = streams[sname]
+            # comm launches take the Stream (RCCL wrappers use it as a context); others the handle
+            items[i][1](st if sname == "comm" else st.cuda_stream)
 
     def _launch_bucket_reduce(self, k, s):
         lo, hi, tab = self.bucket_tables[k]
@@ -1209,7 +1271,8 @@ class BatchPlan:
 
     def _body(self, with_optim: bool):
         self._run_seq()
-        if self.training and with_optim and not self.early_optim and not self.optim_fused:
+        if (self.training and with_optim and not self.early_optim and not self.optim_fused
+                and not self.optim_on_comm):
             self._launch_optim()
 
     def _dp_segments(self):

@@ -131,8 +131,9 @@ class RefExecutor(Executor):
         base = getattr(opt, "_base_optimizer", opt)
         base.iterations += 1
         t = base.iterations
-        lr = base.current_lr() if base.initial_decay == 0 else float(base.lr) / (
-            1.0 + base.initial_decay * (t - 1))
+        lr = self.base_lr_for_step(t, float(base.lr))
+        if base.initial_decay != 0:
+            lr = lr / (1.0 + base.initial_decay * (t - 1))
         n = self.store.numel
         p, g = self.store.master[:n], self.store.grad[:n]
         k = base.kind

@@ -45,6 +45,12 @@ class MetricAverageCallback(Callback):
 
 
 class LearningRateScheduleCallback(Callback):
+    """Generic per-epoch (staircase) or per-batch LR multiplier schedule, host-driven.
+
+    Same constructor and semantics as ``horovod.keras.callbacks.LearningRateScheduleCallback``
+    (Apache-2.0, Uber Technologies; API shape and behaviour followed for drop-in use, not
+    its code).  A non-staircase schedule writes the LR every batch and so forces the fit
+    loop to one step per graph replay; the warmup below avoids that."""
     needs_batch_logs = False
 
     def __init__(self, multiplier, start_epoch=0, end_epoch=None, staircase=True,
@@ -89,27 +95,59 @@ class LearningRateScheduleCallback(Callback):
             logs["lr"] = float(get_value(self.model.optimizer.lr))
 
 
-class LearningRateWarmupCallback(LearningRateScheduleCallback):
-    """Goyal et al. gradual warmup: lr/size -> lr over ``warmup_epochs`` (``rpv.py:89-92``).
-    With warmup_epochs=0 (the reference default) it is a no-op."""
+class LearningRateWarmupCallback(Callback):
+    """Gradual LR warmup from ``lr / size`` to ``lr`` over ``warmup_epochs`` (Goyal et al.
+    2017; the schedule ``rpv.py:89-92`` requests through Horovod's callback of this name).
+
+    The ramp is evaluated BY THE EXECUTOR for every optimizer step (device step bookkeeping
+    on the GPU, ``misc.hip:step_bookkeeping``): this callback only registers it at train
+    begin, so it neither writes the LR per batch nor forces the fit loop to one step per
+    graph replay.  Step g (0-based from the first batch of epoch 0) uses
+    ``lr * (1/size) * ((g + 1) / steps_per_epoch * (size - 1) / warmup_epochs + 1)``;
+    ``optimizer.lr`` is kept at the value of the epoch's last step for the epoch logs and
+    for later callbacks (ReduceLROnPlateau sees it, as with Horovod).  ``warmup_epochs=0``
+    (the reference default) is a no-op."""
+    needs_batch_logs = False
 
     def __init__(self, warmup_epochs=5, momentum_correction=True, steps_per_epoch=None, verbose=0):
-        def multiplier(epoch):
-            epoch += 1.0 / self.steps_per_epoch
-            return 1.0 / dist.size() * (epoch * (dist.size() - 1) / warmup_epochs + 1)
-        super().__init__(multiplier, start_epoch=0, end_epoch=warmup_epochs, staircase=False,
-                         momentum_correction=momentum_correction, steps_per_epoch=steps_per_epoch)
-        self.verbose = verbose
+        super().__init__()
         self.warmup_epochs = warmup_epochs
+        self.steps_per_epoch = steps_per_epoch
+        self.verbose = verbose
+        self.initial_lr = None
 
-    def on_batch_begin(self, batch, logs=None):
+    def _spe(self):
+        if self.steps_per_epoch:
+            return int(self.steps_per_epoch)
+        if self.params.get("steps"):
+            return int(self.params["steps"])
+        if self.params.get("samples") and self.params.get("batch_size"):
+            return -(-int(self.params["samples"]) // int(self.params["batch_size"]))
+        raise ValueError("LearningRateWarmupCallback: steps per epoch unknown (pass steps_per_epoch)")
+
+    def on_train_begin(self, logs=None):
         if self.warmup_epochs <= 0:
             return
-        super().on_batch_begin(batch, logs)
+        self.initial_lr = float(get_value(self.model.optimizer.lr))
+        self._n = self._spe()
+        ex = self.model._executor
+        base = getattr(self.model.optimizer, "_base_optimizer", self.model.optimizer)
+        # steps of this fit() run count from its first batch
+        ex.set_lr_warmup(int(base.iterations), int(round(self.warmup_epochs * self._n)), self._n, dist.size(),
+                         float(self.warmup_epochs), self.initial_lr)
 
     def on_epoch_end(self, epoch, logs=None):
-        if self.warmup_epochs > 0:
-            super().on_epoch_end(epoch, logs)
-            if epoch == self.end_epoch - 1 and self.verbose > 0:
-                print("\nEpoch %d: finished gradual learning rate warmup to %g." %
-                      (epoch + 1, float(get_value(self.model.optimizer.lr))))
+        if self.warmup_epochs <= 0 or self.initial_lr is None or epoch >= self.warmup_epochs:
+            return
+        from ..models.executor_base import warmup_lr
+        g = min((epoch + 1) * self._n, int(round(self.warmup_epochs * self._n))) - 1
+        lr = warmup_lr(g, self._n, dist.size(), float(self.warmup_epochs), self.initial_lr)
+        set_value(self.model.optimizer.lr, lr)
+        if logs is not None:
+            logs["lr"] = lr
+        if epoch == self.warmup_epochs - 1 and self.verbose > 0:
+            print("\nEpoch %d: gradual learning rate warmup to %g done." % (epoch + 1, lr))
+
+    def on_train_end(self, logs=None):
+        if self.warmup_epochs > 0 and self.model is not None and self.model._executor is not None:
+            self.model._executor.set_lr_warmup(0, 0, 1, 1, 1.0, 0.0)

@@ -83,6 +83,15 @@ class NativeComm:
             self.all_reduce(t)
             torch.cuda.current_stream(device).synchronize()
 
+    @property
+    def nranks(self) -> int:
+        """Rank count as reported by the RCCL communicator (ncclCommCount)."""
+        return self._c.comm_count()
+
+    @property
+    def comm_rank(self) -> int:
+        return self._c.comm_rank()
+
     # ------------------------------------------------------------------ collectives
     @staticmethod
     def _stream(stream) -> int:

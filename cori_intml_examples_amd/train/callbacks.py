@@ -84,7 +84,9 @@ class CallbackList:
 
     @property
     def batch_begin_needed(self) -> bool:
-        return any(type(c).on_batch_begin is not Callback.on_batch_begin for c in self.callbacks)
+        # overridden in the class, or set on the instance (LambdaCallback(on_batch_begin=...))
+        return any(type(c).on_batch_begin is not Callback.on_batch_begin or "on_batch_begin" in vars(c)
+                   for c in self.callbacks)
 
 
 class History(Callback):
@@ -228,7 +230,11 @@ class ModelCheckpoint(Callback):
 
 class ReduceLROnPlateau(Callback):
     """Keras defaults: monitor val_loss, factor 0.1, min_delta 1e-4, cooldown 0, min_lr 0;
-    writes ``lr`` into the epoch logs (``rpv.py:94-98``)."""
+    writes ``lr`` into the epoch logs (``rpv.py:94-98``).
+
+    Attribution: the decision logic follows Keras 2.2's ``ReduceLROnPlateau``
+    (keras/callbacks.py, MIT license, (c) François Chollet and contributors) step for step,
+    so that the reference's LR trajectories are reproduced exactly."""
     needs_batch_logs = False
 
     def __init__(self, monitor="val_loss", factor=0.1, patience=10, verbose=0, mode="auto",
@@ -282,6 +288,8 @@ class ReduceLROnPlateau(Callback):
 
 
 class EarlyStopping(Callback):
+    """Keras 2.2 ``EarlyStopping`` semantics (keras/callbacks.py, MIT license, (c) François
+    Chollet and contributors; logic followed step for step for bit-identical stopping)."""
     needs_batch_logs = False
 
     def __init__(self, monitor="val_loss", min_delta=0, patience=0, verbose=0, mode="auto",

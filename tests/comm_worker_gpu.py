@@ -32,6 +32,7 @@ def main(out):
     rep["backend"] = st.backend
     rep["native"] = st.comm is not None
     comm = st.comm
+    rep["rccl_nranks"] = comm.nranks
     dev = torch.device("cuda", 0)
     # primitives (size 1: sum/avg are the identity; gather/scatter are copies)
     t = torch.arange(1000, dtype=torch.float32, device=dev)

@@ -57,7 +57,9 @@ def test_native_comm_engine_gpu(tmp_path):
     assert rep["allreduce_tensor"] == pytest.approx(12.0)
     cap, seg = rep["train"]["captured"], rep["train"]["segmented"]
     assert cap["reducer"] == "NativeGradReducer" and cap["comm_in_graph"]
-    assert cap["n_comm_launches"] == len(cap["buckets"]) == 2
+    # per bucket: the all-reduce and the bucket's optimizer update, both on the comm stream
+    assert cap["n_comm_launches"] == 2 * len(cap["buckets"]) == 4
+    assert rep["rccl_nranks"] == 1
     # size-1 all-reduce is exact: both DP modes agree bit for bit; against the single-GPU
     # step (whose optimizer is fused into the gradient reduction) only fp contraction differs
     assert rep["train"]["captured_vs_segmented"] == 0.0, rep["train"]
@@ -65,3 +67,21 @@ def test_native_comm_engine_gpu(tmp_path):
     assert not seg["comm_in_graph"] and seg["max_abs_diff"] < 1e-4, seg
     assert rep["train"]["bf16_wire"]["rel_diff"] < 0.05, rep["train"]["bf16_wire"]
     assert rep["abort_raises"] and rep["healthy"], rep
+
+
+@pytest.mark.gpu
+def test_native_comm_in_process_gpu():
+    """The RCCL engine loaded in THIS process (so the loaded-.so audit sees _comm): a size-1
+    communicator reports its rank count, all-reduces in place and closes cleanly."""
+    import torch
+    from cori_intml_examples_amd.parallel import comm as C
+    dev = torch.device("cuda", 0)
+    c = C.NativeComm(0, 1, dev, timeout_s=60.0)
+    try:
+        assert c.nranks == 1 and c.comm_rank == 0
+        t = torch.arange(4096, dtype=torch.float32, device=dev)
+        c.all_reduce(t)
+        torch.cuda.synchronize()
+        assert torch.equal(t, torch.arange(4096, dtype=torch.float32, device=dev))
+    finally:
+        c.close()

@@ -123,22 +123,44 @@ def test_history_lr_and_callbacks_order():
     assert len(h2.epoch) == 2
 
 
-def test_lr_warmup_callback_ramps():
+def test_lr_warmup_callback_matches_per_batch_schedule():
+    """The device/executor-evaluated warmup gives exactly the weights of writing
+    lr * (1/size) * ((g+1)/spe * (size-1)/W + 1) into the optimizer before every batch
+    (the Horovod callback's per-batch behaviour), and keeps fit() on multi-step replays."""
     from cori_intml_examples_amd.parallel import callbacks as hcb
     from cori_intml_examples_amd.parallel import dist
+    from cori_intml_examples_amd.models.executor_base import warmup_lr
 
     x, y, _ = synthetic_rpv(64, size=16, seed=1)
-    m = zoo.rpv_cnn((16, 16, 1), [4, 4, 4], [8], optimizer="Adam", lr=0.004, device="cpu")
-    lrs = []
-    rec = cbks.LambdaCallback(on_batch_end=lambda b, logs: lrs.append(optim.get_value(m.optimizer.lr)))
     orig = dist.size
     dist.size = lambda: 4                          # pretend 4 ranks: warmup lr/4 -> lr
     try:
-        m.fit(x, y, batch_size=16, epochs=2, verbose=0, callbacks=[hcb.LearningRateWarmupCallback(2), rec])
+        m = zoo.rpv_cnn((16, 16, 1), [4, 4, 4], [8], dropout=0.0, optimizer="SGD", lr=0.004, device="cpu")
+        w0 = m.get_weights()
+        cb = hcb.LearningRateWarmupCallback(2)
+        assert not cbks.CallbackList([cb]).batch_begin_needed
+        h = m.fit(x, y, batch_size=16, epochs=3, verbose=0, shuffle=False, callbacks=[cb])
+        wa = m.get_weights()
+
+        m2 = zoo.rpv_cnn((16, 16, 1), [4, 4, 4], [8], dropout=0.0, optimizer="SGD", lr=0.004, device="cpu")
+        m2.set_weights(w0)
+        step = {"g": 0}
+
+        def begin(b, logs):
+            g = step["g"]
+            optim.set_value(m2.optimizer.lr, warmup_lr(g, 4, 4, 2.0, 0.004) if g < 8 else 0.004)
+            step["g"] += 1
+        m2.fit(x, y, batch_size=16, epochs=3, verbose=0, shuffle=False,
+               callbacks=[cbks.LambdaCallback(on_batch_begin=begin)])
+        wb = m2.get_weights()
     finally:
         dist.size = orig
-    assert lrs[0] < lrs[3] < lrs[-1] <= 0.004 + 1e-12
-    assert lrs[0] == pytest.approx(0.004 / 4 * (0.25 * 3 / 2 + 1))
+    for a, b in zip(wa, wb):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+    # epoch logs carry the LR of the epoch's last step; after warmup the full LR
+    assert h.history["lr"][0] == pytest.approx(0.004 / 4 * (4 / 4 * 3 / 2 + 1))
+    assert h.history["lr"][1] == pytest.approx(0.004)
+    assert optim.get_value(m.optimizer.lr) == pytest.approx(0.004)
 
 
 def test_optimizer_closed_form_single_step():

@@ -289,3 +289,40 @@ def test_conv_stack_forward_matches_per_layer(kind, drop, cin, hw, monkeypatch):
         if a is not None:
             assert torch.equal(a, b)
     assert torch.equal(w1, w0)
+
+
+def test_device_lr_warmup_matches_host_schedule():
+    """The LR warmup evaluated by the device step bookkeeping (fit() keeps multi-step graph
+    replays) gives the weights of writing each step's warmup LR from the host before every
+    batch (one step per replay)."""
+    from cori_intml_examples_amd import optim
+    from cori_intml_examples_amd.models.executor_base import warmup_lr
+    from cori_intml_examples_amd.parallel import callbacks as hcb
+    from cori_intml_examples_amd.parallel import dist
+    from cori_intml_examples_amd.train import callbacks as cbks
+    orig = dist.size
+    dist.size = lambda: 4
+    try:
+        set_random_seed(9)
+        a = _build("rpv", "cuda", opt="SGD")
+        w0 = a.get_weights()
+        set_random_seed(9)
+        b = _build("rpv", "cuda", opt="SGD")
+        b.set_weights(w0)
+        x, y = _data(a, 16 * 32, seed=2)
+        a.fit(x, y, batch_size=32, epochs=3, verbose=0, shuffle=False, callbacks=[hcb.LearningRateWarmupCallback(2)])
+        lr0 = float(optim.get_value(b.optimizer.lr))
+        step = {"g": 0}
+
+        def begin(bi, logs):
+            g = step["g"]
+            optim.set_value(b.optimizer.lr, warmup_lr(g, 16, 4, 2.0, lr0) if g < 32 else lr0)
+            step["g"] += 1
+        b.fit(x, y, batch_size=32, epochs=3, verbose=0, shuffle=False,
+              callbacks=[cbks.LambdaCallback(on_batch_begin=begin)])
+    finally:
+        dist.size = orig
+    assert (32, "train") in a._executor._plans
+    assert a._executor._plans[(32, "train")].multi_graphs, "warmup must not force one step per replay"
+    for wa, wb in zip(a.get_weights(), b.get_weights()):
+        np.testing.assert_allclose(wa, wb, rtol=1e-5, atol=1e-6)
