@@ -351,7 +351,8 @@ class HipExecutor(Executor):
         w = self.lr_warmup or (0, 0, 1, 1, 1.0, 0.0)
         o = self.K.STEP_STATE_WARM_OFFSET
         self._st_i32[o // 4:o // 4 + 4] = torch.tensor(w[:4], dtype=torch.int32)
-        self._st_f32[o // 4 + 4:o // 4 + 6] = torch.tensor(w[4:], dtype=torch.float32)
+        # StepState order: warm_base, warm_epochs
+        self._st_f32[o // 4 + 4:o // 4 + 6] = torch.tensor([w[5], w[4]], dtype=torch.float32)
 
     def _sync_lr(self):
         lr = float(self.opt.lr)
