@@ -130,7 +130,7 @@ def splice_bucket_launches(launches, inserts, per_bucket):
     return out, ready
 
 
-def stream_program(tags, side=False, opt=False):
+def stream_program(tags, side=False, opt=False, comm=True):
     """The stream schedule of a launch sequence, as a list of ops:
     ("run", stream, i)  launch i on "main" / "side" / "opt" / "comm";
     ("wait", dst, src)  make stream dst wait for everything issued so far on src.
@@ -140,7 +140,8 @@ def stream_program(tags, side=False, opt=False):
     latest main launch before it.  'comm' launches fork the comm stream after everything
     issued so far (main and side: the bucket's slab reduction) -- RCCL and the bucket's
     optimizer run there while main continues the backward.  'opt' launches (early per-bucket
-    optimizer) wait for all three.  Every used stream is joined back into main at the end."""
+    optimizer) wait for all three.  Every used stream is joined back into main at the end.
+    ``comm=False``: comm launches run in order on main (a linear graph)."""
     ops, used = [], set()
     main_moved = True
     for i, tag in enumerate(tags):
@@ -159,7 +160,7 @@ def stream_program(tags, side=False, opt=False):
                     ops.append(("wait", "opt", src))
             ops.append(("run", "opt", i))
             used.add("opt")
-        elif tag == "comm":
+        elif tag == "comm" and comm:
             ops.append(("wait", "comm", "main"))
             if "side" in used:
                 ops.append(("wait", "comm", "side"))
@@ -502,7 +503,11 @@ class BatchPlan:
         red = ex.reducer
         self.comm_in_graph = (self.training and red is not None and getattr(red, "capturable", False)
                               and red.active and env_flag("INTML_COMM_CAPTURE", True))
-        self.comm_stream = torch.cuda.Stream(device=dev) if self.comm_in_graph else None
+        # INTML_COMM_FORK=0: the captured all-reduces stay on the main stream (a linear graph:
+        # no cross-queue edges, whose graph-launch cost is several us each, but no overlap)
+        # (default: fork only when there is more than one bucket to overlap; set in _build_reduce)
+        self.comm_fork = None
+        self.comm_stream = None
         # ... and each bucket's optimizer update follows its all-reduce on the comm stream (the
         # 1/size average folded in), so the dense bucket's update overlaps the conv backward and
         # only the last bucket's (small) update is on the step's tail
@@ -1183,6 +1188,10 @@ class BatchPlan:
             inserts.append((max(self.red_ready[i] for i in bg), k))
         extra = []
         if self.comm_in_graph:
+            fork = os.environ.get("INTML_COMM_FORK")
+            self.comm_fork = (fork not in ("0", "false", "False")) if fork else len(bucket_groups) > 1
+            if self.comm_fork:
+                self.comm_stream = torch.cuda.Stream(device=ex.device)
             extra.append(("allreduce_b%d", lambda k: (lambda s: reducer.launch(k, ex.store.grad, s)), "comm"))
             if self.optim_on_comm:
                 extra.append(("optim_b%d", lambda k: (lambda s: self._launch_optim_comm(k, s)), "comm"))
@@ -1248,14 +1257,15 @@ class BatchPlan:
         tags = [it[2] if len(it) > 2 else "main" for it in items]
         streams = {"main": torch.cuda.current_stream(), "side": self.side, "opt": self.opt_stream,
                    "comm": self.comm_stream}
-        for op in stream_program(tags, side=self.side is not None, opt=self.opt_stream is not None):
+        for op in stream_program(tags, side=self.side is not None, opt=self.opt_stream is not None,
+                                 comm=self.comm_stream is not None):
             if op[0] == "wait":
                 streams[op[1]].wait_stream(streams[op[2]])
                 continue
             _, sname, i = op
             st = streams[sname]
             # comm launches take the Stream (RCCL wrappers use it as a context); others the handle
-            items[i][1](st if sname == "comm" else st.cuda_stream)
+            items[i][1](st if tags[i] == "comm" else st.cuda_stream)
 
     def _launch_bucket_reduce(self, k, s):
         lo, hi, tab = self.bucket_tables[k]

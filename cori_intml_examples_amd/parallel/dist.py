@@ -47,7 +47,9 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
     env_shard = os.environ.get("INTML_DP_SHARD")
     if shard_data is None:
         shard_data = True if env_shard is None else env_shard not in ("0", "false", "False")
-    bucket_bytes = bucket_bytes or int(os.environ.get("INTML_BUCKET_BYTES", 1 << 20))
+    # None: adaptive (the native reducer sizes buckets from the model's gradient bytes)
+    env_bb = os.environ.get("INTML_BUCKET_BYTES")
+    bucket_bytes = bucket_bytes or (int(env_bb) if env_bb else None)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -262,7 +264,7 @@ def merge_buckets(groups: Sequence[Tuple[int, int]], bucket_bytes: int):
     for gi, (lo, hi) in enumerate(groups):
         cur.append(gi)
         cur_bytes += (hi - lo) * 4
-        if cur_bytes >= bucket_bytes:
+        if bucket_bytes is not None and cur_bytes >= bucket_bytes:
             buckets.append(cur)
             cur, cur_bytes = [], 0
     if cur:
@@ -296,7 +298,7 @@ class GradReducer:
 
     def configure(self, groups: Sequence[Tuple[int, int]]) -> List[List[int]]:
         """Merge backward-ordered groups into buckets; returns group indices per bucket."""
-        self.bucket_groups, self.buckets = merge_buckets(groups, self.bucket_bytes)
+        self.bucket_groups, self.buckets = merge_buckets(groups, self.bucket_bytes or (4 << 20))
         return self.bucket_groups
 
     def start(self, bucket: int, grad: torch.Tensor):
@@ -340,6 +342,20 @@ class GradReducer:
             grad[: self.store.numel].div_(self.size)
 
 
+def adaptive_bucket_bytes(groups: Sequence[Tuple[int, int]]) -> int:
+    """Bucket size for the captured RCCL data plane.  A gradient of <= 16 MB (e.g. the RPV
+    model's 2.2 MB) is ONE fused all-reduce at the end of the backward on the main stream:
+    a linear graph, because every cross-stream edge of a graph replay costs several us on
+    MI355X (measured: two forked buckets 170 us/step vs one fused 147 us at N=1) -- more than
+    the overlap can win back for a transfer of that size.  Larger gradients (the 34.5M-param
+    legacy RPV model: 138 MB) get ~4 buckets of >= 16 MB forked onto the comm stream so the
+    all-reduces overlap the rest of the backward."""
+    total = 4 * sum(hi - lo for lo, hi in groups)
+    if total <= (16 << 20):
+        return total + 1
+    return max(16 << 20, total // 4)
+
+
 class NativeGradReducer:
     """Bucketed gradient all-reduce on the native RCCL engine, CAPTURABLE: the executor
     inserts ``launch(k, ..)`` into the step's launch sequence on a comm stream forked after
@@ -358,16 +374,18 @@ class NativeGradReducer:
         self.bucket_groups: List[List[int]] = [[0]]
         self.stream = torch.cuda.Stream(device=comm.device)   # for the segmented (uncaptured) mode
         self._stage = {}
+        self._configured = False
 
     @property
     def active(self) -> bool:
         return True
 
     def configure(self, groups: Sequence[Tuple[int, int]]) -> List[List[int]]:
-        bg, spans = merge_buckets(groups, self.bucket_bytes)
-        if spans == self.buckets and (self._stage or self.compression != "bf16"):
+        bg, spans = merge_buckets(groups, self.bucket_bytes or adaptive_bucket_bytes(groups))
+        if self._configured and spans == self.buckets and bg == self.bucket_groups:
             return self.bucket_groups       # same layout (another batch size): keep the staging
         self.bucket_groups, self.buckets = bg, spans   # buffers earlier graphs reference
+        self._configured = True
         self._stage = {}
         if self.compression == "bf16":
             for k, (lo, hi) in enumerate(self.buckets):

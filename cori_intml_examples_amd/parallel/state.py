@@ -13,7 +13,7 @@ class DPState:
     local_size: int
     backend: str
     shard_data: bool = True
-    bucket_bytes: int = 4 << 20
+    bucket_bytes: Optional[int] = None   # None: adaptive (dist.adaptive_bucket_bytes)
     owns_pg: bool = False
     comm: Any = None              # parallel.comm.NativeComm (RCCL data plane) or None
 

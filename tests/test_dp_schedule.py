@@ -124,3 +124,11 @@ def test_bucket_cover():
         bg, sp = merge_buckets(GROUPS, bb)
         check_bucket_cover(sp, 547841)
         assert [s[0] for s in sp] == sorted((s[0] for s in sp), reverse=True)
+
+
+def test_linear_schedule_keeps_comm_on_main():
+    launches, _, _ = _fake_step()
+    tags = [l[2] for l in launches]
+    ops = stream_program(tags, side=False, opt=False, comm=False)
+    assert all(op[0] == "run" and op[1] == "main" for op in ops)
+    assert [launches[op[2]][0] for op in ops] == [l[0] for l in launches]
