@@ -238,3 +238,33 @@ struct RedTable {
   int pad_[2];
   RedDesc d[MAX_RED];
 };
+
+// Fused data-parallel all-reduce + optimizer over xGMI peer memory (xgmi.hip).  Every rank
+// owns chunk r = [r*chunk, (r+1)*chunk) of the flat gradient.  One launch per step:
+//   1. push: workgroup w sends its slice [w*sub, (w+1)*sub) of EVERY chunk j to owner j's
+//      inbox row r (remote stores over xGMI), then flags owner j (flag1[w][r] = seq);
+//   2. reduce: owner r waits for the P flags of its slice, sums inbox rows 0..P-1 in rank
+//      order (deterministic), pushes the sum into every rank's outbox, flags them (flag2);
+//   3. update: every rank waits for the P owners' flags and applies the optimizer to the
+//      whole reduced gradient (identical inputs -> identical weights on every rank).
+// Flags carry a per-workgroup sequence number (ctr[w] + 1), so they never need resetting.
+// Communication memory is uncached device memory shared by IPC handles; every wait is
+// bounded (spin_limit polls) and sets *err instead of hanging.
+#define XGMI_MAX_RANKS 8
+#define XGMI_MAX_WG 256
+struct XgmiArgs {
+  int rank = 0, size = 1;
+  int n = 0;                     // gradient elements (bucket [0, n))
+  int chunk = 0;                 // elements per owner chunk (multiple of 4)
+  int sub = 0;                   // elements per workgroup slice of a chunk (multiple of 4)
+  int spin_limit = 1 << 22;
+  int mode = 1;                  // 0: sum only (reduced gradient -> grad); 1: + optimizer
+  float* grad = nullptr;         // local flat gradient (read in 1, reduced sum written in 3)
+  float* inbox[XGMI_MAX_RANKS] = {};     // rank j's inbox [P][chunk] (as mapped here)
+  float* outbox[XGMI_MAX_RANKS] = {};    // rank j's outbox [P * chunk] = reduced gradient
+  unsigned* flag1[XGMI_MAX_RANKS] = {};  // rank j's phase-1 flags [XGMI_MAX_WG][P]
+  unsigned* flag2[XGMI_MAX_RANKS] = {};  // rank j's phase-2 flags [XGMI_MAX_WG][P]
+  unsigned* ctr = nullptr;       // [XGMI_MAX_WG] local sequence counters
+  int* err = nullptr;            // set to 1 + phase on a timed-out wait
+  OptimArgs opt;
+};

@@ -38,6 +38,13 @@ void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStr
 void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, hipStream_t s);
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s);
 void launch_pack(const float* master, bf16* arena, const PackTable& tab, hipStream_t s);
+int xgmi_grid(const XgmiArgs& a);
+void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s);
+uintptr_t xgmi_alloc_uncached(size_t bytes);
+void xgmi_free(uintptr_t p);
+std::string xgmi_ipc_handle(uintptr_t p);
+uintptr_t xgmi_ipc_open(const std::string& handle);
+void xgmi_ipc_close(uintptr_t p);
 
 static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -267,4 +274,36 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("optim", [](const OptimArgs& a, const PackTable& t, uintptr_t s) { launch_optim(a, t, S(s)); check_last("optim"); });
   m.def("pack", [](uintptr_t master, uintptr_t arena, const PackTable& t, uintptr_t s) {
     launch_pack(reinterpret_cast<const float*>(master), reinterpret_cast<bf16*>(arena), t, S(s)); check_last("pack"); });
+
+  // fused xGMI all-reduce + optimizer (xgmi.hip)
+  m.attr("XGMI_MAX_RANKS") = XGMI_MAX_RANKS;
+  m.attr("XGMI_MAX_WG") = XGMI_MAX_WG;
+  py::class_<XgmiArgs>(m, "XgmiArgs")
+      .def(py::init<>())
+      RW(XgmiArgs, rank) RW(XgmiArgs, size) RW(XgmiArgs, n) RW(XgmiArgs, chunk) RW(XgmiArgs, sub)
+      RW(XgmiArgs, spin_limit) RW(XgmiArgs, mode) PTR(XgmiArgs, grad) PTR(XgmiArgs, ctr) PTR(XgmiArgs, err)
+      RW(XgmiArgs, opt)
+      .def("set_peer", [](XgmiArgs& a, int j, uintptr_t inbox, uintptr_t outbox, uintptr_t f1, uintptr_t f2) {
+        if (j < 0 || j >= XGMI_MAX_RANKS) throw std::out_of_range("peer index");
+        a.inbox[j] = reinterpret_cast<float*>(inbox);
+        a.outbox[j] = reinterpret_cast<float*>(outbox);
+        a.flag1[j] = reinterpret_cast<unsigned*>(f1);
+        a.flag2[j] = reinterpret_cast<unsigned*>(f2);
+      });
+  m.def("xgmi_grid", &xgmi_grid);
+  m.def("xgmi_allreduce", [](const XgmiArgs& a, uintptr_t s) {
+    if (a.size < 1 || a.size > XGMI_MAX_RANKS || a.rank < 0 || a.rank >= a.size) throw std::invalid_argument("xgmi ranks");
+    if (a.chunk % 4 || a.sub % 4 || a.sub <= 0 || (long long)a.chunk * a.size < a.n) throw std::invalid_argument("xgmi geometry");
+    if (xgmi_grid(a) > XGMI_MAX_WG) throw std::invalid_argument("xgmi grid > XGMI_MAX_WG");
+    for (int j = 0; j < a.size; ++j)
+      if (!a.inbox[j] || !a.outbox[j] || !a.flag1[j] || !a.flag2[j]) throw std::invalid_argument("xgmi peer not set");
+    if (!a.grad || !a.ctr || !a.err || (a.mode == 1 && (!a.opt.p || !a.opt.st))) throw std::invalid_argument("xgmi null pointer");
+    launch_xgmi_allreduce(a, S(s));
+    check_last("xgmi_allreduce");
+  });
+  m.def("xgmi_alloc_uncached", &xgmi_alloc_uncached);
+  m.def("xgmi_free", &xgmi_free);
+  m.def("xgmi_ipc_handle", [](uintptr_t p) { return py::bytes(xgmi_ipc_handle(p)); });
+  m.def("xgmi_ipc_open", [](py::bytes h) { return xgmi_ipc_open(std::string(h)); });
+  m.def("xgmi_ipc_close", &xgmi_ipc_close);
 }

@@ -1,0 +1,180 @@
+// Fused data-parallel gradient all-reduce + optimizer over xGMI (SURVEY.md §5.1 item 3:
+// small-bucket P2P all-reduce; N7 comm).  Two-shot (reduce-scatter + all-gather) by direct
+// peer stores into IPC-mapped uncached device memory, with the Keras update fused into the
+// final pass -- ONE kernel on the training stream instead of an RCCL collective plus an
+// optimizer launch (a linear HIP graph: no cross-queue edges).  See XgmiArgs (args.h).
+//
+// Memory model (MI355X_MICROARCH.md "inter-workgroup visibility", cdna_hip_programming.md
+// Guideline 16, at system scope across GPUs):
+//   producer: payload stores -> every wave s_waitcnt vmcnt(0) -> workgroup barrier ->
+//             release fence (system) -> s_waitcnt vmcnt(0) -> relaxed system-scope flag store;
+//   consumer: relaxed system-scope poll (bounded) -> acquire fence (system) -> barrier -> loads.
+// The inbox/outbox/flags are uncached device memory, so neither side's L2 holds a stale copy.
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "args.h"
+#include "optim_math.h"
+
+namespace {
+
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Lanes 0..P-1 of wave 0 each raise flag `slot` of rank `lane` to seq.
+__device__ __forceinline__ void signal_all(unsigned* const* flags, int slot, int P, unsigned seq) {
+  drain_stores();
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < P) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    drain_stores();
+    __hip_atomic_store(flags[t] + slot, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Wait until local flags [base, base + P) all reach seq (lanes 0..P-1 poll one each).
+// Returns false (and sets *err) if a flag does not arrive within spin_limit polls.
+__device__ __forceinline__ bool wait_all(const unsigned* flags, int P, unsigned seq, int limit, int* err,
+                                         int phase) {
+  __shared__ int s_ok;
+  const int t = threadIdx.x;
+  if (t == 0) s_ok = 1;
+  __syncthreads();
+  if (t < P) {
+    int spins = 0;
+    while (__hip_atomic_load(flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+      if (++spins > limit) {
+        s_ok = 0;
+        __hip_atomic_store(err, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    drain_stores();
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+__device__ __forceinline__ float4 load4_guarded(const float* p, long long idx, long long n) {
+  if (idx + 4 <= n) return *reinterpret_cast<const float4*>(p + idx);
+  float4 v = {0.f, 0.f, 0.f, 0.f};
+  if (idx < n) v.x = p[idx];
+  if (idx + 1 < n) v.y = p[idx + 1];
+  if (idx + 2 < n) v.z = p[idx + 2];
+  if (idx + 3 < n) v.w = p[idx + 3];
+  return v;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
+  __shared__ unsigned s_seq;
+  const int w = blockIdx.x, t = threadIdx.x;
+  if (t == 0) s_seq = a.ctr[w] + 1u;
+  __syncthreads();
+  const unsigned seq = s_seq;
+  const int P = a.size, r = a.rank, C = a.chunk;
+  const int k0 = w * a.sub, k1 = min(k0 + a.sub, C);
+  const long long n = a.n;
+
+  // 1. push my slice of every chunk to its owner's inbox row r
+  for (int j = 0; j < P; ++j) {
+    float* dst = a.inbox[j] + (size_t)r * C;
+    const long long base = (long long)j * C;
+    for (int k = k0 + 4 * t; k < k1; k += 1024)
+      *reinterpret_cast<float4*>(dst + k) = load4_guarded(a.grad, base + k, n);
+  }
+  signal_all(a.flag1, w * P + r, P, seq);
+
+  // 2. reduce my chunk's slice over the P rows in rank order, push it to every outbox
+  bool ok = wait_all(a.flag1[r] + w * P, P, seq, a.spin_limit, a.err, 1);
+  if (ok) {
+    const float* in = a.inbox[r];
+    for (int k = k0 + 4 * t; k < k1; k += 1024) {
+      float4 s = *reinterpret_cast<const float4*>(in + k);
+      for (int q = 1; q < P; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(in + (size_t)q * C + k);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      for (int j = 0; j < P; ++j) *reinterpret_cast<float4*>(a.outbox[j] + (size_t)r * C + k) = s;
+    }
+  }
+  signal_all(a.flag2, w * P + r, P, seq);
+
+  // 3. the whole reduced gradient is in my outbox: record it and update the parameters
+  ok = wait_all(a.flag2[r] + w * P, P, seq, a.spin_limit, a.err, 2) && ok;
+  if (ok) {
+    const float* red = a.outbox[r];
+    const OptimArgs& o = a.opt;
+    for (int q = 0; q < P; ++q) {
+      for (int k = k0 + 4 * t; k < k1; k += 1024) {
+        const long long idx = (long long)q * C + k;
+        if (idx >= n) break;
+        const float4 g4 = *reinterpret_cast<const float4*>(red + idx);
+        const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+        const int m = (int)min(4LL, n - idx);
+        for (int e = 0; e < m; ++e) {
+          a.grad[idx + e] = gv[e];
+          if (a.mode == 1) {
+            float p = o.p[idx + e];
+            float s0 = o.s0 ? o.s0[idx + e] : 0.f, s1 = o.s1 ? o.s1[idx + e] : 0.f;
+            opt_update<KIND>(o, o.st, p, gv[e] * o.grad_scale, &s0, &s1);
+            o.p[idx + e] = p;
+            if (o.s0) o.s0[idx + e] = s0;
+            if (o.s1) o.s1[idx + e] = s1;
+          }
+        }
+      }
+    }
+    if (a.mode == 1 && o.defer_pack && w == 0 && t == 0) o.st->packs_stale = 1;
+  }
+  if (t == 0) a.ctr[w] = seq;
+}
+
+}  // namespace
+
+int xgmi_grid(const XgmiArgs& a) { return (a.chunk + a.sub - 1) / a.sub; }
+
+void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s) {
+  const dim3 grid(xgmi_grid(a)), block(256);
+  switch (a.mode == 1 ? a.opt.kind : -1) {
+    case OPT_ADAM: hipLaunchKernelGGL(xgmi_allreduce_kernel<OPT_ADAM>, grid, block, 0, s, a); break;
+    case OPT_NADAM: hipLaunchKernelGGL(xgmi_allreduce_kernel<OPT_NADAM>, grid, block, 0, s, a); break;
+    case OPT_ADADELTA: hipLaunchKernelGGL(xgmi_allreduce_kernel<OPT_ADADELTA>, grid, block, 0, s, a); break;
+    case OPT_RMSPROP: hipLaunchKernelGGL(xgmi_allreduce_kernel<OPT_RMSPROP>, grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL(xgmi_allreduce_kernel<OPT_SGD>, grid, block, 0, s, a); break;
+  }
+}
+
+// ---------------------------------------------------------------- host: memory + IPC
+uintptr_t xgmi_alloc_uncached(size_t bytes) {
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess || p == nullptr)
+    throw std::runtime_error("hipExtMallocWithFlags(uncached) failed");
+  if (hipMemset(p, 0, bytes) != hipSuccess) throw std::runtime_error("hipMemset failed");
+  if (hipDeviceSynchronize() != hipSuccess) throw std::runtime_error("hipDeviceSynchronize failed");
+  return reinterpret_cast<uintptr_t>(p);
+}
+
+void xgmi_free(uintptr_t p) { hipFree(reinterpret_cast<void*>(p)); }
+
+std::string xgmi_ipc_handle(uintptr_t p) {
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, reinterpret_cast<void*>(p));
+  if (e != hipSuccess) throw std::runtime_error(std::string("hipIpcGetMemHandle: ") + hipGetErrorString(e));
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+uintptr_t xgmi_ipc_open(const std::string& handle) {
+  if (handle.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("bad IPC handle size");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle.data(), sizeof(h));
+  void* p = nullptr;
+  hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) throw std::runtime_error(std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+  return reinterpret_cast<uintptr_t>(p);
+}
+
+void xgmi_ipc_close(uintptr_t p) { hipIpcCloseMemHandle(reinterpret_cast<void*>(p)); }

@@ -1187,7 +1187,14 @@ class BatchPlan:
             self.bucket_tables.append((lo, hi, tab))
             inserts.append((max(self.red_ready[i] for i in bg), k))
         extra = []
-        if self.comm_in_graph:
+        fused = self.comm_in_graph and getattr(reducer, "xgmi", None) is not None
+        if fused:
+            # xGMI all-reduce + optimizer in one kernel on the main stream (linear graph)
+            self.comm_fork, self.optim_on_comm = False, True
+            extra.append(("xgmi_allreduce_optim_b%d",
+                          lambda k: (lambda s: reducer.launch_fused(
+                              ex.store.grad, ex._optim_args(False, defer_pack=True), s)), "main"))
+        elif self.comm_in_graph:
             fork = os.environ.get("INTML_COMM_FORK")
             self.comm_fork = (fork not in ("0", "false", "False")) if fork else len(bucket_groups) > 1
             if self.comm_fork:

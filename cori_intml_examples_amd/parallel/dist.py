@@ -375,6 +375,8 @@ class NativeGradReducer:
         self.stream = torch.cuda.Stream(device=comm.device)   # for the segmented (uncaptured) mode
         self._stage = {}
         self._configured = False
+        self.xgmi = None               # parallel.xgmi.XgmiAllreduce when the fused path is on
+        self._xgmi_err_host = None
 
     @property
     def active(self) -> bool:
@@ -387,10 +389,32 @@ class NativeGradReducer:
         self.bucket_groups, self.buckets = bg, spans   # buffers earlier graphs reference
         self._configured = True
         self._stage = {}
+        self._setup_xgmi()
         if self.compression == "bf16":
             for k, (lo, hi) in enumerate(self.buckets):
                 self._stage[k] = torch.empty(hi - lo, dtype=torch.bfloat16, device=self.comm.device)
         return self.bucket_groups
+
+    def _setup_xgmi(self):
+        """ONE fused bucket, fp32 wire, N > 1 (``INTML_XGMI=1`` also at N = 1; ``=0`` off):
+        the fused xGMI all-reduce + optimizer kernel replaces RCCL + the optimizer launch,
+        if every rank's setup and self-test pass (collective; same decision on all ranks)."""
+        mode = os.environ.get("INTML_XGMI", "auto").lower()
+        want = (mode in ("1", "on", "true") or (mode == "auto" and self.size > 1))
+        ok = want and len(self.buckets) == 1 and self.buckets[0][0] == 0 and self.compression is None
+        n = self.buckets[0][1] if ok else 0
+        if self.xgmi is not None and (not ok or self.xgmi.n != n):
+            self.xgmi.close()
+            self.xgmi = None
+        if ok and self.xgmi is None:
+            from . import xgmi as X
+            self.xgmi = X.create(self.comm.rank, self.size, n, self.comm.device, allgather)
+            if self.xgmi is not None:
+                self._xgmi_err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+
+    def launch_fused(self, grad: torch.Tensor, opt_args, stream: int) -> None:
+        """The fused all-reduce + optimizer of the single bucket (capturable)."""
+        self.xgmi.launch(grad.data_ptr(), stream, opt=opt_args)
 
     def launch(self, bucket: int, grad: torch.Tensor, stream: torch.cuda.Stream) -> None:
         """Enqueue bucket ``bucket``'s all-reduce on ``stream`` (capturable)."""
@@ -417,8 +441,13 @@ class NativeGradReducer:
         torch.cuda.current_stream().wait_stream(self.stream)
 
     def after_step(self) -> None:
-        """Watchdog marker after a step (raises if a peer failed / RCCL reported an error)."""
+        """Watchdog marker after a step (raises if a peer failed / RCCL reported an error);
+        with the xGMI path, the error word of an earlier launch (async copy, no sync)."""
         self.comm.mark()
+        if self.xgmi is not None:
+            if int(self._xgmi_err_host[0]):
+                raise RuntimeError("xgmi all-reduce: a wait timed out (peer rank dead or hung)")
+            self._xgmi_err_host.copy_(self.xgmi.err, non_blocking=True)
 
     def reduce_all(self, grad: torch.Tensor, average: bool = True) -> None:
         for i in range(len(self.buckets)):

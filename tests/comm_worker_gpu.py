@@ -77,6 +77,16 @@ def main(out):
         results[name]["w"] = w
     results["captured_vs_segmented"] = float(np.abs(results["captured"].pop("w") - results["segmented"].pop("w")).max())
     os.environ["INTML_COMM_CAPTURE"] = "1"
+    # the fused xGMI all-reduce + optimizer kernel (forced on at size 1)
+    os.environ["INTML_XGMI"] = "1"
+    m = zoo.rpv_cnn((64, 64, 3), use_horovod=True, **kw)
+    m.set_weights(w0)
+    w = train(m)
+    plan = next(iter(m._executor._plans.values()))
+    results["xgmi"] = {"active": m._executor.reducer.xgmi is not None,
+                       "launches": [it[0] for it in plan.launches if "xgmi" in it[0] or "allreduce" in it[0]],
+                       "max_abs_diff": float(np.abs(w - wb).max())}
+    os.environ["INTML_XGMI"] = "0"
     opt = hvd.DistributedOptimizer("Adam", compression=hvd.Compression.fp16)
     m = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw)
     m.compile(optimizer=opt, loss="binary_crossentropy", metrics=["accuracy"])

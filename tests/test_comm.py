@@ -67,6 +67,9 @@ def test_native_comm_engine_gpu(tmp_path):
     assert cap["max_abs_diff"] < 1e-4, cap
     assert not seg["comm_in_graph"] and seg["max_abs_diff"] < 1e-4, seg
     assert rep["train"]["bf16_wire"]["rel_diff"] < 0.05, rep["train"]["bf16_wire"]
+    xg = rep["train"]["xgmi"]
+    assert xg["active"] and xg["launches"] == ["xgmi_allreduce_optim_b0"], xg
+    assert xg["max_abs_diff"] < 1e-4, xg
     assert rep["abort_raises"] and rep["healthy"], rep
 
 
@@ -86,3 +89,37 @@ def test_native_comm_in_process_gpu():
         assert torch.equal(t, torch.arange(4096, dtype=torch.float32, device=dev))
     finally:
         c.close()
+
+
+def test_xgmi_geometry():
+    from cori_intml_examples_amd.parallel.xgmi import geometry
+    for n in (1, 7, 1000, 548129, 100003, 34515201):
+        for P in (1, 2, 4, 8):
+            chunk, sub, grid = geometry(n, P)
+            assert chunk % 4 == 0 and sub % 4 == 0 and chunk * P >= n
+            assert 1 <= grid <= 256 and (grid - 1) * sub < chunk <= grid * sub
+
+
+@pytest.mark.gpu
+def test_xgmi_two_processes_one_gpu(tmp_path):
+    """Two ranks on one GPU through IPC-mapped peer memory: collective self-test, the fused
+    Adam update matches the closed form, and both ranks end with identical weights."""
+    env = dict(os.environ, PYTHONPATH=ROOT, INTML_XGMI_SPIN_LIMIT=str(1 << 20))
+    for k in ("WORLD_SIZE", "RANK", "INTML_DP_BACKEND", "INTML_COMM"):
+        env.pop(k, None)
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "tests", "xgmi_worker_gpu.py"), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    reps = [json.load(open(tmp_path / ("xgmi%d.json" % i))) for i in range(2)]
+    for rep in reps:
+        assert rep["created"], r.stderr[-3000:]
+        assert rep["err"] == 0 and rep["grad_sum_ok"], rep
+        assert rep["adam_maxdiff"] < 1e-6, rep
+    assert reps[0]["p_digest"] == reps[1]["p_digest"]
