@@ -226,7 +226,8 @@ def main():
         sums = hvd.allgather(weight_checksum(model)) if size > 1 else [weight_checksum(model)]
         rstats = hvd.allgather(stats) if size > 1 else [stats]
         selfcheck = {
-            "data_plane": "rccl-native" if comm is not None else ("torch-" + str(st.backend)),
+            "data_plane": ("xgmi-fused-allreduce+optim" if getattr(red, "xgmi", None) is not None else
+                           "rccl-native" if comm is not None else ("torch-" + str(st.backend))),
             "rccl_nranks": comm.nranks if comm is not None else None,
             "world_size": size,
             "bucket_bytes": [4 * (hi - lo) for lo, hi in red.buckets] if red is not None else None,

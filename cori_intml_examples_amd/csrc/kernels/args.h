@@ -259,6 +259,7 @@ struct XgmiArgs {
   int sub = 0;                   // elements per workgroup slice of a chunk (multiple of 4)
   int spin_limit = 1 << 22;
   int mode = 1;                  // 0: sum only (reduced gradient -> grad); 1: + optimizer
+  int fence = 1;                 // system-scope release/acquire fences around the flags
   float* grad = nullptr;         // local flat gradient (read in 1, reduced sum written in 3)
   float* inbox[XGMI_MAX_RANKS] = {};     // rank j's inbox [P][chunk] (as mapped here)
   float* outbox[XGMI_MAX_RANKS] = {};    // rank j's outbox [P * chunk] = reduced gradient

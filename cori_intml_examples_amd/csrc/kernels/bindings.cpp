@@ -40,7 +40,7 @@ void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s);
 void launch_pack(const float* master, bf16* arena, const PackTable& tab, hipStream_t s);
 int xgmi_grid(const XgmiArgs& a);
 void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s);
-uintptr_t xgmi_alloc_uncached(size_t bytes);
+uintptr_t xgmi_alloc_uncached(size_t bytes, bool finegrained);
 void xgmi_free(uintptr_t p);
 std::string xgmi_ipc_handle(uintptr_t p);
 uintptr_t xgmi_ipc_open(const std::string& handle);
@@ -281,7 +281,7 @@ PYBIND11_MODULE(_kernels, m) {
   py::class_<XgmiArgs>(m, "XgmiArgs")
       .def(py::init<>())
       RW(XgmiArgs, rank) RW(XgmiArgs, size) RW(XgmiArgs, n) RW(XgmiArgs, chunk) RW(XgmiArgs, sub)
-      RW(XgmiArgs, spin_limit) RW(XgmiArgs, mode) PTR(XgmiArgs, grad) PTR(XgmiArgs, ctr) PTR(XgmiArgs, err)
+      RW(XgmiArgs, spin_limit) RW(XgmiArgs, mode) RW(XgmiArgs, fence) PTR(XgmiArgs, grad) PTR(XgmiArgs, ctr) PTR(XgmiArgs, err)
       RW(XgmiArgs, opt)
       .def("set_peer", [](XgmiArgs& a, int j, uintptr_t inbox, uintptr_t outbox, uintptr_t f1, uintptr_t f2) {
         if (j < 0 || j >= XGMI_MAX_RANKS) throw std::out_of_range("peer index");
@@ -301,7 +301,7 @@ PYBIND11_MODULE(_kernels, m) {
     launch_xgmi_allreduce(a, S(s));
     check_last("xgmi_allreduce");
   });
-  m.def("xgmi_alloc_uncached", &xgmi_alloc_uncached);
+  m.def("xgmi_alloc_uncached", &xgmi_alloc_uncached, py::arg("bytes"), py::arg("finegrained") = false);
   m.def("xgmi_free", &xgmi_free);
   m.def("xgmi_ipc_handle", [](uintptr_t p) { return py::bytes(xgmi_ipc_handle(p)); });
   m.def("xgmi_ipc_open", [](py::bytes h) { return xgmi_ipc_open(std::string(h)); });

@@ -22,13 +22,15 @@ namespace {
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Lanes 0..P-1 of wave 0 each raise flag `slot` of rank `lane` to seq.
-__device__ __forceinline__ void signal_all(unsigned* const* flags, int slot, int P, unsigned seq) {
+__device__ __forceinline__ void signal_all(unsigned* const* flags, int slot, int P, unsigned seq, int fence) {
   drain_stores();
   __syncthreads();
   const int t = threadIdx.x;
   if (t < P) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    drain_stores();
+    if (fence) {     // payload in uncached memory is not in any cache: drained stores suffice
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      drain_stores();
+    }
     __hip_atomic_store(flags[t] + slot, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -36,7 +38,7 @@ __device__ __forceinline__ void signal_all(unsigned* const* flags, int slot, int
 // Wait until local flags [base, base + P) all reach seq (lanes 0..P-1 poll one each).
 // Returns false (and sets *err) if a flag does not arrive within spin_limit polls.
 __device__ __forceinline__ bool wait_all(const unsigned* flags, int P, unsigned seq, int limit, int* err,
-                                         int phase) {
+                                         int phase, int fence) {
   __shared__ int s_ok;
   const int t = threadIdx.x;
   if (t == 0) s_ok = 1;
@@ -51,8 +53,10 @@ __device__ __forceinline__ bool wait_all(const unsigned* flags, int P, unsigned 
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    drain_stores();
+    if (fence) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      drain_stores();
+    }
   }
   __syncthreads();
   return s_ok != 0;
@@ -79,49 +83,83 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
   const int k0 = w * a.sub, k1 = min(k0 + a.sub, C);
   const long long n = a.n;
 
+  // Every phase first loads all P float4 of a thread into registers, then stores: the
+  // compiler cannot reorder loads across stores to possibly-aliasing pointers, and each
+  // uncached / remote access costs microseconds, so they must all be in flight together.
+  float* __restrict__ grad = a.grad;
+
   // 1. push my slice of every chunk to its owner's inbox row r
-  for (int j = 0; j < P; ++j) {
-    float* dst = a.inbox[j] + (size_t)r * C;
-    const long long base = (long long)j * C;
-    for (int k = k0 + 4 * t; k < k1; k += 1024)
-      *reinterpret_cast<float4*>(dst + k) = load4_guarded(a.grad, base + k, n);
+  for (int k = k0 + 4 * t; k < k1; k += 1024) {
+    float4 v[XGMI_MAX_RANKS];
+#pragma unroll
+    for (int j = 0; j < XGMI_MAX_RANKS; ++j)
+      if (j < P) v[j] = load4_guarded(grad, (long long)j * C + k, n);
+#pragma unroll
+    for (int j = 0; j < XGMI_MAX_RANKS; ++j)
+      if (j < P) *reinterpret_cast<float4*>(a.inbox[j] + (size_t)r * C + k) = v[j];
   }
-  signal_all(a.flag1, w * P + r, P, seq);
+  signal_all(a.flag1, w * P + r, P, seq, a.fence);
 
   // 2. reduce my chunk's slice over the P rows in rank order, push it to every outbox
-  bool ok = wait_all(a.flag1[r] + w * P, P, seq, a.spin_limit, a.err, 1);
+  bool ok = wait_all(a.flag1[r] + w * P, P, seq, a.spin_limit, a.err, 1, a.fence);
   if (ok) {
-    const float* in = a.inbox[r];
+    const float* __restrict__ in = a.inbox[r];
     for (int k = k0 + 4 * t; k < k1; k += 1024) {
-      float4 s = *reinterpret_cast<const float4*>(in + k);
-      for (int q = 1; q < P; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(in + (size_t)q * C + k);
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
-      for (int j = 0; j < P; ++j) *reinterpret_cast<float4*>(a.outbox[j] + (size_t)r * C + k) = s;
+      float4 v[XGMI_MAX_RANKS];
+#pragma unroll
+      for (int q = 0; q < XGMI_MAX_RANKS; ++q)
+        if (q < P) v[q] = *reinterpret_cast<const float4*>(in + (size_t)q * C + k);
+      float4 s4 = v[0];
+#pragma unroll
+      for (int q = 1; q < XGMI_MAX_RANKS; ++q)
+        if (q < P) { s4.x += v[q].x; s4.y += v[q].y; s4.z += v[q].z; s4.w += v[q].w; }
+#pragma unroll
+      for (int j = 0; j < XGMI_MAX_RANKS; ++j)
+        if (j < P) *reinterpret_cast<float4*>(a.outbox[j] + (size_t)r * C + k) = s4;
     }
   }
-  signal_all(a.flag2, w * P + r, P, seq);
+  signal_all(a.flag2, w * P + r, P, seq, a.fence);
 
   // 3. the whole reduced gradient is in my outbox: record it and update the parameters
-  ok = wait_all(a.flag2[r] + w * P, P, seq, a.spin_limit, a.err, 2) && ok;
+  ok = wait_all(a.flag2[r] + w * P, P, seq, a.spin_limit, a.err, 2, a.fence) && ok;
   if (ok) {
-    const float* red = a.outbox[r];
+    const float* __restrict__ red = a.outbox[r];
     const OptimArgs& o = a.opt;
-    for (int q = 0; q < P; ++q) {
-      for (int k = k0 + 4 * t; k < k1; k += 1024) {
+    for (int k = k0 + 4 * t; k < k1; k += 1024) {
+      float4 g[XGMI_MAX_RANKS];
+#pragma unroll
+      for (int q = 0; q < XGMI_MAX_RANKS; ++q)
+        if (q < P) g[q] = *reinterpret_cast<const float4*>(red + (size_t)q * C + k);
+#pragma unroll
+      for (int q = 0; q < XGMI_MAX_RANKS; ++q) {
         const long long idx = (long long)q * C + k;
-        if (idx >= n) break;
-        const float4 g4 = *reinterpret_cast<const float4*>(red + idx);
-        const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
-        const int m = (int)min(4LL, n - idx);
-        for (int e = 0; e < m; ++e) {
-          a.grad[idx + e] = gv[e];
+        if (q >= P || idx >= n) continue;
+        const float4 g4 = g[q];
+        if (idx + 4 <= n) {       // float4 path (idx, C, k multiples of 4: 16-byte aligned)
+          *reinterpret_cast<float4*>(grad + idx) = g4;
           if (a.mode == 1) {
-            float p = o.p[idx + e];
+            float4 p4 = *reinterpret_cast<const float4*>(o.p + idx);
+            float4 m4 = o.s0 ? *reinterpret_cast<const float4*>(o.s0 + idx) : float4{0.f, 0.f, 0.f, 0.f};
+            float4 v4 = o.s1 ? *reinterpret_cast<const float4*>(o.s1 + idx) : float4{0.f, 0.f, 0.f, 0.f};
+            const float gs = o.grad_scale;
+            opt_update<KIND>(o, o.st, p4.x, g4.x * gs, &m4.x, &v4.x);
+            opt_update<KIND>(o, o.st, p4.y, g4.y * gs, &m4.y, &v4.y);
+            opt_update<KIND>(o, o.st, p4.z, g4.z * gs, &m4.z, &v4.z);
+            opt_update<KIND>(o, o.st, p4.w, g4.w * gs, &m4.w, &v4.w);
+            *reinterpret_cast<float4*>(o.p + idx) = p4;
+            if (o.s0) *reinterpret_cast<float4*>(o.s0 + idx) = m4;
+            if (o.s1) *reinterpret_cast<float4*>(o.s1 + idx) = v4;
+          }
+          continue;
+        }
+        const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+        for (int e = 0; e < (int)(n - idx); ++e) {
+          grad[idx + e] = gv[e];
+          if (a.mode == 1) {
+            float pe = o.p[idx + e];
             float s0 = o.s0 ? o.s0[idx + e] : 0.f, s1 = o.s1 ? o.s1[idx + e] : 0.f;
-            opt_update<KIND>(o, o.st, p, gv[e] * o.grad_scale, &s0, &s1);
-            o.p[idx + e] = p;
+            opt_update<KIND>(o, o.st, pe, gv[e] * o.grad_scale, &s0, &s1);
+            o.p[idx + e] = pe;
             if (o.s0) o.s0[idx + e] = s0;
             if (o.s1) o.s1[idx + e] = s1;
           }
@@ -149,16 +187,17 @@ void launch_xgmi_allreduce(const XgmiArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- host: memory + IPC
-uintptr_t xgmi_alloc_uncached(size_t bytes) {
+uintptr_t xgmi_alloc_uncached(size_t bytes, bool finegrained) {
   void* p = nullptr;
-  if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess || p == nullptr)
-    throw std::runtime_error("hipExtMallocWithFlags(uncached) failed");
+  if (hipExtMallocWithFlags(&p, bytes, finegrained ? hipDeviceMallocFinegrained : hipDeviceMallocUncached) !=
+          hipSuccess || p == nullptr)
+    throw std::runtime_error("hipExtMallocWithFlags(uncached/fine-grained) failed");
   if (hipMemset(p, 0, bytes) != hipSuccess) throw std::runtime_error("hipMemset failed");
   if (hipDeviceSynchronize() != hipSuccess) throw std::runtime_error("hipDeviceSynchronize failed");
   return reinterpret_cast<uintptr_t>(p);
 }
 
-void xgmi_free(uintptr_t p) { hipFree(reinterpret_cast<void*>(p)); }
+void xgmi_free(uintptr_t p) { (void)hipFree(reinterpret_cast<void*>(p)); }
 
 std::string xgmi_ipc_handle(uintptr_t p) {
   hipIpcMemHandle_t h;
@@ -177,4 +216,4 @@ uintptr_t xgmi_ipc_open(const std::string& handle) {
   return reinterpret_cast<uintptr_t>(p);
 }
 
-void xgmi_ipc_close(uintptr_t p) { hipIpcCloseMemHandle(reinterpret_cast<void*>(p)); }
+void xgmi_ipc_close(uintptr_t p) { (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(p)); }

@@ -66,7 +66,7 @@ class XgmiAllreduce:
         err = None
         torch.cuda.set_device(device)
         try:
-            self.buf = K.xgmi_alloc_uncached(self.nbytes)
+            self.buf = K.xgmi_alloc_uncached(self.nbytes, os.environ.get("INTML_XGMI_MEM", "uncached") == "finegrained")
             handle = K.xgmi_ipc_handle(self.buf)
         except Exception as e:        # noqa: BLE001 -- reported through the vote below
             err, handle = "setup: %s" % e, b""
@@ -91,6 +91,7 @@ class XgmiAllreduce:
         a.rank, a.size, a.n, a.chunk, a.sub = rank, size, n, self.chunk, self.sub
         a.spin_limit = int(spin_limit or os.environ.get("INTML_XGMI_SPIN_LIMIT", 1 << 22))
         a.ctr, a.err = self.ctr.data_ptr(), self.err.data_ptr()
+        a.fence = int(os.environ.get("INTML_XGMI_FENCE", "1"))
         if err is None:
             for j, b in enumerate(bases):
                 a.set_peer(j, b + self.off_in, b + self.off_out, b + self.off_f1, b + self.off_f2)
