@@ -246,6 +246,24 @@ def main():
                 e2 = max(hvd.allgather(e2))
             selfcheck["nodp_ms_per_step"] = round(e2 / args.steps * 1e3, 4)
             selfcheck["exposed_comm_us_per_step"] = round((elapsed - e2) / args.steps * 1e6, 2)
+            if getattr(red, "xgmi", None) is not None:
+                # the same DP step with the RCCL all-reduce + optimizer launch instead of the
+                # fused xGMI kernel (comparison only; the line's value is the default path)
+                old = os.environ.get("INTML_XGMI")
+                os.environ["INTML_XGMI"] = "0"
+                try:
+                    alt, *_ = build(args, size, True, dev)
+                    hvd.broadcast_global_variables(0, model=alt)
+                    data3 = synthetic(max(args.samples, B * 4), shape, ncls, alt._executor, dev, g)
+                    e3, _ = time_steps(alt, data3, B, args.steps, args.warmup, chunk, g, dev)
+                finally:
+                    if old is None:
+                        os.environ.pop("INTML_XGMI", None)
+                    else:
+                        os.environ["INTML_XGMI"] = old
+                if size > 1:
+                    e3 = max(hvd.allgather(e3))
+                selfcheck["rccl_path_ms_per_step"] = round(e3 / args.steps * 1e3, 4)
 
     ms = elapsed / steps * 1e3
     value = size * B * steps / elapsed

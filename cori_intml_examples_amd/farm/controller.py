@@ -51,6 +51,7 @@ class _EngineRec:
         self.queue: Deque[str] = collections.deque()
         self.restarts = 0
         self.started_at = 0.0
+        self.stats: Dict[str, Any] = {}     # last resource telemetry from the engine
 
 
 class Controller:
@@ -225,8 +226,10 @@ class Controller:
         elif t == "ids":
             self._send(c, {"type": "reply", "req_id": msg.get("req_id"), "ids": self._ids()})
         elif t == "queue_status":
-            st = {e.eid: {"queue": len(e.queue), "running": e.current, "restarts": e.restarts,
-                          "pid": e.proc.pid if e.proc else None, "gpu": e.gpu} for e in self.engines.values()}
+            st = {e.eid: dict({k: v for k, v in e.stats.items() if k.endswith("_bytes") or k == "t"},
+                              queue=len(e.queue), running=e.current, restarts=e.restarts,
+                              pid=e.proc.pid if e.proc else None, gpu=e.gpu)
+                  for e in self.engines.values()}
             st["unassigned"] = len(self.lb_queue)
             self._send(c, {"type": "reply", "req_id": msg.get("req_id"), "status": st})
         elif t == "abort":
@@ -256,6 +259,9 @@ class Controller:
             rec.queue.append(task.msg_id)
 
     def _handle_engine(self, e: _EngineRec, msg):
+        if msg.get("type") == "stats":
+            e.stats = dict(msg.get("stats") or {}, t=time.time())
+            return
         mid = msg.get("msg_id")
         task = self.tasks.get(mid)
         if task is None:

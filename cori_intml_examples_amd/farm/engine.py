@@ -27,6 +27,7 @@ import os
 import queue
 import sys
 import threading
+import time
 import traceback
 from multiprocessing.connection import Client as _Conn
 from typing import Any, Dict, Optional
@@ -120,10 +121,44 @@ class Engine:
             return eval(payload, self.ns)
         raise ValueError("unknown task kind %r" % kind)
 
+    # -- resource telemetry -------------------------------------------------------------
+    def resource_stats(self) -> Dict[str, Any]:
+        """This engine's GPU and memory use: HIP device (HIP_VISIBLE_DEVICES), HBM reserved /
+        allocated by this process's caching allocator and the device total, host RSS.  Never
+        initialises the GPU itself (a HIP call from this thread would)."""
+        st: Dict[str, Any] = {"gpu": os.environ.get("HIP_VISIBLE_DEVICES"), "pid": os.getpid()}
+        try:
+            with open("/proc/self/statm") as f:
+                st["rss_bytes"] = int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+        except (OSError, ValueError):
+            pass
+        torch = sys.modules.get("torch")
+        try:
+            if torch is not None and torch.cuda.is_initialized():
+                dev = torch.cuda.current_device()
+                st["hbm_reserved_bytes"] = int(torch.cuda.memory_reserved(dev))
+                st["hbm_allocated_bytes"] = int(torch.cuda.memory_allocated(dev))
+                st["hbm_peak_bytes"] = int(torch.cuda.max_memory_reserved(dev))
+                st["hbm_total_bytes"] = int(torch.cuda.get_device_properties(dev).total_memory)
+        except Exception:                # noqa: BLE001 - telemetry must never kill the engine
+            pass
+        return st
+
+    def _telemetry(self, period: float):
+        while True:
+            time.sleep(period)
+            try:
+                self.send({"type": "stats", "stats": self.resource_stats()})
+            except Exception:            # noqa: BLE001 - connection gone: the engine is exiting
+                return
+
     def serve(self):
         global _ENGINE
         _ENGINE = self
         threading.Thread(target=self._reader, daemon=True, name="farm-engine-reader").start()
+        period = float(os.environ.get("INTML_FARM_STATS_PERIOD", "2.0"))
+        if period > 0:
+            threading.Thread(target=self._telemetry, args=(period,), daemon=True, name="farm-engine-stats").start()
         while True:
             try:
                 msg = self.tasks.get()

@@ -394,6 +394,24 @@ class ParamSpanModel:
         with self.lock:
             return self.table[["status"]].copy()
 
+    def resources_text(self) -> str:
+        """Per-engine resource line for the dashboard: GPU, HBM in use / total, host RSS,
+        queue depth and restarts (``get_resource_usage``)."""
+        try:
+            st = self.controller.get_resource_usage()
+        except Exception:                # noqa: BLE001 - the dashboard must keep rendering
+            return ""
+        gib = lambda b: "%.2f" % (b / 2.0 ** 30)
+        lines = []
+        for eid in sorted(k for k in st if isinstance(k, int)):
+            e = st[eid]
+            hbm = ("HBM %s/%s GiB" % (gib(e["hbm_reserved_bytes"]), gib(e.get("hbm_total_bytes", 0)))
+                   if "hbm_reserved_bytes" in e else "HBM -")
+            rss = "RSS %s GiB" % gib(e["rss_bytes"]) if "rss_bytes" in e else "RSS -"
+            lines.append("engine %d gpu %s: %s, %s, queue %d, restarts %d" % (
+                eid, e.get("gpu"), hbm, rss, e.get("queue", 0), e.get("restarts", 0)))
+        return "\n".join(lines)
+
     def snapshot(self):
         with self.lock:
             return copy.deepcopy(self.table)

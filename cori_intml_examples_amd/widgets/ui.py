@@ -153,8 +153,10 @@ else:
 
         def render(self) -> str:
             with self.lock:
-                return _text_table(self.table) + "\n\n" + self.plots[self.active].render() \
+                out = _text_table(self.table) + "\n\n" + self.plots[self.active].render() \
                     if hasattr(self.plots[self.active], "render") else _text_table(self.table)
+            res = self.resources_text()
+            return out + ("\n\n" + res if res else "")
 
         def __repr__(self):
             return self.render()

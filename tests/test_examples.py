@@ -71,3 +71,11 @@ def test_widget_hpo_script():
     out = _run(["widget_hpo_mnist.py", "--cpu", "--engines", "2", "--trials", "2", "--epochs", "2",
                 "--n-train", "300"])
     assert "Ended Training" in out and "best trial" in out
+
+
+def test_widget_hpo_rpv_script():
+    out = _run(["widget_hpo_rpv.py", "--cpu", "--engines", "2", "--trials", "3", "--epochs", "2",
+                "--n-train", "192", "--n-valid", "64", "--batch-size", "32", "--stop-first"])
+    assert "stopped trial 0; restarting it" in out
+    assert "best trial" in out and "worst trial" in out and "best model test metrics" in out
+    assert "engine 0 gpu" in out

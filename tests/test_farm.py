@@ -212,3 +212,21 @@ def test_runtime_dir_rejects_foreign_permissions(tmp_path, monkeypatch):
     os.chmod(path, 0o644)
     with pytest.raises(P.InsecurePathError):
         P.read_connection_file("sec")
+
+
+def test_resource_usage_telemetry(cluster):
+    """Engines report their resources (host RSS; HBM and GPU id on GPU engines) and the
+    controller serves them in queue_status / ModelController.get_resource_usage (the
+    reference's stub, hpo_widgets.py:366-367)."""
+    from cori_intml_examples_amd.widgets import ModelController
+    cl, c = cluster
+    mc = ModelController(client=c)
+    deadline = time.time() + 10
+    st = {}
+    while time.time() < deadline:
+        st = mc.get_resource_usage()
+        if all("rss_bytes" in st.get(e, {}) for e in c.ids):
+            break
+        time.sleep(0.3)
+    for e in c.ids:
+        assert st[e]["rss_bytes"] > 10 << 20 and "gpu" in st[e] and "queue" in st[e], st
