@@ -148,7 +148,10 @@ struct StepState {
   float lr_eff;   // lr after Keras `decay`
   float s[6];     // optimizer scalars for this step (meaning depends on optimizer kind)
   double m_schedule;  // Nadam running product
-  double metrics[4];  // loss_sum, correct_sum, count, spare
+  // metric accumulators as int64 fixed point (loss in units of 2^-32, correct/count exact):
+  // integer atomics commute, so the epoch sums are bit-identical whatever order the head's
+  // workgroups retire in (a float/double atomicAdd is order-dependent in its last bits)
+  long long metrics[4];  // loss_sum * 2^32, correct_sum, count, spare
   // bound dataset (host-written when the executor switches datasets, so captured graphs
   // are dataset-independent): x rows [n][R] bf16, targets [n][C] fp32, epoch permutation
   unsigned long long data_x, data_y, perm;

@@ -1,7 +1,8 @@
 // Fused output head (K11 / K12 + the last dense's K8/K9):
 //   logits = h W + b  ->  softmax | sigmoid | linear  ->  Keras loss (clipping semantics of
 //   categorical_crossentropy / binary_crossentropy) + accuracy,
-//   accumulated into device metrics (one atomic triple per workgroup, no per-batch D2H);
+//   accumulated into device metrics (one int64 fixed-point atomic triple per workgroup,
+//   order-independent, no per-batch D2H);
 // and in training mode, in the same launch:
 //   dz = dL/dlogits / batch, dW / db partial slabs (one per 4-row workgroup, reduced in
 //   fixed order by slab_reduce) and dh = dz W^T routed back through the previous stage's
@@ -163,9 +164,10 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   if (tid == 0 && a.y && a.st) {
     float ls = 0.f, cs = 0.f;
     for (int r = 0; r < rows_here; ++r) { ls += met[r][0]; cs += met[r][1]; }
-    atomicAdd(&a.st->metrics[0], (double)ls);
-    atomicAdd(&a.st->metrics[1], (double)cs);
-    atomicAdd(&a.st->metrics[2], (double)rows_here);
+    // per-workgroup sums in a fixed row order, then order-independent integer atomics
+    atomicAdd((unsigned long long*)&a.st->metrics[0], (unsigned long long)llrint((double)ls * 4294967296.0));
+    atomicAdd((unsigned long long*)&a.st->metrics[1], (unsigned long long)llrintf(cs));
+    atomicAdd((unsigned long long*)&a.st->metrics[2], (unsigned long long)rows_here);
   }
   if (!a.training) return;
 

@@ -450,9 +450,10 @@ class HipExecutor(Executor):
 
     # ------------------------------------------------------------------ metrics
     def _metrics(self):
+        # int64 fixed point (StepState::metrics): loss in units of 2^-32, counts exact
         o = self.K.STEP_STATE_METRICS_OFFSET // 8
-        v = self._st_f64[o:o + 3].tolist()
-        return v
+        ls, cs, n = self.state.view(torch.int64)[o:o + 3].tolist()
+        return [ls / 4294967296.0, float(cs), float(n)]
 
     def reset_metrics(self):
         o = self.K.STEP_STATE_METRICS_OFFSET // 8

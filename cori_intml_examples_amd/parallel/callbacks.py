@@ -1,4 +1,11 @@
-"""Horovod-keras callbacks (``rpv.py:83-93``; ``DistTrain_mnist.ipynb:494``)."""
+"""Horovod-keras callbacks (``rpv.py:83-93``; ``DistTrain_mnist.ipynb:494``).
+
+Attribution: ``LearningRateScheduleCallback`` / ``LearningRateWarmupCallback`` follow the
+semantics (steps-per-epoch autodetection, the Goyal et al. 2017 warmup multiplier, messages)
+of Horovod's Keras callbacks of the same names (Horovod, Apache License 2.0, Copyright 2018
+Uber Technologies, Inc.); the schedule itself runs on the device (``StepState`` warmup
+fields, ``misc.hip`` step bookkeeping), not in a per-batch host callback.
+"""
 from __future__ import annotations
 
 import numpy as np

@@ -5,6 +5,11 @@ user callbacks) and by the engine-side ``IPyParallelLogger`` (``mlextras.py:8-33
 Ordering in ``fit`` follows Keras: BaseLogger -> ProgbarLogger -> user callbacks ->
 History, so Horovod's MetricAverage (user list) runs before ReduceLROnPlateau and
 History records the averaged values (``rpv.py:83-98``).
+
+Attribution: ``ReduceLROnPlateau``, ``EarlyStopping``, ``ModelCheckpoint`` and ``CSVLogger``
+re-implement the documented behaviour of the Keras 2.2 callbacks of the same names (Keras,
+MIT License, Copyright (c) 2015-2018 the Keras authors) so that training runs reproduce the
+reference's LR schedule / stopping decisions bit for bit.
 """
 from __future__ import annotations
 

@@ -21,9 +21,9 @@ def _rel(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-12)
 
 
-def _step(kind, drop, cin, n=40, opt="SGD"):
+def _step(kind, drop, cin, hw=16, n=40, opt="SGD"):
     set_random_seed(99)
-    m = _build(kind, "cuda", opt=opt, drop=drop, cin=cin)
+    m = _build(kind, "cuda", opt=opt, drop=drop, cin=cin, hw=hw)
     ex = m._executor
     x, y = _data(m, n, seed=4)
     d = ex.upload(x, y)
@@ -63,11 +63,17 @@ def _full_dy(bp, g):
 
 CASES = [("rpv", 0.0, 1), ("rpv", 0.3, 3), ("mnist", 0.4, 1), ("odd", 0.25, 2), ("strided", 0.0, 3),
          ("wide", 0.2, 3), ("wide_strided", 0.0, 3)]
+# The benchmarked geometries at the benchmarked batch (bench.py --model rpv / mnist / rpv_legacy):
+# RPV 64x64x3 B=128 takes the 2-band conv_stack split and the pipelined 256-px wgrad_halo
+# blocks; MNIST 28x28x1 conv 32-64; the legacy widths 64-128(s2)-256-256(s2) with the
+# K = 65,536 split-K dense.  (kind, drop, cin, hw, n)
+BENCH_CASES = [("rpv_bench", 0.2, 3, 64, 128), ("mnist_bench", 0.4, 1, 28, 128), ("legacy", 0.0, 1, 64, 128)]
+ALL = [c + (16, 40) for c in CASES] + BENCH_CASES
 
 
-@pytest.mark.parametrize("kind,drop,cin", CASES)
-def test_conv_forward(kind, drop, cin):
-    m, ex, bp, wb = _step(kind, drop, cin)
+@pytest.mark.parametrize("kind,drop,cin,hw,n", ALL)
+def test_conv_forward(kind, drop, cin, hw, n):
+    m, ex, bp, wb = _step(kind, drop, cin, hw, n)
     step = int(ex._st_i32[0].item())
     x = _f(bp.xb).view(bp.bs, ex.in_H, ex.in_W, ex.in_Cs)[..., :ex.in_C]
     for g, cs in zip(ex.convs, ex.plan.convs):
@@ -85,9 +91,9 @@ def test_conv_forward(kind, drop, cin):
         x = got[..., :g.Cout]
 
 
-@pytest.mark.parametrize("kind,drop,cin", CASES)
-def test_conv_wgrad_and_bias(kind, drop, cin):
-    m, ex, bp, wb = _step(kind, drop, cin)
+@pytest.mark.parametrize("kind,drop,cin,hw,n", ALL)
+def test_conv_wgrad_and_bias(kind, drop, cin, hw, n):
+    m, ex, bp, wb = _step(kind, drop, cin, hw, n)
     for g, cs in zip(ex.convs, ex.plan.convs):
         if g.i == 0:
             x = _f(bp.xb).view(bp.bs, ex.in_H, ex.in_W, ex.in_Cs)[..., :ex.in_C]
@@ -103,9 +109,9 @@ def test_conv_wgrad_and_bias(kind, drop, cin):
         assert _rel(gb, db) < 5e-3, "conv %d bias grad" % g.i
 
 
-@pytest.mark.parametrize("kind,drop,cin", CASES)
-def test_conv_dgrad_bwd_through(kind, drop, cin):
-    m, ex, bp, wb = _step(kind, drop, cin)
+@pytest.mark.parametrize("kind,drop,cin,hw,n", ALL)
+def test_conv_dgrad_bwd_through(kind, drop, cin, hw, n):
+    m, ex, bp, wb = _step(kind, drop, cin, hw, n)
     step = int(ex._st_i32[0].item())
     for g, cs in zip(ex.convs, ex.plan.convs):
         if g.i == 0:
@@ -123,9 +129,9 @@ def test_conv_dgrad_bwd_through(kind, drop, cin):
         assert _rel(got, dx) < 1e-2, "dgrad into conv %d: %.3g" % (pg.i, _rel(got, dx))
 
 
-@pytest.mark.parametrize("kind,drop,cin", CASES)
-def test_dense_and_head(kind, drop, cin):
-    m, ex, bp, wb = _step(kind, drop, cin)
+@pytest.mark.parametrize("kind,drop,cin,hw,n", ALL)
+def test_dense_and_head(kind, drop, cin, hw, n):
+    m, ex, bp, wb = _step(kind, drop, cin, hw, n)
     step = int(ex._st_i32[0].item())
 
     def src_val(src):
