@@ -31,6 +31,7 @@ import os
 import sys
 import time
 
+ROOT = os.path.dirname(os.path.abspath(__file__))
 BASELINE_LEGACY_IMG_PER_S = 1240.0   # RPV legacy CNN (34.5M params), 1 GPU, Train_rpv.ipynb:304-312
 BASELINE_MNIST_IMG_PER_S = 43600.0   # MNIST DP aggregate, 8 Haswell nodes, DistTrain_mnist.ipynb:341-357
 
@@ -164,6 +165,23 @@ def run_fit(args, model, shape, ncls, size, dp):
     return elapsed, steps, [(b - a) / (per_rank // args.batch) * 1e3 for a, b in timed]
 
 
+def run_hpo(args, extra):
+    """HPO trials/hour on the BASELINE configs (benchmarks/hpo_throughput.py; one JSON line).
+    Runs in this process before anything touches the GPU (the farm engines / evaluation
+    processes own the GPUs)."""
+    sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+    import hpo_throughput
+    extra = [e for e in extra if e != "--"]
+    if args.hpo == "mnist":     # BASELINE: 64 MNIST trials (DistHPO_mnist: 16 epochs, 60k, B=128)
+        argv = ["--model", "mnist", "--trials", "64"]
+    elif args.hpo == "rpv":     # BASELINE config 5: RPV CNN, 8 concurrent trials (DistWidgetHPO_rpv)
+        argv = ["--model", "rpv", "--trials", "8", "--engines-per-gpu", "8"]
+    else:                       # CrayHPO_rpv: nested HPO x DP, 2-rank evaluations
+        argv = ["--mode", "cray", "--gpus-per-eval", "2", "--generations", "2", "--demes", "2", "--pop-size", "4"]
+    hpo_throughput.main(argv + extra)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -181,7 +199,16 @@ def main():
     ap.add_argument("--via-fit", action="store_true", help="time apps.rpv.train_model epochs (Keras fit path)")
     ap.add_argument("--fit-epochs", type=int, default=4)
     ap.add_argument("--lr-warmup-epochs", type=int, default=0)
-    args = ap.parse_args()
+    ap.add_argument("--hpo", choices=["mnist", "rpv", "cray"], default=None,
+                    help="instead of the training-step bench, measure HPO throughput (BASELINE.json's "
+                         "second metric): mnist = 64 DistHPO_mnist trials spread over the node's GPUs, "
+                         "rpv = DistWidgetHPO_rpv-style 8 concurrent RPV trials, cray = genetic search over "
+                         "2-rank DP train_rpv evaluations; extra flags after -- go to benchmarks/hpo_throughput.py")
+    args, extra = ap.parse_known_args()
+    if args.hpo:
+        return run_hpo(args, extra)
+    if extra:
+        ap.error("unrecognized arguments: %s" % " ".join(extra))
     if args.no_graphs:
         os.environ["INTML_GRAPHS"] = "0"
 
@@ -293,4 +320,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -10,6 +10,13 @@ On one MI355X node the unit is the GPU: the ``gpus`` of the node are cut into sl
 data-parallel job (``torch.distributed.run``, one rank per GPU, its own RCCL communicator
 on 127.0.0.1:<own port>) -- nested HPO x DP.  Slots run concurrently.
 
+``slots`` gives the slot list explicitly instead (one list of GPU ids per slot).  A slot
+that names one GPU more than once runs that many ranks on it (oversubscription: a 1-GPU
+box can still run a 2-rank nested evaluation); RCCL needs distinct devices per rank, so
+such a slot's ranks exchange gradients over gloo (``INTML_DP_BACKEND=gloo``) while the
+compute stays on the GPU.  ``slots_per_gpu`` > 1 repeats every slot that many times
+(several small evaluations share a GPU concurrently, as the farm's engines-per-GPU do).
+
 An evaluation whose command fails or prints no ``FoM:`` line scores ``inf`` (worst);
 ``retries`` re-runs it first.  Each run's stdout/stderr goes to ``log_dir`` if given.
 """
@@ -79,7 +86,8 @@ class Evaluator:
                  alloc_args: Optional[str] = None, launcher: str = "local", verbose: bool = False,
                  gpus: Optional[Sequence[int]] = None, gpus_per_eval: Optional[int] = None,
                  timeout: Optional[float] = None, env: Optional[Dict[str, str]] = None, retries: int = 0,
-                 log_dir: Optional[str] = None, cwd: Optional[str] = None, cpu_slots: Optional[int] = None):
+                 log_dir: Optional[str] = None, cwd: Optional[str] = None, cpu_slots: Optional[int] = None,
+                 slots: Optional[Sequence[Sequence[int]]] = None, slots_per_gpu: int = 1):
         self.cmd = cmd
         self.per_eval = int(gpus_per_eval or nodes_per_eval or 1)
         if gpus is None:
@@ -92,7 +100,12 @@ class Evaluator:
         self.alloc_args, self.launcher, self.verbose = alloc_args, launcher, verbose
         self.timeout, self.retries, self.log_dir, self.cwd = timeout, int(retries), log_dir, cwd
         self.env = dict(env or {})
-        if self.gpus:
+        if slots is not None:
+            self.slots = [list(sl) for sl in slots]
+            if any(len(sl) != self.per_eval for sl in self.slots):
+                raise ValueError("every slot must list gpus_per_eval=%d GPU ids" % self.per_eval)
+            self.gpus = sorted({g for sl in self.slots for g in sl})
+        elif self.gpus:
             if len(self.gpus) < self.per_eval:
                 raise ValueError("gpus_per_eval=%d but only %d GPUs" % (self.per_eval, len(self.gpus)))
             self.slots = [self.gpus[i * self.per_eval:(i + 1) * self.per_eval]
@@ -100,6 +113,8 @@ class Evaluator:
         else:       # no GPU on this host: CPU slots (tests, dry runs)
             n = cpu_slots or (int(nodes) // self.per_eval if nodes else 2)
             self.slots = [None] * max(1, n)
+        if slots_per_gpu > 1:
+            self.slots = [sl for sl in self.slots for _ in range(int(slots_per_gpu))]
         self.history: List[Dict[str, Any]] = []
         self._lock = threading.Lock()
         self._count = 0
@@ -140,7 +155,10 @@ class Evaluator:
         env.update(self.env)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if slot is not None:
-            env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in slot)
+            uniq = list(dict.fromkeys(slot))
+            env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in uniq)
+            if len(uniq) < len(slot):      # ranks share a GPU (LOCAL_RANK % visible devices)
+                env.setdefault("INTML_DP_BACKEND", "gloo")
         else:
             env.setdefault("INTML_DEVICE", "cpu")
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -206,6 +224,10 @@ class Evaluator:
         for t in threads:
             t.join()
         return [r["fom"] for r in results]
+
+    @staticmethod
+    def oversubscribed(slot) -> bool:
+        return slot is not None and len(set(slot)) < len(slot)
 
     def __repr__(self):
         return "Evaluator(%r, slots=%d x %d GPU)" % (self.cmd, self.num_slots, self.per_eval)

@@ -101,3 +101,23 @@ def test_hip_data_parallel_two_ranks(tmp_path):
     assert reps[0]["w1"] == reps[1]["w1"] and reps[0]["wf"] == reps[1]["wf"]       # lockstep
     assert reps[0]["val_loss"] == reps[1]["val_loss"]
     assert reps[0]["rel_diff"] < 0.05, reps[0]["rel_diff"]      # bf16 half-batches vs one global batch
+
+
+def test_nested_hpo_dp_evaluation_gpu(tmp_path):
+    """Nested HPO x DP (CrayHPO_rpv.ipynb:62-64,145-151): one Evaluator evaluation that is a
+    2-rank torch.distributed.run train_rpv job on GPU.  With >= 2 GPUs the slot is two
+    distinct GPUs and gradients go over RCCL; on a 1-GPU box both ranks share GPU 0 (the
+    slot names it twice) and exchange gradients over gloo -- said in the assert message."""
+    import torch
+    from cori_intml_examples_amd import hpo
+    n = torch.cuda.device_count()
+    slots = [[0, 1]] if n >= 2 else [[0, 0]]
+    ev = hpo.Evaluator("python -m cori_intml_examples_amd.apps.train_rpv --synthetic --n-epochs 1 "
+                       "--n-train 2048 --n-valid 512 --fom best", gpus_per_eval=2, slots=slots,
+                       timeout=240, cwd=ROOT, log_dir=str(tmp_path))
+    foms = ev.evaluate([["--lr", "0.001"]])
+    rec = ev.history[0]
+    out = open(sorted(tmp_path.glob("eval*.out"))[0]).read()
+    plane = "gloo, ranks share GPU 0" if n < 2 else "rccl over 2 GPUs"
+    assert rec["ok"] and np.isfinite(foms[0]), "%s: rc %s\n%s" % (plane, rec["rc"], out[-3000:])
+    assert "rank 0/2" in out, out[-2000:]

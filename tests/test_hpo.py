@@ -178,3 +178,35 @@ def test_evaluator_timeout_kills_whole_process_group(tmp_path):
     else:
         os.kill(pid, signal.SIGKILL)
         raise AssertionError("grandchild %d survived the evaluation timeout" % pid)
+
+
+def test_evaluator_explicit_and_shared_gpu_slots(monkeypatch):
+    """Explicit slots; a slot naming one GPU twice runs 2 ranks on it with the gloo data plane;
+    slots_per_gpu repeats slots (several evaluations per GPU)."""
+    monkeypatch.delenv("INTML_DP_BACKEND", raising=False)
+    ev = hpo.Evaluator("python -c pass", gpus_per_eval=2, slots=[[0, 0]], slots_per_gpu=3)
+    assert ev.num_slots == 3 and ev.gpus == [0]
+    assert ev.oversubscribed([0, 0]) and not ev.oversubscribed([0, 1])
+    env = ev._env_for([0, 0])
+    assert env["HIP_VISIBLE_DEVICES"] == "0" and env["INTML_DP_BACKEND"] == "gloo"
+    env = hpo.Evaluator("python -c pass", gpus_per_eval=2, slots=[[2, 3]])._env_for([2, 3])
+    assert env["HIP_VISIBLE_DEVICES"] == "2,3" and "INTML_DP_BACKEND" not in env
+    cmd = ev.command_for(["--lr", "0.1"], [0, 0])
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"] and "2" in cmd
+    with pytest.raises(ValueError):
+        hpo.Evaluator("python -c pass", gpus_per_eval=2, slots=[[0]])
+
+
+def test_cray_bench_cpu():
+    """bench.py --hpo cray: genetic search over 2-rank DP train_rpv processes (gloo on CPU)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--hpo", "cray", "--", "--cpu",
+                        "--generations", "1", "--demes", "1", "--pop-size", "2", "--n-train", "256",
+                        "--n-valid", "128", "--epochs", "1"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["unit"] == "evaluations/hour" and rec["evaluations"] == 2 and rec["failed"] == 0
+    assert rec["gpus_per_eval"] == 2 and rec["value"] > 0
