@@ -121,3 +121,39 @@ def test_nested_hpo_dp_evaluation_gpu(tmp_path):
     plane = "gloo, ranks share GPU 0" if n < 2 else "rccl over 2 GPUs"
     assert rec["ok"] and np.isfinite(foms[0]), "%s: rc %s\n%s" % (plane, rec["rc"], out[-3000:])
     assert "rank 0/2" in out, out[-2000:]
+
+
+def test_dist_train_px_engines_gpu():
+    """DistTrain_rpv through %%px on farm engines (DistTrain_mnist.ipynb:148,294-317,494):
+    two engines pinned to GPU 0, hvd.init() inside the engines turns them into one 2-rank
+    data-parallel job (gloo data plane: RCCL needs distinct GPUs per rank), the HIP
+    executor trains on the GPU and both engines end in lockstep."""
+    from cori_intml_examples_amd import farm
+    from cori_intml_examples_amd.farm import magics
+    cl = farm.start_cluster(2, cluster_id="gpu_px_%d" % os.getpid(), gpus=[0, 0], timeout=300,
+                            env={"INTML_DP_BACKEND": "gloo"})
+    try:
+        with cl.client() as c:
+            ar = magics.px(
+                "import numpy as np\n"
+                "from cori_intml_examples_amd.parallel import hvd\n"
+                "from cori_intml_examples_amd.apps.rpv import build_model, train_model\n"
+                "from cori_intml_examples_amd.io.datasets import synthetic_rpv\n"
+                "hvd.init()\n"
+                "x, y, _ = synthetic_rpv(2048, channels=1, seed=3)\n"
+                "xv, yv, _ = synthetic_rpv(512, channels=1, seed=4)\n"
+                "model = build_model(x.shape[1:], conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.2,\n"
+                "                    optimizer='Adam', lr=0.001 * hvd.size(), use_horovod=True)\n"
+                "history = train_model(model, x, y, xv, yv, batch_size=128, n_epochs=2, use_horovod=True, verbose=0)\n"
+                "wsum = float(sum(np.abs(w).sum() for w in model.get_weights()))\n"
+                "dev = str(model.device); ex = type(model._executor).__name__; world = hvd.size()\n",
+                client=c, verbose=False, block=True)
+            dv = c[:]
+            assert dv.pull("world") == [2, 2]
+            assert dv.pull("ex") == ["HipExecutor"] * 2 and all(d.startswith("cuda") for d in dv.pull("dev"))
+            ws = dv.pull("wsum")
+            assert ws[0] == ws[1], ws                                   # lockstep weights
+            vl = dv.pull("history.history['val_loss']")
+            assert len(vl[0]) == 2 and vl[0] == vl[1] and np.all(np.isfinite(vl[0])), vl
+    finally:
+        cl.stop()
