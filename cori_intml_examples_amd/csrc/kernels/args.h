@@ -82,12 +82,15 @@ struct ConvStackArgs {
   uint32_t seed = 0;
   const StepState* st = nullptr;
   int off_w = 0, off_buf[2] = {0, 0}, off_codes = 0, lds_bytes = 0;   // LDS layout (bytes)
-  int dbg = 0;   // ablation (timing only, wrong results): 1 no MFMA loop, 2 no epilogue, 4 no global stores, 8 no staging
+  int off_bias = 0;                   // LDS bytes: biases [MAX_STACK][64] fp32
+  int dbg = 0;   // ablation (timing only, wrong results): 1 no MFMA loop, 2 no epilogue, 4 no global stores, 8 no staging;
+                 // 16 = generic layer path only (A/B of the row-aligned path; results exact)
   int splits = 1;                     // workgroups (row bands) per image
   // per layer, per band: conv-output rows [c0, c1) computed, stage-output rows [own0, own1)
   // stored, input halo image = input rows [ib, ib + ih)
   int rows[MAX_STACK][MAX_STACK_SPLIT][6] = {};
   StackLayer L[MAX_STACK];
+  unsigned long long* ts = nullptr;   // diagnostics: per-wave phase stamps [blocks*8][32]: 16 wall, 16 shader clock (null = off)
 };
 
 // Weight gradient: dW[k][n] = sum_pixels im2col(x)[p][k] * dY[p][n]  (split over pixels)
@@ -226,7 +229,7 @@ struct RedDesc {
   int ld;              // row stride (n) of the slab
   int dst_off, numel, type;
   int KH, KW, Cin, Cout, Cs;   // conv: k = tap*Cs + ci ; flat: C=Cin (channels), Cs
-  int tpe;             // threads per element (1..64, power of 2): lanes split the S partials
+  int tpe;             // threads per element (1..256, power of 2): lanes split the S partials
   int blk0;            // first workgroup of this descriptor in the launch
   int pad_;
 };

@@ -137,7 +137,7 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(ConvStackArgs, x) RW(ConvStackArgs, B) RW(ConvStackArgs, n) RW(ConvStackArgs, seed)
       PTR(ConvStackArgs, st) RW(ConvStackArgs, dbg) RW(ConvStackArgs, off_w) RW(ConvStackArgs, off_codes) RW(ConvStackArgs, lds_bytes)
       .def("set_buf_offsets", [](ConvStackArgs& a, int b0, int b1) { a.off_buf[0] = b0; a.off_buf[1] = b1; })
-      RW(ConvStackArgs, splits)
+      RW(ConvStackArgs, splits) PTR(ConvStackArgs, ts) RW(ConvStackArgs, off_bias)
       .def("set_rows", [](ConvStackArgs& a, int l, int sp, int c0, int c1, int o0, int o1, int ib, int ih) {
         if (l < 0 || l >= MAX_STACK || sp < 0 || sp >= MAX_STACK_SPLIT) throw std::out_of_range("conv stack rows");
         const int v[6] = {c0, c1, o0, o1, ib, ih};
@@ -207,18 +207,27 @@ PYBIND11_MODULE(_kernels, m) {
       .def(py::init([]() { RedTable t; memset(&t, 0, sizeof(t)); return t; }))
       .def_readonly("n", &RedTable::n)
       .def("add", [](RedTable& t, uintptr_t slab, long long stride_s, int S, int ld, int dst_off, int numel,
-                      int type, int KH, int KW, int Cin, int Cout, int Cs) {
+                      int type, int KH, int KW, int Cin, int Cout, int Cs, int tpe) {
         if (t.n >= MAX_RED) throw std::runtime_error("RedTable full");
         RedDesc& d = t.d[t.n++];
         d.slab = reinterpret_cast<const float*>(slab); d.stride_s = stride_s; d.S = S; d.ld = ld;
         d.dst_off = dst_off; d.numel = numel; d.type = type; d.KH = KH; d.KW = KW; d.Cin = Cin;
         d.Cout = Cout; d.Cs = Cs; d.pad_ = 0;
-        // threads per element: enough lanes that each sums <= ~8 partials
-        d.tpe = S <= 4 ? 1 : S <= 32 ? 4 : S <= 512 ? 16 : 64;
+        // threads per element (power of 2, <= 64): E = 256 / tpe consecutive elements per
+        // workgroup keep each slab-row read >= 16 contiguous bytes; each thread sums its
+        // S / tpe partials 8 independent loads at a time
+        if (tpe > 0) {
+          if (tpe > 256 || (tpe & (tpe - 1))) throw std::invalid_argument("tpe: power of 2 <= 256");
+          d.tpe = tpe;
+        } else {
+          d.tpe = 1;                                    // ~S/16 partials per thread (sweep:
+          while (d.tpe < 64 && d.tpe * 16 < S) d.tpe *= 2;   // scripts/red_sweep.py)
+        }
         d.blk0 = t.nblocks;
         const int epb = 256 / d.tpe;
         t.nblocks += (numel + epb - 1) / epb;
-      });
+      }, py::arg("slab"), py::arg("stride_s"), py::arg("S"), py::arg("ld"), py::arg("dst_off"), py::arg("numel"),
+      py::arg("type"), py::arg("KH"), py::arg("KW"), py::arg("Cin"), py::arg("Cout"), py::arg("Cs"), py::arg("tpe") = -1);
 
   m.attr("STEP_STATE_BYTES") = (int)sizeof(StepState);
   m.attr("STEP_STATE_METRICS_OFFSET") = (int)offsetof(StepState, metrics);

@@ -35,6 +35,17 @@
 
 typedef LDS bf16 lbf16;
 
+__device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// phase stamp (diagnostics only: A.ts null in production): wall clock per wave, lane 0
+#define STACK_STAMP(i)                                                                                   \
+  if (A.ts && (threadIdx.x & 63) == 0) {                                                                 \
+    unsigned long long* ts_ = A.ts + ((size_t)blockIdx.x * STACK_WAVES + (threadIdx.x >> 6)) * 32 + (i);  \
+    ts_[0] = wall_clock64();                                                                             \
+    ts_[16] = clock64();                                                                                 \
+  }
+
+
 // One layer over the workgroup's conv-output rows [c0, c1).  Local conv row y reads rows
 // y + roff + ky of the input halo image `in`; stage output row py lands in row py - obase
 // of `outimg` (skipped outside [0, OH)); codes are kept for the local stage rows.
@@ -42,7 +53,7 @@ template <int NT, int TM, bool CS4>
 __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                             int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
                                             int OW, LDS uint8_t* codes, const lbf16* wl, const LDS int* tab,
-                                            const lbf16* zl, uint32_t step) {
+                                            const lbf16* zl, uint32_t step, const LDS float* lb) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
   const int Wi = L.Wo + L.KW - 1;
   const int Cs = L.Cs_in, Cso = L.Cs_out, Cout = L.Cout, Wp = L.Wp, Wo = L.Wo, KS = L.KS;
@@ -62,7 +73,7 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int n = nt * 16 + r;
-    bias[nt] = (L.bias && n < Cout) ? L.bias[n] : 0.f;
+    bias[nt] = n < Cout ? lb[n] : 0.f;     // staged in LDS at kernel start
   }
   for (int tb = wave * TM; tb < ntiles; tb += STACK_WAVES * TM) {
     bool rv[TM];
@@ -183,13 +194,138 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
   }
 }
 
+// Row-aligned fast path for pooled layers whose pooled width is a multiple of 4 (every
+// pooled layer of the RPV / DistTrain_mnist stacks): an m-tile is 4 consecutive pooling
+// windows of ONE pooled row, so the tile -> (row, column) split is wave-uniform scalar
+// arithmetic and each lane's pixel is a fixed offset from the tile base (no per-lane
+// divisions, no per-tile validity selects).  The per-lane tap offsets of every k-step are
+// computed once per layer into registers (KS is a template parameter), and the k padding
+// beyond the last tap points at the pixel itself -- finite activations times the pack's
+// zero rows -- instead of a zero buffer behind a select.  Same k order, rounding points,
+// argmax codes and dropout counters as stack_layer (bit-identical).
+template <int NT, int TM, bool CS4, int KS>
+__device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
+                                                 int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
+                                                 int OW, LDS uint8_t* codes, const lbf16* wl, uint32_t step,
+                                                 const LDS float* lb, bool stamp) {
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Wi = L.Wo + L.KW - 1;
+  const int Cs = L.Cs_in, Cso = L.Cs_out, Cout = L.Cout, Wp = L.Wp;
+  const int p0 = c0 >> 1;
+  const int tpr = Wp >> 2;                      // tiles per pooled row
+  const int ntiles = ((c1 - c0) >> 1) * tpr;
+  const uint32_t thr = L.drop_thr, sid = L.stream_id, seed = A.seed;
+  const float dscale = L.drop_scale;
+  const uint32_t qb = (uint32_t)(b * L.Hp + p0) * (uint32_t)Wp;
+  // lane -> (window j, sub-pixel dy, dx) of the tile's 2 x 8 conv pixels
+  const int lane_px = ((((r >> 1) & 1) * Wi) + 2 * (r >> 2) + (r & 1)) * Cs;
+  // per-lane tap offsets of every k-step (k = tap * Cs + c, lanes of group g hold k0 .. k0+7)
+  int e0[KS], e1[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int k0 = ks * 32 + g * 8;
+    if (CS4) {
+      const int t0 = k0 >> 2, t1 = t0 + 1;
+      e0[ks] = t0 < 9 ? ((t0 / 3) * Wi + (t0 % 3)) * 4 : 0;
+      e1[ks] = t1 < 9 ? ((t1 / 3) * Wi + (t1 % 3)) * 4 : 0;
+    } else {
+      const int tap = k0 / Cs, c = k0 - tap * Cs;
+      e0[ks] = tap < 9 ? ((tap / 3) * Wi + (tap % 3)) * Cs + c : 0;
+    }
+  }
+  float bias[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n = nt * 16 + r;
+    bias[nt] = n < Cout ? lb[n] : 0.f;     // staged in LDS at kernel start
+  }
+  for (int tb = wave * TM; tb < ntiles; tb += STACK_WAVES * TM) {
+    int base[TM];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      const int tile = min(tb + t, ntiles - 1);   // duplicate of a valid tile: computed, not stored
+      const int pyl = tile / tpr, wx0 = (tile - pyl * tpr) * 4;
+      base[t] = ((2 * pyl + roff) * Wi + 2 * wx0) * Cs + lane_px;
+    }
+    f32x4 acc[TM][NT];
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // software-pipelined k loop: the fragments of k-step ks+1 are requested before the
+    // MFMAs of k-step ks issue (sched_barrier pins the order), so LDS latency hides behind
+    // the matrix work instead of a wait in front of every MFMA pair
+    bf16x8 af[2][TM], bf[2][NT];
+    auto load_k = [&](int ks, bf16x8* a, bf16x8* bv) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        if (CS4) {
+          const bf16x4 v0 = *reinterpret_cast<const LDS bf16x4*>(in + base[t] + e0[ks]);
+          const bf16x4 v1 = *reinterpret_cast<const LDS bf16x4*>(in + base[t] + e1[ks]);
+          a[t] = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+        } else {
+          a[t] = *reinterpret_cast<const LDS bf16x8*>(in + base[t] + e0[ks]);
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bv[nt] = *reinterpret_cast<const LDS bf16x8*>(wl + ((ks * NT + nt) * 64 + lane) * 8);
+    };
+    load_k(0, af[0], bf[0]);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) load_k(ks + 1, af[(ks + 1) & 1], bf[(ks + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int t = 0; t < TM; ++t) acc[t][nt] = mfma16(af[ks & 1][t], bf[ks & 1][nt], acc[t][nt]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (stamp && tb == wave * TM) {
+      asm volatile("" ::"v"(acc[0][0][0]));
+      STACK_STAMP(14);
+    }
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      const int tile = tb + t;
+      if (tile >= ntiles) break;
+      const int pyl = tile / tpr, pxl = (tile - pyl * tpr) * 4 + g;
+      const int orow = p0 + pyl - obase;
+      const bool keep = orow >= 0 && orow < OH;
+      const int oo = (orow * OW + pxl + ol) * Cso, co = (pyl * Wp + pxl) * Cso;
+      const uint32_t qi = (qb + (uint32_t)(pyl * Wp + pxl)) * (uint32_t)Cout;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int n = nt * 16 + r;
+        if (n >= Cso) continue;
+        float best = 0.f;
+        int code = 0;
+        if (n < Cout) {
+          best = -3.4e38f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v = acc[t][nt][j] + bias[nt];
+            if (L.relu) v = fmaxf(v, 0.f);
+            if (v > best) { best = v; code = j; }
+          }
+          if (thr) best = dropout_keep(qi + (uint32_t)n, seed, sid, step, thr) ? best * dscale : 0.f;
+          if (keep) outimg[oo + n] = f2bf(best);
+        }
+        codes[co + n] = (uint8_t)code;
+      }
+    }
+    if (stamp && tb == wave * TM) STACK_STAMP(15);
+  }
+}
+
 template <int NT, bool CS4>
 __device__ __forceinline__ void stack_layer_tm(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                                int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
                                                int OW, LDS uint8_t* codes, const lbf16* wl, const LDS int* tab,
-                                               const lbf16* zl, uint32_t step) {
+                                               const lbf16* zl, uint32_t step, const LDS float* lb) {
   constexpr int TM = NT >= 2 ? 2 : 4;
-  stack_layer<NT, TM, CS4>(A, L, b, c0, c1, roff, in, outimg, obase, OH, ol, OW, codes, wl, tab, zl, step);
+  stack_layer<NT, TM, CS4>(A, L, b, c0, c1, roff, in, outimg, obase, OH, ol, OW, codes, wl, tab, zl, step, lb);
 }
 
 __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const ConvStackArgs A) {
@@ -202,10 +338,27 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   lbf16* wlds = (lbf16*)(smem + A.off_w);
   LDS uint8_t* codes = (LDS uint8_t*)(smem + A.off_codes);
   const uint32_t step = A.st ? (uint32_t)A.st->t : 0u;
+  STACK_STAMP(0);
   if (tid < 8) ((LDS uint32_t*)zl)[tid] = 0u;
+  // biases -> LDS [layer][64] (read by the epilogues: no global load after the prefetch
+  // below, which would otherwise make its first use wait for every prefetched vector)
+  LDS float* lbias = (LDS float*)(smem + A.off_bias);
+  for (int i = tid; i < A.n * 64; i += STACK_THREADS) {
+    const StackLayer& L = A.L[i >> 6];
+    const int c = i & 63;
+    lbias[i] = (L.bias && c < L.Cout) ? L.bias[c] : 0.f;
+  }
 
-  // every layer's weight pack -> LDS (one contiguous run per layer)
-  for (int l = 0; l < ((A.dbg & 8) ? 0 : A.n); ++l) {
+  // Weight packs -> LDS.  Layer 0's synchronously; the later layers' are loaded into
+  // registers now (issued after the image, so waiting for the image does not wait for them)
+  // and written to LDS only before layer 1 -- their latency hides behind layer 0.
+  constexpr int PF = 8;
+  // vectors of layers 1, 2, 3 (static indices: the kernarg loads hoist out of the loops)
+  const int nv1 = A.n > 1 ? A.L[1].KS * A.L[1].NT * 64 : 0;
+  const int nv2 = A.n > 2 ? A.L[2].KS * A.L[2].NT * 64 : 0;
+  const int nv3 = A.n > 3 ? A.L[3].KS * A.L[3].NT * 64 : 0;
+  const bool prefetch = !(A.dbg & 8) && A.n > 1 && nv1 + nv2 + nv3 <= PF * STACK_THREADS;
+  for (int l = 0; l < ((A.dbg & 8) ? 0 : (prefetch ? 1 : A.n)); ++l) {
     const StackLayer& L = A.L[l];
     const int nv = L.KS * L.NT * 64;
     const bf16* src = L.wpk;
@@ -248,6 +401,19 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     }
   }
 
+  bf16x8 pf[PF];
+  if (prefetch) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int v = tid + j * STACK_THREADS;
+      const bf16* src = v < nv1 ? A.L[1].wpk + (size_t)v * 8
+                      : v < nv1 + nv2 ? A.L[2].wpk + (size_t)(v - nv1) * 8
+                      : A.L[A.n > 3 ? 3 : 1].wpk + (size_t)(v < nv1 + nv2 + nv3 ? v - nv1 - nv2 : 0) * 8;
+      pf[j] = load_bf16x8_if(v < nv1 + nv2 + nv3, src, A.L[1].wpk);
+    }
+  }
+
+  STACK_STAMP(1);
   for (int l = 0; l < A.n; ++l) {
     const StackLayer L = A.L[l];      // by value: one batch of scalar loads per layer instead of
     const bool last = l + 1 == A.n;   // a kernarg reload of every field after each barrier
@@ -266,11 +432,39 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       const StackLayer& N = A.L[l + 1];
       obase = A.rows[l + 1][sp][4], OH = A.rows[l + 1][sp][5], ol = N.pad_l, OW = N.Wo + N.KW - 1;
     }
+    if (l == 1 && prefetch) {
+      const int w1 = A.L[1].w_lds, w2 = A.n > 2 ? A.L[2].w_lds : 0, w3 = A.n > 3 ? A.L[3].w_lds : 0;
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int v = tid + j * STACK_THREADS;
+        const int e = v < nv1 ? w1 + v * 8 : v < nv1 + nv2 ? w2 + (v - nv1) * 8 : w3 + (v - nv1 - nv2) * 8;
+        if (v < nv1 + nv2 + nv3) *reinterpret_cast<LDS bf16x8*>(wlds + e) = pf[j];
+      }
+    }
     {
       LDS bf16x8* z = (LDS bf16x8*)out;
-      const int nz = (OH * OW * L.Cs_out) >> 3;   // Cs_out % 8 == 0
       const bf16x8 zero8 = zero_bf16x8();
-      for (int i = tid; i < nz; i += STACK_THREADS) z[i] = zero8;
+      // The epilogue writes every channel of output rows [wr0, wr1) x columns [ol, ol + Wp)
+      // (all channels when Cs_out == Cout); only the rest of the image needs zeros.
+      const int nr = L.pool ? (c1 - c0) >> 1 : c1 - c0;
+      const int wr0 = max(0, p0 - obase), wr1 = min(OH, p0 - obase + nr);
+      if (L.Cs_out == L.Cout && wr0 < wr1 && !(A.dbg & 3)) {
+        const int cpp = L.Cs_out >> 3;
+        const int nrow = OW * cpp;                          // vectors per image row
+        const int ntop = wr0 * nrow, nbot = (OH - wr1) * nrow;
+        const int nside = (OW - L.Wp) * cpp;                // border vectors per written row
+        for (int i = tid; i < ntop + nbot; i += STACK_THREADS) z[i < ntop ? i : wr1 * nrow + (i - ntop)] = zero8;
+        if (nside > 0) {
+          const int lcols = ol * cpp;
+          for (int i = tid; i < (wr1 - wr0) * nside; i += STACK_THREADS) {
+            const int rr = i / nside, c = i - rr * nside;
+            z[(wr0 + rr) * nrow + (c < lcols ? c : c + L.Wp * cpp)] = zero8;
+          }
+        }
+      } else {
+        const int nz = (OH * OW * L.Cs_out) >> 3;   // Cs_out % 8 == 0
+        for (int i = tid; i < nz; i += STACK_THREADS) z[i] = zero8;
+      }
       const int Wi = L.Wo + L.KW - 1, KHW = L.KH * L.KW, cw = L.Cs_in == 4 ? 4 : 8;
       const int ntab = L.Cs_in == 4 ? L.KS * 8 : L.KS * 4;
       for (int c = tid; c < ntab; c += STACK_THREADS) {
@@ -284,9 +478,23 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       }
     }
     __syncthreads();
+    STACK_STAMP(2 + 4 * l);
     const lbf16* wl = wlds + L.w_lds;
-#define STACK_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, OW, codes, wl, tab, zl, step
-    if (L.Cs_in == 4) {
+#define STACK_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, OW, codes, wl, tab, zl, step, lbias + l * 64
+#define ROWS_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, OW, codes, wl, step, lbias + l * 64, l == A.n - 1
+    // row-aligned fast path (pooled, pooled width % 4 == 0, 3x3, instantiated KS), else generic
+    const bool rows_ok = !(A.dbg & 16) && L.pool && (L.Wp & 3) == 0 && L.KH == 3 && L.KW == 3 && !(A.dbg & 3);
+    // TM = 1 when it evens out the waves' tile counts (few tiles per workgroup)
+    const int ntl = ((c1 - c0) >> 1) * (L.Wp >> 2);
+    const bool tm1 = ntl <= STACK_WAVES || cdiv(ntl, STACK_WAVES) < 2 * cdiv(ntl, 2 * STACK_WAVES);
+    if (rows_ok && L.Cs_in == 4 && L.KS == 2 && L.NT == 1) stack_layer_rows<1, 4, true, 2>(ROWS_ARGS);
+    else if (rows_ok && L.Cs_in == 4 && L.KS == 2 && L.NT == 2) stack_layer_rows<2, 2, true, 2>(ROWS_ARGS);
+    else if (rows_ok && L.Cs_in != 4 && L.KS == 5 && L.NT == 2 && tm1) stack_layer_rows<2, 1, false, 5>(ROWS_ARGS);
+    else if (rows_ok && L.Cs_in != 4 && L.KS == 5 && L.NT == 2) stack_layer_rows<2, 2, false, 5>(ROWS_ARGS);
+    else if (rows_ok && L.Cs_in != 4 && L.KS == 9 && L.NT == 4 && tm1) stack_layer_rows<4, 1, false, 9>(ROWS_ARGS);
+    else if (rows_ok && L.Cs_in != 4 && L.KS == 9 && L.NT == 4) stack_layer_rows<4, 2, false, 9>(ROWS_ARGS);
+    else if (rows_ok && L.Cs_in != 4 && L.KS == 9 && L.NT == 2) stack_layer_rows<2, 2, false, 9>(ROWS_ARGS);
+    else if (L.Cs_in == 4) {
       switch (L.NT) {
         case 1: stack_layer_tm<1, true>(STACK_ARGS); break;
         case 2: stack_layer_tm<2, true>(STACK_ARGS); break;
@@ -302,7 +510,10 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       }
     }
 #undef STACK_ARGS
+#undef ROWS_ARGS
+    STACK_STAMP(3 + 4 * l);
     __syncthreads();
+    STACK_STAMP(4 + 4 * l);
     // owned stage rows (+ argmax codes) -> global, 16-byte stores
     if (!(A.dbg & 4)) {
       const int cch = L.Cs_out >> 3;
@@ -323,6 +534,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
         for (int i = tid; i < nb; i += STACK_THREADS) gc[i] = lc[i];
       }
     }
+    STACK_STAMP(5 + 4 * l);
     // (no barrier: the next layer writes `codes` / the other buffer only after its own)
   }
 }

@@ -78,8 +78,9 @@ __device__ __forceinline__ void gather_block(const GatherArgs& a, const StepStat
 // Each descriptor owns a contiguous range of workgroups; a workgroup covers E = 256/tpe
 // consecutive elements: thread t -> element t % E (consecutive lanes read consecutive
 // addresses of one slab: coalesced) and split-lane t / E (the tpe split-lanes of an
-// element sum interleaved subsets of the S slabs with independent unrolled loads).  The tpe
-// partials are combined through LDS in a fixed order -> bitwise reproducible.
+// element sum interleaved subsets of <= 4 of the S slabs, loads all in flight: the
+// reduction is one memory round trip deep however many slabs there are).  The tpe
+// partials are combined by a fixed-order LDS tree -> bitwise reproducible.
 // Returns true on the thread that holds the final sum of element `dst` (in `val`).
 __device__ __forceinline__ bool slab_reduce_elem(const RedTable& tab, float* red, int& dst, float& val) {
   int di = 0;
@@ -109,28 +110,35 @@ __device__ __forceinline__ bool slab_reduce_elem(const RedTable& tab, float* red
     }
     const float* p = d.slab + src;
     const size_t st = (size_t)d.stride_s;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    // 8 independent loads per round (all issued before the first add), fixed summation order
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int s = lane;
-    for (; s + 3 * tpe < d.S; s += 4 * tpe) {
-      a0 += p[(size_t)s * st];
-      a1 += p[(size_t)(s + tpe) * st];
-      a2 += p[(size_t)(s + 2 * tpe) * st];
-      a3 += p[(size_t)(s + 3 * tpe) * st];
+    for (; s + 7 * tpe < d.S; s += 8 * tpe) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(s + u * tpe) * st];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += v[u];
     }
-    for (; s < d.S; s += tpe) a0 += p[(size_t)s * st];
-    acc = (a0 + a1) + (a2 + a3);
+#pragma unroll
+    for (int u = 0; u < 7; ++u)
+      if (s + u * tpe < d.S) a[u] += p[(size_t)(s + u * tpe) * st];
+    acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   }
   dst = d.dst_off + le;
   if (tpe == 1) {
     val = acc;
     return in;
   }
+  // fixed-order tree over the tpe split-lanes (bitwise reproducible)
   red[threadIdx.x] = acc;
   __syncthreads();
+  for (int off = tpe >> 1; off > 0; off >>= 1) {
+    if (lane < off) red[threadIdx.x] += red[threadIdx.x + off * E];
+    __syncthreads();
+  }
   if (lane != 0 || !in) return false;
-  float sum = 0.f;
-  for (int k = 0; k < tpe; ++k) sum += red[k * E + el];
-  val = sum;
+  val = red[el];
   return true;
 }
 

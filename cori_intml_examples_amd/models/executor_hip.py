@@ -851,12 +851,13 @@ class BatchPlan:
         layout = self._stack_layout(convs, rows, splits)
         if layout is None:
             return None
-        off_w, w_off, off_b0, off_b1, off_codes, lds = layout
+        off_w, w_off, off_b0, off_b1, off_codes, lds, off_bias = layout
         n = len(convs)
         a = K.ConvStackArgs()
         a.x = self.xb.data_ptr()
         a.B, a.n, a.seed, a.st = self.bs, n, ex.seed, ex.state.data_ptr()
         a.off_w, a.off_codes, a.lds_bytes = off_w, off_codes, lds
+        a.off_bias = off_bias
         a.dbg = int(os.environ.get("INTML_STACK_DBG", "0"))
         a.set_buf_offsets(off_b0, off_b1)
         a.splits = splits
@@ -926,7 +927,8 @@ class BatchPlan:
 
         n = len(convs)
         ntab = max((g.KS * 8 if g.Cs_in == 4 else g.KS * 4) for g in convs)
-        off_w = 32 + a16(4 * ntab)
+        off_bias = 32 + a16(4 * ntab)
+        off_w = off_bias + 4 * 64 * self.ex.K.MAX_STACK      # biases [layer][64] fp32
         w_off, welems = [], 0
         for g in convs:
             w_off.append(welems)
@@ -947,7 +949,7 @@ class BatchPlan:
         lds = off_codes + a16(codes)
         if lds > self.LDS_LIMIT:
             return None
-        return off_w, w_off, off_b0, off_b1, off_codes, lds
+        return off_w, w_off, off_b0, off_b1, off_codes, lds, off_bias
 
     @staticmethod
     def _wide(Cs_in: int, KS: int, NT: int) -> bool:
@@ -1180,9 +1182,10 @@ class BatchPlan:
         inserts = []                       # (launch index to insert after, bucket)
         for k, bg in enumerate(bucket_groups):
             tab = K.RedTable()
-            for i in bg:
-                for d in self.red_groups[i][2]:
-                    tab.add(*d)
+            # longest reductions (most slabs) first: their workgroups dispatch first and their
+            # memory round trips overlap the many short ones instead of trailing the launch
+            for d in sorted((d for i in bg for d in self.red_groups[i][2]), key=lambda d: -d[2]):
+                tab.add(*d)
             lo = min(self.red_groups[i][0] for i in bg)
             hi = max(self.red_groups[i][1] for i in bg)
             self.bucket_tables.append((lo, hi, tab))
