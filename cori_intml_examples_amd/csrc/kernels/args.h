@@ -116,6 +116,7 @@ struct WgradArgs {
   // when it applies: 8 n-tiles per workgroup, unpooled dY)
   const bf16* zero = nullptr;
   int dbg = 0;   // ablation (timing only): 1 skip staging, 2 skip MFMA, 4 skip slab stores
+  unsigned long long* ts = nullptr;   // diagnostics: per-workgroup [start, end] wall clock (null = off)
 };
 
 // Dense forward, split-K partial products: part[s][m][n]

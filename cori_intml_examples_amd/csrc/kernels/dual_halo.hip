@@ -10,49 +10,10 @@
 // The LDS request is the max of the two bodies' needs.
 #include <algorithm>
 
-#include "conv_halo_body.h"
-#include "wgrad_halo_body.h"
+#include "dual_halo_body.h"
 
 size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc);
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT);
-
-template <int NTC, int MTW, int NTT>
-__global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, const WgradArgs wa, const int MT,
-                                                        const int n_w, const int wgx, const int wgy, const int cgx) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TM = NTC >= 8 ? 2 : 4;
-  int id = blockIdx.x;
-  if (id < n_w) {
-    const int bx = id % wgx;
-    id /= wgx;
-    wgrad_halo_body<MTW, NTT, false, true>(wa, MT, bx, id % wgy, id / wgy, smem);
-  } else {
-    id -= n_w;
-    conv_halo_body<NTC, TM, 8, false>(ca, id % cgx, id / cgx, smem);
-  }
-}
-
-template <int NTC, int MTW, int NTT>
-static void dual_t(const ConvMMArgs& ca, const WgradArgs& wa, int MT, dim3 wg, int cgx, int cgy, size_t lds,
-                   hipStream_t s) {
-  auto k = dual_halo_kernel<NTC, MTW, NTT>;
-  if (lds > 65536) hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const int n_w = wg.x * wg.y * wg.z;
-  hipLaunchKernelGGL(k, dim3(n_w + cgx * cgy), dim3(256), lds, s, ca, wa, MT, n_w, (int)wg.x, (int)wg.y, cgx);
-}
-
-template <int NTC>
-static bool dual_w(const ConvMMArgs& ca, const WgradArgs& wa, int MT, int NTT, int mtw, dim3 wg, int cgx, int cgy,
-                   size_t lds, hipStream_t s) {
-#define C(M_, N_)                                                      \
-  if (mtw <= M_ && NTT == N_) {                                        \
-    dual_t<NTC, M_, N_>(ca, wa, MT, wg, cgx, cgy, lds, s);             \
-    return true;                                                       \
-  }
-  C(1, 1) C(2, 1) C(4, 1) C(1, 2) C(2, 2) C(4, 2) C(1, 4) C(2, 4) C(4, 4) C(1, 8) C(2, 8)
-#undef C
-  return false;
-}
 
 // Returns false (nothing launched) when the pair is not a supported combination; the caller
 // then launches the two kernels separately.
@@ -65,11 +26,24 @@ bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT
   const int mtw = (MT + (wa.bslab ? 1 : 0) + 3) / 4;
   const size_t lds = std::max(conv_halo_lds_bytes(ca, ntc), wgrad_halo_lds_bytes(wa, MT, NTT));
   if (lds > 160 * 1024) return false;
+  // dgrad m-tiles per wave per pass: the TM in {4, 2} that minimises the busiest wave's
+  // tile count over the block (ties -> larger TM: more fragment reuse); TM = 1 only when
+  // the block has <= 4 tiles (measured: TM 1 loses its fragment reuse on longer blocks)
+  const int rows = std::min(ca.R, ca.Ho);
+  const int ntiles = ca.pool ? ((rows / 2) * ca.Wp + 3) / 4 : (rows * ca.Wo + 15) / 16;
+  int tm = ntc >= 8 ? 2 : 4, best = 1 << 30;
+  for (int t : {4, 2, 1}) {
+    if (ntc >= 8 && t == 4) continue;
+    if (ntc > 2 && t != (ntc >= 8 ? 2 : 4)) continue;
+    if (t == 1 && ntiles > 4) continue;
+    const int load = t * ((ntiles + 4 * t - 1) / (4 * t));   // tiles of the busiest wave
+    if (load < best) { best = load; tm = t; }
+  }
   switch (ntc) {
-    case 1: return dual_w<1>(ca, wa, MT, NTT, mtw, wg, cgx, cgy, lds, s);
-    case 2: return dual_w<2>(ca, wa, MT, NTT, mtw, wg, cgx, cgy, lds, s);
-    case 4: return dual_w<4>(ca, wa, MT, NTT, mtw, wg, cgx, cgy, lds, s);
-    case 8: return dual_w<8>(ca, wa, MT, NTT, mtw, wg, cgx, cgy, lds, s);
+    case 1: return dual_launch_n1(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, s);
+    case 2: return dual_launch_n2(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, s);
+    case 4: return dual_launch_n4(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, s);
+    case 8: return dual_launch_n8(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, s);
   }
   return false;
 }

@@ -1,0 +1,62 @@
+// Kernel template + launch dispatch of the dual (wgrad + dgrad) backward launch, shared by
+// the per-NTC translation units dual_halo_n*.hip (split so hipcc builds them in parallel).
+#pragma once
+#include "conv_halo_body.h"
+#include "wgrad_halo_body.h"
+
+template <int NTC, int MTW, int NTT, int TM>
+__global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, const WgradArgs wa, const int MT,
+                                                        const int n_w, const int wgx, const int wgy, const int cgx) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int id = blockIdx.x;
+  if (wa.ts && threadIdx.x == 0) wa.ts[2 * blockIdx.x] = wall_clock64();
+  if (id < n_w) {
+    const int bx = id % wgx;
+    id /= wgx;
+    wgrad_halo_body<MTW, NTT, false, true>(wa, MT, bx, id % wgy, id / wgy, smem);
+  } else {
+    id -= n_w;
+    conv_halo_body<NTC, TM, 8, false>(ca, id % cgx, id / cgx, smem);
+  }
+  if (wa.ts) {
+    __syncthreads();
+    if (threadIdx.x == 0) wa.ts[2 * blockIdx.x + 1] = wall_clock64();
+  }
+}
+
+template <int NTC, int MTW, int NTT, int TM>
+static void dual_t(const ConvMMArgs& ca, const WgradArgs& wa, int MT, dim3 wg, int cgx, int cgy, size_t lds,
+                   hipStream_t s) {
+  auto k = dual_halo_kernel<NTC, MTW, NTT, TM>;
+  if (lds > 65536) hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const int n_w = wg.x * wg.y * wg.z;
+  hipLaunchKernelGGL(k, dim3(n_w + cgx * cgy), dim3(256), lds, s, ca, wa, MT, n_w, (int)wg.x, (int)wg.y, cgx);
+}
+
+// tm: m-tiles per wave per pass of the dgrad body (TM_DEFAULT, or 1 / 2 for NTC <= 2 when
+// that evens out the four waves' tile counts on small row blocks)
+template <int NTC>
+static bool dual_w(const ConvMMArgs& ca, const WgradArgs& wa, int MT, int NTT, int mtw, int tm, dim3 wg, int cgx,
+                   int cgy, size_t lds, hipStream_t s) {
+  constexpr int TMD = NTC >= 8 ? 2 : 4;
+#define C(M_, N_)                                                          \
+  if (mtw <= M_ && NTT == N_) {                                            \
+    if constexpr (NTC <= 2) {                                              \
+      if (tm == 1) { dual_t<NTC, M_, N_, 1>(ca, wa, MT, wg, cgx, cgy, lds, s); return true; } \
+      if (tm == 2) { dual_t<NTC, M_, N_, 2>(ca, wa, MT, wg, cgx, cgy, lds, s); return true; } \
+    }                                                                      \
+    dual_t<NTC, M_, N_, TMD>(ca, wa, MT, wg, cgx, cgy, lds, s);            \
+    return true;                                                           \
+  }
+  C(1, 1) C(2, 1) C(4, 1) C(1, 2) C(2, 2) C(4, 2) C(1, 4) C(2, 4) C(4, 4) C(1, 8) C(2, 8)
+#undef C
+  return false;
+}
+
+#define DUAL_N_DECL(N)                                                                                        \
+  bool dual_launch_n##N(const ConvMMArgs& ca, const WgradArgs& wa, int MT, int NTT, int mtw, int tm, dim3 wg, \
+                        int cgx, int cgy, size_t lds, hipStream_t s)
+DUAL_N_DECL(1);
+DUAL_N_DECL(2);
+DUAL_N_DECL(4);
+DUAL_N_DECL(8);

@@ -16,7 +16,13 @@
 template <int MTW, int NTT, bool CS4, bool PIPE>
 __global__ __launch_bounds__(256) void wgrad_halo_kernel(const WgradArgs a, const int MT) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const size_t lin = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
+  if (a.ts && threadIdx.x == 0) a.ts[2 * lin] = wall_clock64();
   wgrad_halo_body<MTW, NTT, CS4, PIPE>(a, MT, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  if (a.ts) {
+    __syncthreads();
+    if (threadIdx.x == 0) a.ts[2 * lin + 1] = wall_clock64();
+  }
 }
 
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT) {

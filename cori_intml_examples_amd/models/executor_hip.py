@@ -818,7 +818,7 @@ class BatchPlan:
                 if dual:
                     # one launch for the layer's wgrad and dgrad (independent GEMMs sharing dY):
                     # replaces the wgrad launch in place (its slabs are final after it)
-                    ntc = self._halo_cfg(a, g.NTd, False)
+                    ntc = self._halo_cfg(a, g.NTd, False, dual=True)
                     dname = "wgrad_dgrad_conv%d" % g.i
                     self.launches[w_at] = (dname, lambda s, a=a, n=ntc, w=wa, c=cfg: self._dual(a, n, w, c, s), "main")
                 else:
@@ -987,8 +987,12 @@ class BatchPlan:
             K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
             K.conv_halo(a, ntc, s)
 
-    def _halo_cfg(self, a, NT, pool):
-        """Pick n-tiles per workgroup (weight LDS slice) and R output rows per block."""
+    def _halo_cfg(self, a, NT, pool, dual=False):
+        """Pick n-tiles per workgroup (weight LDS slice) and R output rows per block: the
+        largest block that still leaves >= `want` workgroups (a dgrad co-scheduled with its
+        wgrad in one launch wants fewer, longer workgroups: each stages the whole weight
+        slice, and the launch should fit the CUs in one wave)."""
+        want = int(os.environ.get("INTML_DGRAD_MIN_WGS" if dual else "INTML_HALO_MIN_WGS", "512"))
         KS = a.KS
         ntc = 8
         while ntc > 1 and (ntc > NT or KS * ntc > 64):
@@ -1006,8 +1010,8 @@ class BatchPlan:
             halo = ((R - 1) * a.stride + a.KH) * W_in * a.Cs_in * 2
             if halo + KS * ntc * 1024 > 80 * 1024:
                 break
-            if a.B * cdiv(Ho, R) * gy >= 512:
-                best = R          # largest block that still leaves >= 512 workgroups
+            if a.B * cdiv(Ho, R) * gy >= want:
+                best = R          # largest block that still leaves >= `want` workgroups
         a.R = best
         lds = K_lds = self.ex.K.conv_halo_lds_bytes(a, ntc)
         if lds > 150 * 1024:

@@ -1,0 +1,69 @@
+"""Per-workgroup start/end (wall clock) of the conv backward launches of the RPV B=128 step:
+the two dual (wgrad + dgrad) launches and the first conv's wgrad.  Shows the launch config,
+and for the wgrad and dgrad workgroups separately: start spread, duration, last end."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from cori_intml_examples_amd.apps import zoo
+
+os.environ["INTML_GRAPHS"] = "0"
+dev = torch.device("cuda", 0)
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+model = zoo.rpv_cnn((64, 64, 3), conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.2, optimizer="Adam",
+                    lr=1e-3, device=dev)
+ex = model._executor
+ex.use_graphs = False
+rs = np.random.RandomState(0)
+d = ex.upload(rs.rand(B * 4, 64, 64, 3).astype(np.float32), (rs.rand(B * 4) > 0.5).astype(np.float32))
+ex.train_step(d, torch.arange(d.n, device=dev), 0, B)
+torch.cuda.synchronize()
+bp = ex._plans[(B, "train")]
+s = torch.cuda.current_stream().cuda_stream
+
+
+def cdiv(a, b):
+    return (a + b - 1) // b
+
+
+def stats(v):
+    return "med %6.2f p90 %6.2f max %6.2f" % (np.median(v), np.percentile(v, 90), v.max())
+
+
+for name, fn, *_ in bp.launches:
+    if not (name.startswith("wgrad_dgrad") or name.startswith("wgrad_conv")):
+        continue
+    dfl = fn.__defaults__
+    if name.startswith("wgrad_dgrad"):
+        ca, ntc, wa, cfg = dfl
+    else:
+        ca, ntc, (wa, cfg) = None, None, dfl
+    MT, NTT, S = cfg
+    n_w = S * cdiv(wa.NT, NTT) * cdiv(wa.Ktiles, MT)
+    n_c = 0
+    if ca is not None:
+        n_c = ca.B * cdiv(ca.Ho, ca.R) * cdiv(ca.NT, ntc)
+    ts = torch.zeros(2 * (n_w + n_c), dtype=torch.int64, device=dev)
+    wa.ts = ts.data_ptr()
+    for _ in range(10):
+        fn(s)
+    torch.cuda.synchronize()
+    wa.ts = 0
+    t = ts.view(-1, 2).cpu().numpy().astype(np.float64) * 0.01
+    t0 = t[:, 0].min()
+    st, en = t[:, 0] - t0, t[:, 1] - t0
+    du = en - st
+    print("%s: wgrad R=%d bps=%d MT=%d NTT=%d S=%d Ktiles=%d NT=%d -> %d WGs" % (
+        name, wa.R, wa.blocks_per_split, MT, NTT, S, wa.Ktiles, wa.NT, n_w), end="")
+    if ca is not None:
+        print("; dgrad R=%d ntc=%d KS=%d NT=%d Ho=%d Wo=%d -> %d WGs" % (ca.R, ntc, ca.KS, ca.NT, ca.Ho, ca.Wo, n_c))
+    else:
+        print()
+    print("   span %.2f us" % en.max())
+    for lab, sl in (("wgrad", slice(0, n_w)), ("dgrad", slice(n_w, n_w + n_c))):
+        if sl.stop <= sl.start:
+            continue
+        print("   %s start %s | dur %s | end %s" % (lab, stats(st[sl]), stats(du[sl]), stats(en[sl])))
