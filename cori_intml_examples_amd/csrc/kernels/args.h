@@ -52,7 +52,9 @@ struct ConvMMArgs {
   // >= 16 zero bytes in global memory: source of padded / out-of-range rows for the LDS-DMA
   // conv_tile path (set => that path is used when there is no unpool-on-load input)
   const bf16* zero = nullptr;
-  int dbg = 0;   // ablation (timing only, wrong results): 1 skip staging, 2 skip MFMA, 4 skip stores
+  int dbg = 0;   // ablation (timing only, wrong results): 1 skip staging, 2 skip MFMA, 4 skip stores,
+                 // 8 skip the weight staging only; 16 = per-pixel unpool staging (A/B, exact)
+  unsigned long long* ts = nullptr;   // diagnostics: [grid block][8] phase stamps, wave 0 lane 0 (null = off)
 };
 
 // Layer-fused forward of a conv stack (conv_stack.hip): one workgroup per image, all

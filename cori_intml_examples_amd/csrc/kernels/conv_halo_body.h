@@ -6,6 +6,9 @@
 
 // NTC n-tiles of the weight slice, TM m-tiles per wave per pass (each A fragment feeds NTC
 // MFMAs and each weight fragment TM), KCH k-steps per batch of independent reads.
+#define HALO_STAMP(i)                                                                \
+  if (a.ts && threadIdx.x == 0) a.ts[(size_t)blockIdx.x * 8 + (i)] = wall_clock64();
+
 template <int NTC, int TM, int KCH, bool CS4>
 __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx, const int by, char* smem) {
   const int KS = a.KS, R = a.R, s = a.stride, dil = a.in_dil, Cs = a.Cs_in;
@@ -23,10 +26,40 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
   const int oy0 = (bx - b * nrb) * R;
   const int nt0 = by * NTC;
 
+  HALO_STAMP(0);
   if (tid < 8) reinterpret_cast<uint32_t*>(zl)[tid] = 0u;
   const bool dbg_stage = !(a.dbg & 1), dbg_mfma = !(a.dbg & 2), dbg_store = !(a.dbg & 4);
+  // input halo geometry (staged after the weights: issuing the halo's HBM loads first was
+  // measured 3 us slower -- the weights' LDS stores then wait behind them)
+  const int hcw = CS4 ? 4 : 8;
+  const int hcpp = Cs / hcw;
+  const int nch = R_in * W_in * hcpp;
+  const int yb = oy0 * s - a.pad_t, xb0 = -a.pad_l;
+  const bf16* xbase = a.in_code ? a.x + (size_t)b * a.in_pH * a.in_pW * Cs : a.x + (size_t)b * a.H * a.W * Cs;
+  const uint8_t* cbase = a.in_code ? a.in_code + (size_t)b * a.in_pH * a.in_pW * Cs : nullptr;
+  const FastDiv fcpp(hcpp), fwin(W_in);
+  auto coords = [&](int i, int& c, int& iy, int& ix) -> bool {
+    const int pix = fcpp.div(i);
+    c = (i - pix * hcpp) * hcw;
+    const int r = fwin.div(pix);
+    iy = yb + r;
+    ix = xb0 + (pix - r * W_in);
+    bool ok = iy >= 0 && ix >= 0;
+    if (dil > 1) {
+      ok = ok && (iy % dil == 0) && (ix % dil == 0);
+      iy /= dil;
+      ix /= dil;
+    }
+    return ok && iy < a.H && ix < a.W;
+  };
+  auto halo8 = [&](int i) {
+    int c, iy, ix;
+    const bool ok = coords(i, c, iy, ix);
+    if (cbase) return unpool_load8(xbase, cbase, a.in_pH, a.in_pW, Cs, iy, ix, c, ok);
+    return load_bf16x8_if(ok, xbase + ((size_t)iy * a.W + ix) * Cs + c, xbase);
+  };
   // weights -> LDS
-  if (dbg_stage) staged_copy<8, bf16x8>(
+  if (dbg_stage && !(a.dbg & 8)) staged_copy<8, bf16x8>(
       KS * NTC * 64, tid, 256,
       [&](int i) {
         const int ks = i / (NTC * 64);   // compile-time power of two
@@ -36,6 +69,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
         return load_bf16x8_if(ok, a.wpk + ((size_t)(ks * a.NT + nt) * 64 + (rem & 63)) * 8, a.wpk);
       },
       [&](int i, const bf16x8& v) { *reinterpret_cast<bf16x8*>(wl + (size_t)i * 8) = v; });
+  HALO_STAMP(1);
   // k-chunk -> halo offset table
   {
     const int KHW = a.KH * a.KW;
@@ -53,27 +87,6 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
   }
   // input halo -> LDS
   if (dbg_stage) {
-    const int cw = CS4 ? 4 : 8;
-    const int cpp = Cs / cw;
-    const int nch = R_in * W_in * cpp;
-    const int yb = oy0 * s - a.pad_t, xb0 = -a.pad_l;
-    const bf16* xbase = a.in_code ? a.x + (size_t)b * a.in_pH * a.in_pW * Cs : a.x + (size_t)b * a.H * a.W * Cs;
-    const uint8_t* cbase = a.in_code ? a.in_code + (size_t)b * a.in_pH * a.in_pW * Cs : nullptr;
-    const FastDiv fcpp(cpp), fwin(W_in);
-    auto coords = [&](int i, int& c, int& iy, int& ix) -> bool {
-      const int pix = fcpp.div(i);
-      c = (i - pix * cpp) * cw;
-      const int r = fwin.div(pix);
-      iy = yb + r;
-      ix = xb0 + (pix - r * W_in);
-      bool ok = iy >= 0 && ix >= 0;
-      if (dil > 1) {
-        ok = ok && (iy % dil == 0) && (ix % dil == 0);
-        iy /= dil;
-        ix /= dil;
-      }
-      return ok && iy < a.H && ix < a.W;
-    };
     if (CS4) {
       staged_copy<8, bf16x4>(
           nch, tid, 256,
@@ -83,19 +96,72 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
             return load_bf16x4_if(ok, xbase + ((size_t)iy * a.W + ix) * 4, xbase);
           },
           [&](int i, const bf16x4& v) { *reinterpret_cast<bf16x4*>(xl + (size_t)i * 4) = v; });
+    } else if (cbase && dil == 1 && !(a.dbg & 16)) {
+      // Pooled input (dY = unpool(dP, codes)): load each pooled chunk ONCE and expand it into
+      // the (up to) four full-resolution halo pixels of its window -- a quarter of the
+      // global loads of rebuilding every pixel from its window (unpool_load8 per pixel).
+      const int Ha = 2 * a.in_pH, Wa = 2 * a.in_pW;
+      // halo pixels outside the pooled area (padding, odd edge) hold zeros
+      for (int i = tid; i < nch; i += 256) {
+        const int pix = fcpp.div(i);
+        const int r = fwin.div(pix);
+        const int y = yb + r, x = xb0 + (pix - r * W_in);
+        if (y < 0 || x < 0 || y >= Ha || x >= Wa) *reinterpret_cast<bf16x8*>(xl + (size_t)i * 8) = zero_bf16x8();
+      }
+      const int y_lo = max(yb, 0), y_hi = min(yb + R_in, Ha);
+      const int x_lo = max(xb0, 0), x_hi = min(xb0 + W_in, Wa);
+      if (y_lo < y_hi && x_lo < x_hi) {
+        const int py0 = y_lo >> 1, npy = ((y_hi - 1) >> 1) - py0 + 1;
+        const int px0 = x_lo >> 1, npx = ((x_hi - 1) >> 1) - px0 + 1;
+        const int nq = npy * npx * hcpp;
+        const FastDiv fnpx(npx);
+        constexpr int UQ = 4;
+        for (int q0 = tid; q0 < nq; q0 += 256 * UQ) {
+          uint4 raw[UQ];
+          uint2 cw[UQ];
+          int qy[UQ], qx[UQ], qc[UQ];
+#pragma unroll
+          for (int u = 0; u < UQ; ++u) {   // branch-free: clamped index, always loaded
+            const int q = min(q0 + u * 256, nq - 1);
+            const int pp = fcpp.div(q);
+            qc[u] = (q - pp * hcpp) * 8;
+            const int ry = fnpx.div(pp);
+            qy[u] = py0 + ry;
+            qx[u] = px0 + (pp - ry * npx);
+            const size_t o = ((size_t)qy[u] * a.in_pW + qx[u]) * Cs + qc[u];
+            raw[u] = *reinterpret_cast<const uint4*>(xbase + o);
+            cw[u] = *reinterpret_cast<const uint2*>(cbase + o);
+          }
+#pragma unroll
+          for (int u = 0; u < UQ; ++u) {
+            if (q0 + u * 256 >= nq) break;
+#pragma unroll
+            for (int pos = 0; pos < 4; ++pos) {
+              const int y = 2 * qy[u] + (pos >> 1), x = 2 * qx[u] + (pos & 1);
+              if (y < y_lo || y >= y_hi || x < x_lo || x >= x_hi) continue;
+              uint32_t m[4];
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const uint32_t w = h ? cw[u].y : cw[u].x;
+                m[2 * h] = (((w & 0xFF) == (uint32_t)pos) ? 0x0000FFFFu : 0u) |
+                           ((((w >> 8) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
+                m[2 * h + 1] = ((((w >> 16) & 0xFF) == (uint32_t)pos) ? 0x0000FFFFu : 0u) |
+                               ((((w >> 24) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
+              }
+              const uint4 v = {raw[u].x & m[0], raw[u].y & m[1], raw[u].z & m[2], raw[u].w & m[3]};
+              *reinterpret_cast<uint4*>(xl + ((size_t)((y - yb) * W_in + (x - xb0)) * Cs + qc[u])) = v;
+            }
+          }
+        }
+      }
     } else {
       staged_copy<8, bf16x8>(
-          nch, tid, 256,
-          [&](int i) {
-            int c, iy, ix;
-            const bool ok = coords(i, c, iy, ix);
-            if (cbase) return unpool_load8(xbase, cbase, a.in_pH, a.in_pW, Cs, iy, ix, c, ok);
-            return load_bf16x8_if(ok, xbase + ((size_t)iy * a.W + ix) * Cs + c, xbase);
-          },
-          [&](int i, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + (size_t)i * 8) = v; });
+          nch, tid, 256, halo8, [&](int i, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + (size_t)i * 8) = v; });
     }
   }
+  HALO_STAMP(2);
   __syncthreads();
+  HALO_STAMP(3);
 
   const int wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
   const int rows = min(R, a.Ho - oy0);
@@ -174,6 +240,10 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
       }
     }
 
+    if (tb == 0) {
+      asm volatile("" ::"v"(acc[0][0][0]));
+      HALO_STAMP(4);
+    }
     if (!dbg_store) {
 #pragma unroll
       for (int t = 0; t < TM; ++t)
@@ -277,6 +347,8 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
       }
       __builtin_amdgcn_wave_barrier();
     }
+    if (tb == 0) HALO_STAMP(5);
   }
+  HALO_STAMP(6);
 }
 

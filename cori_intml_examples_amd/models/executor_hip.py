@@ -992,9 +992,11 @@ class BatchPlan:
         largest block that still leaves >= `want` workgroups (a dgrad co-scheduled with its
         wgrad in one launch wants fewer, longer workgroups: each stages the whole weight
         slice, and the launch should fit the CUs in one wave)."""
-        want = int(os.environ.get("INTML_DGRAD_MIN_WGS" if dual else "INTML_HALO_MIN_WGS", "512"))
+        want = int(os.environ.get("INTML_DGRAD_MIN_WGS", "256") if dual else os.environ.get("INTML_HALO_MIN_WGS", "512"))
         KS = a.KS
-        ntc = 8
+        # co-scheduled dgrad: one n-tile per workgroup and whole-image blocks (measured on the
+        # RPV stack: each workgroup stages half the weights, the launch fits the CUs in one wave)
+        ntc = int(os.environ.get("INTML_DGRAD_NTC", "1")) if dual else 8
         while ntc > 1 and (ntc > NT or KS * ntc > 64):
             ntc //= 2
         if KS * ntc > 96:

@@ -48,10 +48,20 @@ for name, fn, *_ in bp.launches:
         n_c = ca.B * cdiv(ca.Ho, ca.R) * cdiv(ca.NT, ntc)
     ts = torch.zeros(2 * (n_w + n_c), dtype=torch.int64, device=dev)
     wa.ts = ts.data_ptr()
+    ph = None
+    if ca is not None:
+        ph = torch.zeros(8 * (n_w + n_c), dtype=torch.int64, device=dev)
+        ca.ts = ph.data_ptr()
     for _ in range(10):
         fn(s)
     torch.cuda.synchronize()
     wa.ts = 0
+    if ca is not None:
+        ca.ts = 0
+        p = ph.view(-1, 8).cpu().numpy().astype(np.float64)[n_w:] * 0.01
+        labels = ["weights staged", "halo staged", "barrier", "1st pass MFMA", "1st pass epilogue", "wave-0 done"]
+        print("   dgrad phases (wave 0, median us):", ", ".join(
+            "%s +%.2f" % (lab, np.median(p[:, i + 1] - p[:, i])) for i, lab in enumerate(labels)))
     t = ts.view(-1, 2).cpu().numpy().astype(np.float64) * 0.01
     t0 = t[:, 0].min()
     st, en = t[:, 0] - t0, t[:, 1] - t0
@@ -67,3 +77,29 @@ for name, fn, *_ in bp.launches:
         if sl.stop <= sl.start:
             continue
         print("   %s start %s | dur %s | end %s" % (lab, stats(st[sl]), stats(du[sl]), stats(en[sl])))
+
+# A/B of dgrad-body variants inside the dual launches (ca.dbg), interleaved rounds
+def _t(fn, reps=40):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        fn(s)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+variants = [int(v) for v in os.environ.get("AB_DBG", "0,16").split(",")]
+for name, fn, *_ in bp.launches:
+    if not name.startswith("wgrad_dgrad"):
+        continue
+    ca = fn.__defaults__[0]
+    res = {v: [] for v in variants}
+    for _ in range(5):
+        for v in variants:
+            ca.dbg = v
+            _t(fn, 5)
+            res[v].append(_t(fn))
+    ca.dbg = 0
+    print("%s A/B ca.dbg: %s" % (name, "  ".join("%d: %.2f" % (v, np.median(res[v])) for v in variants)))
