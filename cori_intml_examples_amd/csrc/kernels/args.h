@@ -117,7 +117,8 @@ struct WgradArgs {
   // >= 16 zero bytes: LDS-DMA source of padded rows (set => wgrad_tile uses the DMA path
   // when it applies: 8 n-tiles per workgroup, unpooled dY)
   const bf16* zero = nullptr;
-  int dbg = 0;   // ablation (timing only): 1 skip staging, 2 skip MFMA, 4 skip slab stores
+  int dbg = 0;   // ablation (timing only): 1 skip staging, 2 skip MFMA, 4 skip slab stores;
+                 // 16 = per-pixel unpool staging of pooled dY (A/B, exact)
   unsigned long long* ts = nullptr;   // diagnostics: per-workgroup [start, end] wall clock (null = off)
 };
 

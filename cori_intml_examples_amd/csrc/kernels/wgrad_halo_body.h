@@ -77,6 +77,44 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   const int nch_y = npb32 * cpr;                    // dY chunks per block
   const FastDiv fcpp(cpp), fwin(W_in), fcpr(cpr), fwo(a.Wo);
   const bool dbg_stage = !(a.dbg & 1);
+  // Pooled dY (dP + argmax codes) over whole even blocks: stage each pooled chunk ONCE and
+  // expand it into its 2x2 window's pixel rows in LDS (a quarter of the global loads of a
+  // per-pixel unpool; every LDS dY element of the block is written, zeros included).
+  const int hw = a.Wo >> 1;
+  // (pipelined path only: in the plain path its extra registers cost occupancy -- measured)
+  const bool pexp = PIPE && a.dy_code && !(a.dbg & 16) && (R & 1) == 0 && a.Ho % R == 0 && (a.Wo & 1) == 0 &&
+                    npb32 == npb && a.NT % NTT == 0 && a.NT * 16 <= a.Cs_dy && 2 * a.dHp >= a.Ho &&
+                    2 * a.dWp >= a.Wo;
+  const int nq = (R >> 1) * hw * cpr;               // pooled dY chunks per block
+  const FastDiv fhw(hw > 0 ? hw : 1);
+  // pooled chunk q of the block starting at conv row oy0 -> global dP offset (in elements)
+  auto pq_off = [&](int q, int b, int oy0) -> size_t {
+    const int p2 = fcpr.div(q), ch = q - p2 * cpr;
+    const int ry = fhw.div(p2);
+    const int wy = (oy0 >> 1) + ry, wx = p2 - ry * hw;
+    return (((size_t)b * a.dHp + wy) * a.dWp + wx) * a.Cs_dy + nt0 * 16 + ch * 8;
+  };
+  // write pooled chunk q (dP values v, codes cw) to the 4 pixels of its window
+  auto pq_store = [&](int q, const uint4& v, const uint2& cw) {
+    const int p2 = fcpr.div(q), ch = q - p2 * cpr;
+    const int ry = fhw.div(p2);
+    const int p00 = (2 * ry) * a.Wo + 2 * (p2 - ry * hw);
+#pragma unroll
+    for (int pos = 0; pos < 4; ++pos) {
+      uint32_t m[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t w = h ? cw.y : cw.x;
+        m[2 * h] = (((w & 0xFF) == (uint32_t)pos) ? 0x0000FFFFu : 0u) |
+                   ((((w >> 8) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
+        m[2 * h + 1] = ((((w >> 16) & 0xFF) == (uint32_t)pos) ? 0x0000FFFFu : 0u) |
+                       ((((w >> 24) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
+      }
+      const int p = p00 + (pos >> 1) * a.Wo + (pos & 1);
+      *reinterpret_cast<uint4*>(dyl + (size_t)p * ldb + ch * 8) =
+          uint4{v.x & m[0], v.y & m[1], v.z & m[2], v.w & m[3]};
+    }
+  };
 
   // MFMA reduction over the staged block's npix pixels
   auto mma_block = [&](const int npix) {
@@ -115,7 +153,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   // block blk's MFMAs run, and go to LDS after the barrier that retires blk's readers --
   // the staging loads' latency, not the MFMAs, was the per-block cost.
   constexpr int WH_PX = 4, WH_PY = 4;
-  if (PIPE && dbg_stage && nch_x <= WH_PX * 256 && nch_y <= WH_PY * 256) {
+  if (PIPE && dbg_stage && nch_x <= WH_PX * 256 && (pexp ? nq : nch_y) <= WH_PY * 256) {
     uint4 xr[WH_PX], yr[WH_PY];
     uint2 yc[WH_PY];
     uint32_t yp[WH_PY];
@@ -139,6 +177,15 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
           const uint4 v = *reinterpret_cast<const uint4*>(src);
           xr[u] = ok ? v : uint4{0u, 0u, 0u, 0u};
         }
+      }
+      if (pexp) {
+#pragma unroll
+        for (int u = 0; u < WH_PY; ++u) {
+          const size_t o = pq_off(min(tid + u * 256, nq - 1), b, oy0);
+          yr[u] = *reinterpret_cast<const uint4*>(a.dy + o);
+          yc[u] = *reinterpret_cast<const uint2*>(a.dy_code + o);
+        }
+        return;
       }
       const size_t boff = (size_t)b * a.dHp * a.dWp * a.Cs_dy;
 #pragma unroll
@@ -172,6 +219,12 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
         if (idx >= nch_x) continue;
         if (CS4) reinterpret_cast<uint2*>(xl)[idx] = uint2{xr[u].x, xr[u].y};
         else reinterpret_cast<uint4*>(xl)[idx] = xr[u];
+      }
+      if (pexp) {
+#pragma unroll
+        for (int u = 0; u < WH_PY; ++u)
+          if (tid + u * 256 < nq) pq_store(tid + u * 256, yr[u], yc[u]);
+        return;
       }
 #pragma unroll
       for (int u = 0; u < WH_PY; ++u) {
@@ -244,7 +297,22 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
               [&](int idx, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + (size_t)idx * 8) = v; });
         }
       }
-      if (dbg_stage) {   // dY rows (rebuilt from pooled dP + codes when the conv is pooled)
+      if (dbg_stage && pexp) {   // dY rows from pooled chunks, each loaded once
+        constexpr int UQ = 4;
+        for (int q0 = tid; q0 < nq; q0 += 256 * UQ) {
+          uint4 v[UQ];
+          uint2 cw[UQ];
+#pragma unroll
+          for (int u = 0; u < UQ; ++u) {
+            const size_t o = pq_off(min(q0 + u * 256, nq - 1), b, oy0);
+            v[u] = *reinterpret_cast<const uint4*>(a.dy + o);
+            cw[u] = *reinterpret_cast<const uint2*>(a.dy_code + o);
+          }
+#pragma unroll
+          for (int u = 0; u < UQ; ++u)
+            if (q0 + u * 256 < nq) pq_store(q0 + u * 256, v[u], cw[u]);
+        }
+      } else if (dbg_stage) {   // dY rows (rebuilt from pooled dP + codes when the conv is pooled)
         const size_t boff = (size_t)b * a.dHp * a.dWp * a.Cs_dy;
         staged_copy<8, bf16x8>(
             nch_y, tid, 256,

@@ -94,12 +94,14 @@ variants = [int(v) for v in os.environ.get("AB_DBG", "0,16").split(",")]
 for name, fn, *_ in bp.launches:
     if not name.startswith("wgrad_dgrad"):
         continue
-    ca = fn.__defaults__[0]
+    ca, wa = fn.__defaults__[0], fn.__defaults__[2]
     res = {v: [] for v in variants}
     for _ in range(5):
         for v in variants:
             ca.dbg = v
+            wa.dbg = v
             _t(fn, 5)
             res[v].append(_t(fn))
     ca.dbg = 0
-    print("%s A/B ca.dbg: %s" % (name, "  ".join("%d: %.2f" % (v, np.median(res[v])) for v in variants)))
+    wa.dbg = 0
+    print("%s A/B dbg (dgrad + wgrad): %s" % (name, "  ".join("%d: %.2f" % (v, np.median(res[v])) for v in variants)))
