@@ -18,7 +18,7 @@ void launch_wgrad_tile(const WgradArgs& a, int ntc, hipStream_t s);
 size_t wgrad_tile_lds_bytes(int ntc);
 void launch_wgrad_halo(const WgradArgs& a, int MT, int NTT, int splits, hipStream_t s);
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT);
-int head_rows_per_block();
+int head_rows_per_block(bool fused);
 int head_epi_max();
 void launch_wgrad(const WgradArgs& a, int ktw, int ntt, int splits, hipStream_t s);
 size_t wgrad_lds_bytes(int KT, int NTT);
@@ -240,7 +240,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wgrad_lds_bytes", &wgrad_lds_bytes);
   m.def("conv_halo_lds_bytes", &conv_halo_lds_bytes);
   m.def("wgrad_halo_lds_bytes", &wgrad_halo_lds_bytes);
-  m.def("head_rows_per_block", &head_rows_per_block);
+  m.def("head_rows_per_block", &head_rows_per_block, py::arg("fused") = false);
   m.def("conv_tile_lds_bytes", &conv_tile_lds_bytes);
   m.def("conv_tile", [](const ConvMMArgs& a, int ntc, uintptr_t s) {
     launch_conv_tile(a, ntc, S(s)); check_last("conv_tile"); });

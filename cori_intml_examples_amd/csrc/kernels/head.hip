@@ -39,19 +39,74 @@ __device__ __forceinline__ float dense_epi_value(const DenseEpiArgs& e, int m, i
   return v;
 }
 
+// One split group's partial sum of dense_epi_value (sg in 0..3), its <= 16 loads issued
+// together; same summation order as dense_epi_value (bit-identical).
+__device__ __forceinline__ float dense_epi_group(const DenseEpiArgs& e, int m, int n, int sg) {
+  const size_t stride = (size_t)e.M * e.ldp;
+  const float* p = e.part + (size_t)m * e.ldp + n;
+  float v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int sp = sg + 4 * j;
+    v[j] = p[(size_t)min(sp, e.splits - 1) * stride];
+  }
+  // dense_epi_value's loops over the preloaded values: pairs (s, s + 4) while s + 4 < splits,
+  // then the remaining s into a0
+  float a0 = 0.f, a1 = 0.f;
+  int jn = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (sg + 8 * i + 4 < e.splits) {
+      a0 += v[2 * i];
+      a1 += v[2 * i + 1];
+      jn = 2 * i + 2;
+    }
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj)
+    if (jj >= jn && sg + 4 * jj < e.splits) a0 += v[jj];
+  return a0 + a1;
+}
+
+template <int RB>
 __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
-  __shared__ float dz_s[HEAD_RB][16];
-  __shared__ float met[HEAD_RB][2];
-  __shared__ bf16 hs[HEAD_RB][HEAD_EPI_MAX];
+  __shared__ float dz_s[RB][16];
+  __shared__ float met[RB][2];
+  __shared__ bf16 hs[RB][HEAD_EPI_MAX];
+  __shared__ float red4[RB == 1 ? 4 : 1][RB == 1 ? HEAD_EPI_MAX : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int row0 = blockIdx.x * HEAD_RB;
+  const int row0 = blockIdx.x * RB;
   const int N = a.N;
   const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
-  const int row = row0 + wave;
+  const int rw = RB == 1 ? 0 : wave;                 // this wave's row slot
+  const bool row_wave = RB != 1 || wave == 0;        // RB == 1: wave 0 computes the row
+  const int row = row0 + rw;
   const bool fused = a.epi.part != nullptr;
-  if (fused) {   // previous dense layer's epilogue for this workgroup's rows
+  if (fused && RB == 1 && a.epi.splits <= 64) {
+    // one row per workgroup: the four split groups of every column in parallel (all their
+    // loads in flight), combined in dense_epi_value's fixed order
     const DenseEpiArgs& e = a.epi;
-    const int nr = min(HEAD_RB, a.M - row0);
+    for (int task = tid; task < 4 * e.Ns; task += 256) {
+      const int n = task % e.Ns, sg = task / e.Ns;
+      red4[sg][n] = n < e.N ? dense_epi_group(e, row0, n, sg) : 0.f;
+    }
+    __syncthreads();
+    for (int n = tid; n < e.Ns; n += 256) {
+      float v = 0.f;
+      if (n < e.N) {
+        v = (red4[0][n] + red4[1][n]) + (red4[2][n] + red4[3][n]);
+        if (e.bias) v += e.bias[n];
+        if (e.relu) v = fmaxf(v, 0.f);
+        if (e.drop_thr)
+          v = dropout_keep((uint32_t)(row0 * e.N + n), e.seed, e.stream_id, step, e.drop_thr) ? v * e.drop_scale : 0.f;
+      }
+      const bf16 hb = f2bf(v);
+      hs[0][n] = hb;
+      e.out[(size_t)row0 * e.Ns + n] = hb;     // saved activation (ReLU mask of the backward)
+    }
+    __syncthreads();
+  } else if (fused) {   // previous dense layer's epilogue for this workgroup's rows
+    const DenseEpiArgs& e = a.epi;
+    const int nr = min(RB, a.M - row0);
     for (int idx = tid; idx < nr * e.Ns; idx += 256) {
       const int rl = idx / e.Ns, n = idx - rl * e.Ns;
       const int m = row0 + rl;
@@ -74,11 +129,11 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   float z[16];
 #pragma unroll
   for (int n = 0; n < 16; ++n) z[n] = 0.f;
-  if (row < a.M) {
+  if (row < a.M && row_wave) {
     const bf16* hr = a.h + (size_t)row * a.Ks;
     for (int k = lane; k < a.K; k += 64) {
       const int kp = a.flat_C ? flat_keras_to_padded(k, a.flat_C, a.flat_Cs) : k;
-      const float hv = fused ? bf2f(hs[wave][kp]) : bf2f(hr[kp]);
+      const float hv = fused ? bf2f(hs[rw][kp]) : bf2f(hr[kp]);
       const float* wr = a.w + (size_t)k * N;
 #pragma unroll
       for (int n = 0; n < 16; ++n)
@@ -92,7 +147,7 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
       for (int off = 32; off > 0; off >>= 1) z[n] += __shfl_xor(z[n], off);
     }
   }
-  if (lane == 0) {
+  if (lane == 0 && row_wave) {
     float dz[16];
 #pragma unroll
     for (int n = 0; n < 16; ++n) dz[n] = 0.f;
@@ -155,12 +210,12 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
         }
       }
     }
-    for (int n = 0; n < 16; ++n) dz_s[wave][n] = dz[n] * a.inv_bs;
-    met[wave][0] = loss;
-    met[wave][1] = correct;
+    for (int n = 0; n < 16; ++n) dz_s[rw][n] = dz[n] * a.inv_bs;
+    met[rw][0] = loss;
+    met[rw][1] = correct;
   }
   __syncthreads();
-  const int rows_here = min(HEAD_RB, a.M - row0);
+  const int rows_here = min(RB, a.M - row0);
   if (tid == 0 && a.y && a.st) {
     float ls = 0.f, cs = 0.f;
     for (int r = 0; r < rows_here; ++r) { ls += met[r][0]; cs += met[r][1]; }
@@ -205,9 +260,12 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   }
 }
 
-void launch_head(const HeadArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(head_kernel, dim3((a.M + HEAD_RB - 1) / HEAD_RB), dim3(256), 0, s, a);
-}
+// Rows per workgroup: 4 (one wave per row), or 1 when the head also runs the previous dense
+// layer's split-K epilogue (a row per workgroup spreads that reduction over 128 workgroups)
+int head_rows_per_block(bool fused) { return fused ? 1 : HEAD_RB; }
 
-int head_rows_per_block() { return HEAD_RB; }
+void launch_head(const HeadArgs& a, hipStream_t s) {
+  if (a.epi.part != nullptr) hipLaunchKernelGGL(head_kernel<1>, dim3(a.M), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(head_kernel<HEAD_RB>, dim3((a.M + HEAD_RB - 1) / HEAD_RB), dim3(256), 0, s, a);
+}
 int head_epi_max() { return HEAD_EPI_MAX; }

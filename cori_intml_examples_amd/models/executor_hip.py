@@ -541,11 +541,12 @@ class BatchPlan:
             self.dense_part.append(z(splits, bs, g.NT * 16, dt=torch.float32))
             self.dense_dh.append(z(bs, g.Ns) if self.training else None)
         hd = ex.plan.head
-        self.head_blocks = cdiv(bs, K.head_rows_per_block())
+        self.head_blocks = cdiv(bs, K.head_rows_per_block(False))   # re-set below if the head fuses the epilogue
+        head_slab_blocks = cdiv(bs, K.head_rows_per_block(True))
         self.probs = z(bs, hd.N, dt=torch.float32) if mode == "predict" else None
         if self.training:
-            self.head_wslab = z(self.head_blocks, hd.K, hd.N, dt=torch.float32)
-            self.head_bslab = z(self.head_blocks, hd.N, dt=torch.float32)
+            self.head_wslab = z(head_slab_blocks, hd.K, hd.N, dt=torch.float32)
+            self.head_bslab = z(head_slab_blocks, hd.N, dt=torch.float32)
         self._build_args()
 
     # ---------------------------------------------------------------- helpers
@@ -677,10 +678,11 @@ class BatchPlan:
                 e.drop_scale = 1.0 / (1.0 - g.rate)
             e.seed, e.stream_id, e.st = ex.seed, g.stream, st_ptr
             if (g.j == len(ex.denses) - 1 and ex.head_src.kind == "dense" and g.Ns <= K.head_epi_max()
-                    and env_flag("INTML_FUSE_HEAD", False)):
-                # opt-in: measured slower at batch 128 (the head's 32 workgroups then serialise
-                # the split-K reduction the 256-workgroup epilogue spreads over the chip)
-                head_epi = e          # the head launch reduces this layer's partials itself
+                    and env_flag("INTML_FUSE_HEAD", True)):
+                # the head launch (one row per workgroup, the row's split groups in parallel)
+                # reduces this layer's partials itself: one kernel boundary fewer
+                head_epi = e
+                self.head_blocks = cdiv(bs, K.head_rows_per_block(True))
             else:
                 self.launches.append(("dense_epi%d" % g.j, lambda s, e=e: K.dense_epi(e, s)))
 
