@@ -203,7 +203,7 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
 // beyond the last tap points at the pixel itself -- finite activations times the pack's
 // zero rows -- instead of a zero buffer behind a select.  Same k order, rounding points,
 // argmax codes and dropout counters as stack_layer (bit-identical).
-template <int NT, int TM, bool CS4, int KS>
+template <int NT, int TM, bool CS4, int KS, bool FULL>
 __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                                  int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
                                                  int OW, LDS uint8_t* codes, const lbf16* wl, uint32_t step,
@@ -240,12 +240,20 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
     const int n = nt * 16 + r;
     bias[nt] = n < Cout ? lb[n] : 0.f;     // staged in LDS at kernel start
   }
+  // tile -> (pooled row, first window): scalar shift when tiles-per-row is a power of two
+  const bool tpow2 = (tpr & (tpr - 1)) == 0;
+  const int tsh = __builtin_ctz(tpr);
+  auto trow = [&](int tile) { return tpow2 ? tile >> tsh : tile / tpr; };
+  // epilogue lane constants: window g of the tile, channel r of n-tile 0
+  const int lo_g = g * Cso + r;
+  const uint32_t qlane = (uint32_t)g * (uint32_t)Cout + (uint32_t)r;
+  // FULL: Cso == Cout == NT * 16 (no padded channels): no per-lane channel guards
   for (int tb = wave * TM; tb < ntiles; tb += STACK_WAVES * TM) {
     int base[TM];
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
       const int tile = min(tb + t, ntiles - 1);   // duplicate of a valid tile: computed, not stored
-      const int pyl = tile / tpr, wx0 = (tile - pyl * tpr) * 4;
+      const int pyl = trow(tile), wx0 = (tile - pyl * tpr) * 4;
       base[t] = ((2 * pyl + roff) * Wi + 2 * wx0) * Cs + lane_px;
     }
     f32x4 acc[TM][NT];
@@ -290,9 +298,29 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
     for (int t = 0; t < TM; ++t) {
       const int tile = tb + t;
       if (tile >= ntiles) break;
-      const int pyl = tile / tpr, pxl = (tile - pyl * tpr) * 4 + g;
+      const int pyl = trow(tile), wx0 = (tile - pyl * tpr) * 4;
       const int orow = p0 + pyl - obase;
       const bool keep = orow >= 0 && orow < OH;
+      if (FULL) {   // scalar tile bases + lane constants: one add per address
+        const int ob = (orow * OW + wx0 + ol) * Cso + lo_g, cb = (pyl * Wp + wx0) * Cso + lo_g;
+        const uint32_t qt = (qb + (uint32_t)(pyl * Wp + wx0)) * (uint32_t)Cout + qlane;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          float best = -3.4e38f;
+          int code = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v = acc[t][nt][j] + bias[nt];
+            if (L.relu) v = fmaxf(v, 0.f);
+            if (v > best) { best = v; code = j; }
+          }
+          if (thr) best = dropout_keep(qt + (uint32_t)(nt * 16), seed, sid, step, thr) ? best * dscale : 0.f;
+          if (keep) outimg[ob + nt * 16] = f2bf(best);
+          codes[cb + nt * 16] = (uint8_t)code;
+        }
+        continue;
+      }
+      const int pxl = wx0 + g;
       const int oo = (orow * OW + pxl + ol) * Cso, co = (pyl * Wp + pxl) * Cso;
       const uint32_t qi = (qb + (uint32_t)(pyl * Wp + pxl)) * (uint32_t)Cout;
 #pragma unroll
@@ -487,13 +515,20 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     // TM = 1 when it evens out the waves' tile counts (few tiles per workgroup)
     const int ntl = ((c1 - c0) >> 1) * (L.Wp >> 2);
     const bool tm1 = ntl <= STACK_WAVES || cdiv(ntl, STACK_WAVES) < 2 * cdiv(ntl, 2 * STACK_WAVES);
-    if (rows_ok && L.Cs_in == 4 && L.KS == 2 && L.NT == 1) stack_layer_rows<1, 4, true, 2>(ROWS_ARGS);
-    else if (rows_ok && L.Cs_in == 4 && L.KS == 2 && L.NT == 2) stack_layer_rows<2, 2, true, 2>(ROWS_ARGS);
-    else if (rows_ok && L.Cs_in != 4 && L.KS == 5 && L.NT == 2 && tm1) stack_layer_rows<2, 1, false, 5>(ROWS_ARGS);
-    else if (rows_ok && L.Cs_in != 4 && L.KS == 5 && L.NT == 2) stack_layer_rows<2, 2, false, 5>(ROWS_ARGS);
-    else if (rows_ok && L.Cs_in != 4 && L.KS == 9 && L.NT == 4 && tm1) stack_layer_rows<4, 1, false, 9>(ROWS_ARGS);
-    else if (rows_ok && L.Cs_in != 4 && L.KS == 9 && L.NT == 4) stack_layer_rows<4, 2, false, 9>(ROWS_ARGS);
-    else if (rows_ok && L.Cs_in != 4 && L.KS == 9 && L.NT == 2) stack_layer_rows<2, 2, false, 9>(ROWS_ARGS);
+    const bool full = L.Cs_out == L.Cout && L.Cout == L.NT * 16;
+#define ROWS(NT_, TM_, CS4_, KS_)                                                   \
+  {                                                                                 \
+    if (full) stack_layer_rows<NT_, TM_, CS4_, KS_, true>(ROWS_ARGS);               \
+    else stack_layer_rows<NT_, TM_, CS4_, KS_, false>(ROWS_ARGS);                   \
+  }
+    if (rows_ok && L.Cs_in == 4 && L.KS == 2 && L.NT == 1) ROWS(1, 4, true, 2)
+    else if (rows_ok && L.Cs_in == 4 && L.KS == 2 && L.NT == 2) ROWS(2, 2, true, 2)
+    else if (rows_ok && L.Cs_in != 4 && L.KS == 5 && L.NT == 2 && tm1) ROWS(2, 1, false, 5)
+    else if (rows_ok && L.Cs_in != 4 && L.KS == 5 && L.NT == 2) ROWS(2, 2, false, 5)
+    else if (rows_ok && L.Cs_in != 4 && L.KS == 9 && L.NT == 4 && tm1) ROWS(4, 1, false, 9)
+    else if (rows_ok && L.Cs_in != 4 && L.KS == 9 && L.NT == 4) ROWS(4, 2, false, 9)
+    else if (rows_ok && L.Cs_in != 4 && L.KS == 9 && L.NT == 2) ROWS(2, 2, false, 9)
+#undef ROWS
     else if (L.Cs_in == 4) {
       switch (L.NT) {
         case 1: stack_layer_tm<1, true>(STACK_ARGS); break;

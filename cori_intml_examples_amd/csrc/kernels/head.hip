@@ -13,6 +13,7 @@
 
 #define HEAD_RB 4
 #define HEAD_EPI_MAX 1024   // widest previous dense whose epilogue the head absorbs
+#define HEAD_W_LDS 2048     // head weights staged in LDS up to this many floats
 
 // dense_epilogue_kernel's value for (m, n): the same 4-way interleaved split order
 // (bit-identical), then bias, ReLU, dropout.
@@ -73,7 +74,13 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   __shared__ float met[RB][2];
   __shared__ bf16 hs[RB][HEAD_EPI_MAX];
   __shared__ float red4[RB == 1 ? 4 : 1][RB == 1 ? HEAD_EPI_MAX : 1];
+  __shared__ float wsh[HEAD_W_LDS];      // head weights [K][N] when they fit (read twice below)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // head weights -> LDS first: their load overlaps the epilogue's partial-sum loads, and the
+  // logit dot and the dH back-projection then read LDS instead of two global round trips
+  const bool wlds = a.K * a.N <= HEAD_W_LDS;
+  if (wlds)
+    for (int i = tid; i < a.K * a.N; i += 256) wsh[i] = a.w[i];
   const int row0 = blockIdx.x * RB;
   const int N = a.N;
   const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
@@ -126,6 +133,7 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
     a.st->packs_stale = 0;
   }
 
+  if (!fused && wlds) __syncthreads();   // (the fused path's barriers already cover wsh)
   float z[16];
 #pragma unroll
   for (int n = 0; n < 16; ++n) z[n] = 0.f;
@@ -134,10 +142,9 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
     for (int k = lane; k < a.K; k += 64) {
       const int kp = a.flat_C ? flat_keras_to_padded(k, a.flat_C, a.flat_Cs) : k;
       const float hv = fused ? bf2f(hs[rw][kp]) : bf2f(hr[kp]);
-      const float* wr = a.w + (size_t)k * N;
 #pragma unroll
       for (int n = 0; n < 16; ++n)
-        if (n < N) z[n] += hv * wr[n];
+        if (n < N) z[n] += hv * (wlds ? wsh[k * N + n] : a.w[(size_t)k * N + n]);
     }
   }
 #pragma unroll
@@ -253,7 +260,22 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
       float gs = 0.f;
       if (c < t.pC) {
         const int k = (y * t.pW + x) * t.pC + c;
-        for (int n = 0; n < N; ++n) gs += dz_s[rl][n] * a.w[(size_t)k * N + n];
+        for (int n = 0; n < N; ++n) gs += dz_s[rl][n] * (wlds ? wsh[k * N + n] : a.w[(size_t)k * N + n]);
+      }
+      if (fused && t.prev_out == a.epi.out && t.pH == 1 && t.pW == 1) {
+        // the previous stage IS the fused dense layer: its saved output row is in LDS
+        if (c >= t.pCs) continue;
+        if (c >= t.pC) {
+          gs = 0.f;
+        } else {
+          if (t.drop_thr) {
+            const uint32_t idx = (uint32_t)((size_t)(row0 + rl) * t.pC + c);
+            gs = dropout_keep(idx, t.seed, t.stream_id, step, t.drop_thr) ? gs * t.drop_scale : 0.f;
+          }
+          if (t.prev_relu && !(bf2f(hs[rl][c]) > 0.f)) gs = 0.f;
+        }
+        t.dy[(size_t)(row0 + rl) * t.pCs + c] = f2bf(gs);
+        continue;
       }
       bwd_through_store(t, row0 + rl, y, x, c, gs, step);
     }

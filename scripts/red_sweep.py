@@ -55,3 +55,22 @@ for gi, (lo, hi, descs) in enumerate(bp.red_groups):
             t = timeit(lambda st, tab=tab: K.slab_reduce(ex.store.grad.data_ptr(), 0, 0, tab, st))
             row.append("%d:%.2f" % (tpe, t))
         print("grp%d type%d S=%d numel=%d  tpe:us  %s" % (gi, dsc[6], dsc[2], dsc[5], "  ".join(row)), flush=True)
+
+# fused reduce+optimizer launch over subsets of the descriptors
+descs = [d for (_, _, ds) in bp.red_groups for d in ds]
+oa = ex._optim_args(False, defer_pack=True)
+
+
+def table(sel):
+    tab = K.RedTable()
+    for d in sorted(sel, key=lambda d: -d[2]):
+        tab.add(*d)
+    return tab
+
+
+for label, sel in (("all", descs), ("no dense W", [d for d in descs if d[6] != 2]),
+                   ("dense W only", [d for d in descs if d[6] == 2]),
+                   ("conv W only", [d for d in descs if d[6] == 0])):
+    tab = table(sel)
+    t = timeit(lambda st, tab=tab: K.reduce_optim(ex.store.grad.data_ptr(), tab, oa, st))
+    print("reduce_optim [%s] %d WGs: %.2f us" % (label, tab.nblocks if hasattr(tab, "nblocks") else -1, t), flush=True)
