@@ -172,6 +172,7 @@ struct HeadArgs {
   // reduces the split-K partials of its rows itself (bias, ReLU, dropout), writes that
   // layer's bf16 output and uses it as h -- one launch instead of two
   DenseEpiArgs epi;
+  unsigned long long* ts = nullptr;   // diagnostics: [block][8] phase stamps (null = off)
 };
 
 struct GatherArgs {

@@ -109,7 +109,7 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(HeadArgs, h) RW(HeadArgs, M) RW(HeadArgs, K) RW(HeadArgs, Ks) RW(HeadArgs, N)
       RW(HeadArgs, flat_C) RW(HeadArgs, flat_Cs) PTR(HeadArgs, w) PTR(HeadArgs, bias) PTR(HeadArgs, y)
       RW(HeadArgs, act) RW(HeadArgs, training) RW(HeadArgs, inv_bs) PTR(HeadArgs, st) PTR(HeadArgs, probs)
-      PTR(HeadArgs, wslab) PTR(HeadArgs, bslab) RW(HeadArgs, bt) RW(HeadArgs, epi);
+      PTR(HeadArgs, wslab) PTR(HeadArgs, bslab) RW(HeadArgs, bt) RW(HeadArgs, epi) PTR(HeadArgs, ts);
 
   py::class_<GatherArgs>(m, "GatherArgs")
       .def(py::init<>())
@@ -230,7 +230,8 @@ PYBIND11_MODULE(_kernels, m) {
       py::arg("type"), py::arg("KH"), py::arg("KW"), py::arg("Cin"), py::arg("Cout"), py::arg("Cs"), py::arg("tpe") = -1);
 
   m.attr("STEP_STATE_BYTES") = (int)sizeof(StepState);
-  m.attr("STEP_STATE_METRICS_OFFSET") = (int)offsetof(StepState, metrics);
+  m.attr("STEP_STATE_METRICS_OFFSET") = (int)offsetof(StepState, metric_slots);
+  m.attr("STEP_STATE_METRIC_SLOTS") = 16;
   m.attr("STEP_STATE_MSCHED_OFFSET") = (int)offsetof(StepState, m_schedule);
   m.attr("STEP_STATE_LR_OFFSET") = (int)offsetof(StepState, lr);
   m.attr("STEP_STATE_WARM_OFFSET") = (int)offsetof(StepState, warm_t0);

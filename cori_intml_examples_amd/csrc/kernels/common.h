@@ -151,7 +151,7 @@ struct StepState {
   // metric accumulators as int64 fixed point (loss in units of 2^-32, correct/count exact):
   // integer atomics commute, so the epoch sums are bit-identical whatever order the head's
   // workgroups retire in (a float/double atomicAdd is order-dependent in its last bits)
-  long long metrics[4];  // loss_sum * 2^32, correct_sum, count, spare
+  long long metrics[4];  // (unused: see metric_slots)
   // bound dataset (host-written when the executor switches datasets, so captured graphs
   // are dataset-independent): x rows [n][R] bf16, targets [n][C] fp32, epoch permutation
   unsigned long long data_x, data_y, perm;
@@ -166,6 +166,9 @@ struct StepState {
   // inside multi-step graph replays.  warm_steps = 0: off.
   int warm_t0, warm_steps, warm_spe, warm_size;
   float warm_base, warm_epochs;
+  // metric accumulators spread over METRIC_SLOTS slots (workgroup b adds to slot b % 16):
+  // [slot][loss_sum * 2^32, correct_sum, count, spare]; the host sums the slots
+  long long metric_slots[16][4];
 };
 
 enum OptKind { OPT_SGD = 0, OPT_RMSPROP = 1, OPT_ADADELTA = 2, OPT_ADAM = 3, OPT_NADAM = 4 };

@@ -68,9 +68,12 @@ __device__ __forceinline__ float dense_epi_group(const DenseEpiArgs& e, int m, i
   return a0 + a1;
 }
 
-template <int RB>
+#define HEAD_STAMP(i)                                                                 \
+  if (a.ts && threadIdx.x == 0) a.ts[(size_t)blockIdx.x * 8 + (i)] = wall_clock64();
+
+template <int RB, int NM>
 __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
-  __shared__ float dz_s[RB][16];
+  __shared__ float dz_s[RB][NM];
   __shared__ float met[RB][2];
   __shared__ bf16 hs[RB][HEAD_EPI_MAX];
   __shared__ float red4[RB == 1 ? 4 : 1][RB == 1 ? HEAD_EPI_MAX : 1];
@@ -78,6 +81,7 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // head weights -> LDS first: their load overlaps the epilogue's partial-sum loads, and the
   // logit dot and the dH back-projection then read LDS instead of two global round trips
+  HEAD_STAMP(0);
   const bool wlds = a.K * a.N <= HEAD_W_LDS;
   if (wlds)
     for (int i = tid; i < a.K * a.N; i += 256) wsh[i] = a.w[i];
@@ -88,7 +92,17 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   const bool row_wave = RB != 1 || wave == 0;        // RB == 1: wave 0 computes the row
   const int row = row0 + rw;
   const bool fused = a.epi.part != nullptr;
-  if (fused && RB == 1 && a.epi.splits <= 64) {
+  // the rows' targets and the bias too (read by the serial loss code below)
+  __shared__ float ysh[RB][16], bsh[16];
+  if (tid < 16) bsh[tid] = (a.bias && tid < a.N) ? a.bias[tid] : 0.f;
+  if (tid >= 64 && tid < 64 + RB * 16) {
+    const int rl = (tid - 64) >> 4, n = (tid - 64) & 15;
+    ysh[rl][n] = (a.y && n < a.N && row0 + rl < a.M) ? a.y[(size_t)(row0 + rl) * a.N + n] : 0.f;
+  }
+  bool done_epi = false;
+  if constexpr (RB == 1) {
+   if (fused && a.epi.splits <= 64) {
+    done_epi = true;
     // one row per workgroup: the four split groups of every column in parallel (all their
     // loads in flight), combined in dense_epi_value's fixed order
     const DenseEpiArgs& e = a.epi;
@@ -111,7 +125,9 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
       e.out[(size_t)row0 * e.Ns + n] = hb;     // saved activation (ReLU mask of the backward)
     }
     __syncthreads();
-  } else if (fused) {   // previous dense layer's epilogue for this workgroup's rows
+   }
+  }
+  if (fused && !done_epi) {   // previous dense layer's epilogue for this workgroup's rows
     const DenseEpiArgs& e = a.epi;
     const int nr = min(RB, a.M - row0);
     for (int idx = tid; idx < nr * e.Ns; idx += 256) {
@@ -133,35 +149,36 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
     a.st->packs_stale = 0;
   }
 
-  if (!fused && wlds) __syncthreads();   // (the fused path's barriers already cover wsh)
-  float z[16];
+  HEAD_STAMP(1);
+  if (!fused) __syncthreads();   // (the fused path's barriers already cover wsh / ysh / bsh)
+  float z[NM];
 #pragma unroll
-  for (int n = 0; n < 16; ++n) z[n] = 0.f;
+  for (int n = 0; n < NM; ++n) z[n] = 0.f;
   if (row < a.M && row_wave) {
     const bf16* hr = a.h + (size_t)row * a.Ks;
     for (int k = lane; k < a.K; k += 64) {
       const int kp = a.flat_C ? flat_keras_to_padded(k, a.flat_C, a.flat_Cs) : k;
       const float hv = fused ? bf2f(hs[rw][kp]) : bf2f(hr[kp]);
 #pragma unroll
-      for (int n = 0; n < 16; ++n)
+      for (int n = 0; n < NM; ++n)
         if (n < N) z[n] += hv * (wlds ? wsh[k * N + n] : a.w[(size_t)k * N + n]);
     }
   }
 #pragma unroll
-  for (int n = 0; n < 16; ++n) {
+  for (int n = 0; n < NM; ++n) {
     if (n < N) {
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) z[n] += __shfl_xor(z[n], off);
     }
   }
   if (lane == 0 && row_wave) {
-    float dz[16];
+    float dz[NM];
 #pragma unroll
-    for (int n = 0; n < 16; ++n) dz[n] = 0.f;
+    for (int n = 0; n < NM; ++n) dz[n] = 0.f;
     float loss = 0.f, correct = 0.f;
     if (row < a.M) {
-      const float* yr = a.y ? a.y + (size_t)row * N : nullptr;
-      for (int n = 0; n < N; ++n) z[n] += a.bias ? a.bias[n] : 0.f;
+      const float* yr = a.y ? &ysh[rw][0] : nullptr;
+      for (int n = 0; n < N; ++n) z[n] += bsh[n];
       const float eps = 1e-7f;
       if (a.act == 1) {
         const float p = 1.f / (1.f + expf(-z[0]));
@@ -175,12 +192,12 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
           dz[0] = inr ? (pc - yv) : 0.f;
           correct = (rintf(p) == yv) ? 1.f : 0.f;
         }
-      } else if (a.act == 2) {
+      } else if (NM > 1 && a.act == 2) {
         float mx = z[0];
         int am = 0;
         for (int n = 1; n < N; ++n)
           if (z[n] > mx) { mx = z[n]; am = n; }
-        float p[16], s = 0.f;
+        float p[NM], s = 0.f;
         for (int n = 0; n < N; ++n) { p[n] = expf(z[n] - mx); s += p[n]; }
         for (int n = 0; n < N; ++n) p[n] /= s;
         if (a.probs)
@@ -188,7 +205,7 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
         if (yr) {
           float ps = 0.f;
           for (int n = 0; n < N; ++n) ps += p[n];
-          float gq = 0.f, gn[16];
+          float gq = 0.f, gn[NM];
           int ay = 0;
           float ymx = yr[0];
           for (int n = 0; n < N; ++n) {
@@ -217,20 +234,25 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
         }
       }
     }
-    for (int n = 0; n < 16; ++n) dz_s[rw][n] = dz[n] * a.inv_bs;
+    for (int n = 0; n < NM; ++n) dz_s[rw][n] = dz[n] * a.inv_bs;
     met[rw][0] = loss;
     met[rw][1] = correct;
   }
+  HEAD_STAMP(2);
   __syncthreads();
+  HEAD_STAMP(3);
   const int rows_here = min(RB, a.M - row0);
   if (tid == 0 && a.y && a.st) {
     float ls = 0.f, cs = 0.f;
     for (int r = 0; r < rows_here; ++r) { ls += met[r][0]; cs += met[r][1]; }
     // per-workgroup sums in a fixed row order, then order-independent integer atomics
-    atomicAdd((unsigned long long*)&a.st->metrics[0], (unsigned long long)llrint((double)ls * 4294967296.0));
-    atomicAdd((unsigned long long*)&a.st->metrics[1], (unsigned long long)llrintf(cs));
-    atomicAdd((unsigned long long*)&a.st->metrics[2], (unsigned long long)rows_here);
+    // spread over 16 slots: 128 workgroups on one address serialise at the L2 (~2 us)
+    long long* slot = a.st->metric_slots[blockIdx.x & 15];
+    atomicAdd((unsigned long long*)&slot[0], (unsigned long long)llrint((double)ls * 4294967296.0));
+    atomicAdd((unsigned long long*)&slot[1], (unsigned long long)llrintf(cs));
+    atomicAdd((unsigned long long*)&slot[2], (unsigned long long)rows_here);
   }
+  HEAD_STAMP(4);
   if (!a.training) return;
 
   float* ws = a.wslab + (size_t)blockIdx.x * a.K * N;
@@ -247,6 +269,7 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
     for (int rl = 0; rl < rows_here; ++rl) s += dz_s[rl][tid];
     a.bslab[(size_t)blockIdx.x * N + tid] = s;
   }
+  HEAD_STAMP(5);
   const BwdThrough& t = a.bt;
   if (t.dy) {
     const int width = t.pH * t.pW * t.pCs;
@@ -280,14 +303,22 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
       bwd_through_store(t, row0 + rl, y, x, c, gs, step);
     }
   }
+  HEAD_STAMP(6);
 }
 
 // Rows per workgroup: 4 (one wave per row), or 1 when the head also runs the previous dense
 // layer's split-K epilogue (a row per workgroup spreads that reduction over 128 workgroups)
 int head_rows_per_block(bool fused) { return fused ? 1 : HEAD_RB; }
 
+// NM: class-count bound (1 = the binary sigmoid head: no per-class loops or arrays)
 void launch_head(const HeadArgs& a, hipStream_t s) {
-  if (a.epi.part != nullptr) hipLaunchKernelGGL(head_kernel<1>, dim3(a.M), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(head_kernel<HEAD_RB>, dim3((a.M + HEAD_RB - 1) / HEAD_RB), dim3(256), 0, s, a);
+  const dim3 g1(a.M), g4((a.M + HEAD_RB - 1) / HEAD_RB);
+  if (a.N == 1) {
+    if (a.epi.part != nullptr) hipLaunchKernelGGL((head_kernel<1, 1>), g1, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((head_kernel<HEAD_RB, 1>), g4, dim3(256), 0, s, a);
+  } else {
+    if (a.epi.part != nullptr) hipLaunchKernelGGL((head_kernel<1, 16>), g1, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((head_kernel<HEAD_RB, 16>), g4, dim3(256), 0, s, a);
+  }
 }
 int head_epi_max() { return HEAD_EPI_MAX; }

@@ -450,14 +450,15 @@ class HipExecutor(Executor):
 
     # ------------------------------------------------------------------ metrics
     def _metrics(self):
-        # int64 fixed point (StepState::metrics): loss in units of 2^-32, counts exact
+        # int64 fixed point (StepState::metric_slots [16][4]): loss in units of 2^-32, counts
+        # exact; integer sums over the slots are order-independent
         o = self.K.STEP_STATE_METRICS_OFFSET // 8
-        ls, cs, n = self.state.view(torch.int64)[o:o + 3].tolist()
-        return [ls / 4294967296.0, float(cs), float(n)]
+        v = self.state.view(torch.int64)[o:o + 4 * self.K.STEP_STATE_METRIC_SLOTS].view(-1, 4).sum(0).tolist()
+        return [v[0] / 4294967296.0, float(v[1]), float(v[2])]
 
     def reset_metrics(self):
         o = self.K.STEP_STATE_METRICS_OFFSET // 8
-        self._st_f64[o:o + 4].zero_()
+        self._st_f64[o:o + 4 * self.K.STEP_STATE_METRIC_SLOTS].zero_()
         self._metrics_prev = (0.0, 0.0, 0.0)
 
     def read_metrics(self):
