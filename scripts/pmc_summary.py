@@ -45,6 +45,8 @@ def main(paths):
             d.append("wait %.0f%% of wave cycles" % (100 * c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]))
         if "SQ_INSTS_SALU" in c and "SQ_WAVES" in c:
             d.append("SALU/wave %.0f" % (c["SQ_INSTS_SALU"] / waves))
+        if "FETCH_SIZE" in c:
+            d.append("HBM fetch %.1f KB, write %.1f KB" % (c["FETCH_SIZE"], c.get("WRITE_SIZE", 0)))
         if d:
             print("    -> " + ", ".join(d))
 
