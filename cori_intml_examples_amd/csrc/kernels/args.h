@@ -120,6 +120,7 @@ struct WgradArgs {
   int dbg = 0;   // ablation (timing only): 1 skip staging, 2 skip MFMA, 4 skip slab stores;
                  // 16 = per-pixel unpool staging of pooled dY (A/B, exact)
   unsigned long long* ts = nullptr;   // diagnostics: per-workgroup [start, end] wall clock (null = off)
+  unsigned long long* ts2 = nullptr;  // diagnostics: per-workgroup [16] phase stamps (null = off)
 };
 
 // Dense forward, split-K partial products: part[s][m][n]

@@ -11,6 +11,9 @@ __device__ __forceinline__ bf16x4 tr_read_h(const bf16* p) {
 // k-step it reads NTT B fragments + MTW A fragments for MTW*NTT MFMAs.
 // PIPE: software-pipelined block loop (more VGPRs; pays off for workgroups that stream many
 // blocks, not for grids that already hide the latency with many resident workgroups).
+#define WH_STAMP(i)                                                                     \
+  if (a.ts2 && threadIdx.x == 0 && (i) < 16) a.ts2[(size_t)blockIdx.x * 16 + (i)] = wall_clock64();
+
 template <int MTW, int NTT, bool CS4, bool PIPE>
 __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT, const int bx, const int by,
                                                 const int bz, char* smem) {
@@ -33,6 +36,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   const bool do_bias = a.bslab != nullptr && bz == 0;
   const int MTb = MT + (do_bias ? 1 : 0);          // pseudo m-tile MT = bias (ones operand)
 
+  WH_STAMP(0);
   if (tid < 32) reinterpret_cast<uint32_t*>(zl)[tid] = 0u;
   for (int c = tid; c < MT * 4; c += 256) {
     const int k = (mt0 + c / 4) * 16 + 4 * (c & 3);
@@ -250,14 +254,18 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       }
     };
     fetch(blk0);
+    WH_STAMP(1);
     for (int blk = blk0; blk < blk1; ++blk) {
       const int b = blk / nrb, oy0 = (blk - b * nrb) * R;
       const int npix = min(R, a.Ho - oy0) * a.Wo;
       if (blk != blk0) __syncthreads();   // previous block's readers are done
       commit();
       __syncthreads();
+      WH_STAMP(2 + 2 * (blk - blk0));
       fetch(min(blk + 1, blk1 - 1));      // next block's loads fly during this block's MFMAs
       mma_block(npix);
+      if (a.ts2) asm volatile("" ::"v"(acc[0][0][0]));
+      WH_STAMP(3 + 2 * (blk - blk0));
     }
   } else {
     for (int blk = blk0; blk < blk1; ++blk) {
@@ -332,7 +340,10 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
             });
       }
       __syncthreads();
+      WH_STAMP(2 + 2 * (blk - blk0));
       mma_block(npix);
+      if (a.ts2) asm volatile("" ::"v"(acc[0][0][0]));
+      WH_STAMP(3 + 2 * (blk - blk0));
     }
   }
 
@@ -363,5 +374,6 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
         slab[(size_t)((mt0 + mt) * 16 + g * 4 + j) * ld + (nt0 + v) * 16 + i] = acc[u][v][j];
     }
   }
+  WH_STAMP(15);
 }
 

@@ -48,6 +48,8 @@ for name, fn, *_ in bp.launches:
         n_c = ca.B * cdiv(ca.Ho, ca.R) * cdiv(ca.NT, ntc)
     ts = torch.zeros(2 * (n_w + n_c), dtype=torch.int64, device=dev)
     wa.ts = ts.data_ptr()
+    ph2 = torch.zeros(16 * (n_w + n_c), dtype=torch.int64, device=dev)
+    wa.ts2 = ph2.data_ptr()
     ph = None
     if ca is not None:
         ph = torch.zeros(8 * (n_w + n_c), dtype=torch.int64, device=dev)
@@ -56,6 +58,18 @@ for name, fn, *_ in bp.launches:
         fn(s)
     torch.cuda.synchronize()
     wa.ts = 0
+    wa.ts2 = 0
+    q = ph2.view(-1, 16).cpu().numpy().astype(np.float64)[:n_w] * 0.01
+    nb = wa.blocks_per_split
+    segs = ["ktab", "fetch0"] + sum([["commit%d" % k, "mma%d" % k] for k in range(nb)], [])
+    idx = [0, 1] + sum([[2 + 2 * k, 3 + 2 * k] for k in range(nb)], []) + [15]
+    parts = []
+    for k in range(len(idx) - 1):
+        d = q[:, idx[k + 1]] - q[:, idx[k]]
+        d = d[(q[:, idx[k + 1]] > 0) & (q[:, idx[k]] > 0)]
+        if len(d):
+            parts.append("%s->%s +%.2f" % (segs[k] if k < len(segs) else "?", "slab" if idx[k + 1] == 15 else "", np.median(d)))
+    print("   wgrad phases (wave 0, median us):", ", ".join(parts))
     if ca is not None:
         ca.ts = 0
         p = ph.view(-1, 8).cpu().numpy().astype(np.float64)[n_w:] * 0.01
