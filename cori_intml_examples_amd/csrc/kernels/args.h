@@ -93,6 +93,12 @@ struct ConvStackArgs {
   int rows[MAX_STACK][MAX_STACK_SPLIT][6] = {};
   StackLayer L[MAX_STACK];
   unsigned long long* ts = nullptr;   // diagnostics: per-wave phase stamps [blocks*8][32]: 16 wall, 16 shader clock (null = off)
+  // src_mode 1 / 2: image b is dataset row perm[pos + b] (st->pos / st->eval_pos, the
+  // prologue's gather rule) read straight from StepState::data_x instead of A.x; each band
+  // then copies its owned input rows to xout (the batch buffer the backward reads)
+  int src_mode = 0;
+  bf16* xout = nullptr;
+  int xrows[MAX_STACK_SPLIT][2] = {};   // input rows [lo, hi) band sp copies to xout (host-checked)
 };
 
 // Weight gradient: dW[k][n] = sum_pixels im2col(x)[p][k] * dY[p][n]  (split over pixels)
@@ -184,6 +190,7 @@ struct GatherArgs {
   int bs = 0, R = 0, C = 0, Nd = 0;
   bf16* xb = nullptr;
   float* yb = nullptr;
+  int skip_x = 0;                // images read straight from the dataset by the conv stack
 };
 
 struct StepBeginArgs {

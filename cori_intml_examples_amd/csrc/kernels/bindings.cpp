@@ -115,7 +115,7 @@ PYBIND11_MODULE(_kernels, m) {
       .def(py::init<>())
       PTR(GatherArgs, xs) PTR(GatherArgs, ys) PTR(GatherArgs, perm) PTR(GatherArgs, st)
       RW(GatherArgs, bs) RW(GatherArgs, R) RW(GatherArgs, C) RW(GatherArgs, Nd) PTR(GatherArgs, xb)
-      PTR(GatherArgs, yb);
+      PTR(GatherArgs, yb) RW(GatherArgs, skip_x);
 
   py::class_<StepBeginArgs>(m, "StepBeginArgs")
       .def(py::init<>())
@@ -138,6 +138,12 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(ConvStackArgs, st) RW(ConvStackArgs, dbg) RW(ConvStackArgs, off_w) RW(ConvStackArgs, off_codes) RW(ConvStackArgs, lds_bytes)
       .def("set_buf_offsets", [](ConvStackArgs& a, int b0, int b1) { a.off_buf[0] = b0; a.off_buf[1] = b1; })
       RW(ConvStackArgs, splits) PTR(ConvStackArgs, ts) RW(ConvStackArgs, off_bias)
+      RW(ConvStackArgs, src_mode) PTR(ConvStackArgs, xout)
+      .def("set_xrows", [](ConvStackArgs& a, int sp, int lo, int hi) {
+        if (sp < 0 || sp >= MAX_STACK_SPLIT) throw std::out_of_range("conv stack band");
+        a.xrows[sp][0] = lo;
+        a.xrows[sp][1] = hi;
+      })
       .def("set_rows", [](ConvStackArgs& a, int l, int sp, int c0, int c1, int o0, int o1, int ib, int ih) {
         if (l < 0 || l >= MAX_STACK || sp < 0 || sp >= MAX_STACK_SPLIT) throw std::out_of_range("conv stack rows");
         const int v[6] = {c0, c1, o0, o1, ib, ih};

@@ -402,6 +402,14 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     const int Hi = A.rows[0][sp][5], Wi = L.Wo + L.KW - 1, Cs = L.Cs_in;
     const int y0 = A.rows[0][sp][4];
     const bf16* x = A.x + (size_t)b * L.H * L.W * Cs;
+    if (A.src_mode) {   // the prologue's gather rule, read in place (no batch copy)
+      const StepState* st = A.st;
+      const int* perm = reinterpret_cast<const int*>(st->perm);
+      const int row = (A.src_mode == 1 ? st->pos : st->eval_pos) + b;
+      int src = (st->use_perm && perm) ? perm[row] : row;
+      src = min(max(src, 0), st->data_n - 1);
+      x = reinterpret_cast<const bf16*>(st->data_x) + (size_t)src * st->data_R;
+    }
     if (Cs == 4) {
       const FastDiv fwi(Wi);
       staged_copy<8, bf16x4>(
@@ -507,6 +515,30 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     }
     __syncthreads();
     STACK_STAMP(2 + 4 * l);
+    if (l == 0 && A.xout && !(A.dbg & 8)) {
+      // this band's share of the input rows (host-computed partition, inside its staged
+      // halo image) -> the batch buffer the backward pass reads
+      const int r0 = A.xrows[sp][0], r1 = A.xrows[sp][1];
+      const int y0 = A.rows[0][sp][4], Wi = L.Wo + L.KW - 1;
+      const lbf16* img = (const lbf16*)(smem + A.off_buf[0]);
+      bf16* xo = A.xout + ((size_t)b * L.H + r0) * L.W * L.Cs_in;
+      if (L.Cs_in == 4) {
+        const int n = (r1 - r0) * L.W;
+        for (int i = tid; i < n; i += STACK_THREADS) {
+          const int ry = i / L.W, rx = i - ry * L.W;
+          *reinterpret_cast<bf16x4*>(xo + (size_t)i * 4) =
+              *reinterpret_cast<const LDS bf16x4*>(img + ((r0 + ry - y0) * Wi + rx + L.pad_l) * 4);
+        }
+      } else {
+        const int cpp = L.Cs_in >> 3, n = (r1 - r0) * L.W * cpp;
+        for (int i = tid; i < n; i += STACK_THREADS) {
+          const int pix = i / cpp, c = (i - pix * cpp) * 8;
+          const int ry = pix / L.W, rx = pix - ry * L.W;
+          *reinterpret_cast<bf16x8*>(xo + (size_t)pix * L.Cs_in + c) =
+              *reinterpret_cast<const LDS bf16x8*>(img + ((r0 + ry - y0) * Wi + rx + L.pad_l) * L.Cs_in + c);
+        }
+      }
+    }
     const lbf16* wl = wlds + L.w_lds;
 #define STACK_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, OW, codes, wl, tab, zl, step, lbias + l * 64
 #define ROWS_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, OW, codes, wl, step, lbias + l * 64, l == A.n - 1

@@ -69,7 +69,13 @@ __device__ __forceinline__ void gather_block(const GatherArgs& a, const StepStat
   const int nvec = R / 8;   // 16-byte vectors per row
   const uint4* s = reinterpret_cast<const uint4*>(xs + (size_t)src * R);
   uint4* d = reinterpret_cast<uint4*>(a.xb + (size_t)row * R);
-  for (int v = bx * 256 + threadIdx.x; v < nvec; v += gx * 256) d[v] = s[v];
+  if (!a.skip_x) {
+    for (int v = bx * 256 + threadIdx.x; v < nvec; v += gx * 256) d[v] = s[v];
+    // rows of 4-channel pixels with an odd pixel count end in half a vector (R % 8 == 4)
+    if ((R & 7) && bx == 0 && threadIdx.x == 0)
+      *reinterpret_cast<uint2*>(a.xb + (size_t)row * R + nvec * 8) =
+          *reinterpret_cast<const uint2*>(xs + (size_t)src * R + nvec * 8);
+  }
   if (bx == 0 && a.yb && ys)
     for (int c = threadIdx.x; c < C; c += 256) a.yb[(size_t)row * C + c] = ys[(size_t)src * C + c];
 }

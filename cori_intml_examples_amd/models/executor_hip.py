@@ -615,9 +615,18 @@ class BatchPlan:
         # one prologue launch: gather + the previous update's weight re-pack (training: always,
         # except with per-bucket optimizers that pack themselves; eval/predict: only if an
         # optimizer ran since the last pack) + the step bookkeeping
+        stack = self._conv_stack_args(training) if env_flag("INTML_CONV_STACK", True) else None
+        if stack is not None and env_flag("INTML_STACK_DIRECT", False) and self._stack_xrows(stack):
+            # opt-in: the conv stack reads each image straight from the dataset (same row rule
+            # as the gather) and writes the batch buffer for the backward itself, the prologue
+            # gathers only the targets (measured neutral on the RPV step: the prologue's 1 us
+            # moves into the conv stack's staging)
+            stack.src_mode = 1 if training else 2
+            stack.xout = self.xb.data_ptr()
+            ga.skip_x = 1
         pa = K.PrologueArgs()
         pa.sb, pa.ga = sb, ga
-        pa.gather_gx = K.gather_gx(ga.R)
+        pa.gather_gx = 1 if ga.skip_x else K.gather_gx(ga.R)
         pa.gather_blocks = pa.gather_gx * bs
         pa.pack_mode = (0 if self.early_optim else 1) if training else 2
         pa.master = store.master.data_ptr()
@@ -625,7 +634,6 @@ class BatchPlan:
         self.launches.append(("prologue", lambda s, a=pa: K.prologue(a, ex.pack_table, s)))
 
         # ---------------- forward convs
-        stack = self._conv_stack_args(training) if env_flag("INTML_CONV_STACK", True) else None
         if stack is not None:
             self.stack_args = stack
             self.launches.append(("conv_stack_fwd", lambda s, a=stack: K.conv_stack_fwd(a, s)))
@@ -889,6 +897,32 @@ class BatchPlan:
             a.set_layer(i, L)
         self.stack_splits = splits
         return a
+
+    def _stack_xrows(self, a):
+        """Partition of the input rows over the conv stack's bands for the in-place read
+        (each band copies its share to the batch buffer): band sp takes the input rows
+        centred on its owned conv rows, the first band from row 0, the last to row H.
+        False (keep the prologue gather) unless every share lies in its staged halo rows."""
+        g = self.ex.convs[0]
+        P = 2 if g.pool else 1
+        off = (g.KH - 1) // 2 - g.pad_t
+        S = a.splits
+        rows = self._stack_rows(self.ex.convs, S)
+        prev = 0
+        spans = []
+        for sp in range(S):
+            c0, c1, own0, own1, ib, ih = rows[0][sp]
+            lo = 0 if sp == 0 else P * own0 + off
+            hi = g.H if sp == S - 1 else P * own1 + off
+            if lo != prev or hi < lo or lo < ib or hi > ib + ih:
+                return False
+            spans.append((lo, hi))
+            prev = hi
+        if prev != g.H:
+            return False
+        for sp, (lo, hi) in enumerate(spans):
+            a.set_xrows(sp, lo, hi)
+        return True
 
     @staticmethod
     def _stack_rows(convs, splits):
