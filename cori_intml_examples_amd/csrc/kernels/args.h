@@ -244,7 +244,7 @@ struct RedDesc {
   int KH, KW, Cin, Cout, Cs;   // conv: k = tap*Cs + ci ; flat: C=Cin (channels), Cs
   int tpe;             // threads per element (1..256, power of 2): lanes split the S partials
   int blk0;            // first workgroup of this descriptor in the launch
-  int pad_;
+  int vec4;            // 1: identity layout, 4 consecutive elements per thread (float4 traffic)
 };
 
 #define MAX_RED 16

@@ -218,7 +218,11 @@ PYBIND11_MODULE(_kernels, m) {
         RedDesc& d = t.d[t.n++];
         d.slab = reinterpret_cast<const float*>(slab); d.stride_s = stride_s; d.S = S; d.ld = ld;
         d.dst_off = dst_off; d.numel = numel; d.type = type; d.KH = KH; d.KW = KW; d.Cin = Cin;
-        d.Cout = Cout; d.Cs = Cs; d.pad_ = 0;
+        d.Cout = Cout; d.Cs = Cs;
+        // a flattened dense kernel with unpadded channels and slab rows of exactly Cout
+        // columns IS the Keras layout: 4 consecutive elements per thread, float4 traffic
+        d.vec4 = (type == RED_FLATW && Cin == Cs && ld == Cout && numel % 4 == 0 && dst_off % 4 == 0 &&
+                  stride_s % 4 == 0 && S <= 8 && tpe <= 0) ? 1 : 0;
         // threads per element (power of 2, <= 64): E = 256 / tpe consecutive elements per
         // workgroup keep each slab-row read >= 16 contiguous bytes; each thread sums its
         // S / tpe partials 8 independent loads at a time
@@ -230,7 +234,7 @@ PYBIND11_MODULE(_kernels, m) {
           while (d.tpe < 64 && d.tpe * 16 < S) d.tpe *= 2;   // scripts/red_sweep.py)
         }
         d.blk0 = t.nblocks;
-        const int epb = 256 / d.tpe;
+        const int epb = d.vec4 ? 1024 : 256 / d.tpe;
         t.nblocks += (numel + epb - 1) / epb;
       }, py::arg("slab"), py::arg("stride_s"), py::arg("S"), py::arg("ld"), py::arg("dst_off"), py::arg("numel"),
       py::arg("type"), py::arg("KH"), py::arg("KW"), py::arg("Cin"), py::arg("Cout"), py::arg("Cs"), py::arg("tpe") = -1);

@@ -148,8 +148,43 @@ __device__ __forceinline__ bool slab_reduce_elem(const RedTable& tab, float* red
   return true;
 }
 
+// vec4 descriptors (identity layout): thread -> 4 consecutive elements, float4 slab loads in
+// fixed split order (the same per-element order as slab_reduce_elem with tpe = 1).
+__device__ __forceinline__ int red_desc(const RedTable& tab) {
+  int di = 0;
+  while (di + 1 < tab.n && (int)blockIdx.x >= tab.d[di + 1].blk0) ++di;
+  return di;
+}
+
+__device__ __forceinline__ bool slab_reduce_vec4(const RedDesc& d, int& e, float4& g) {
+  const int le = (((int)blockIdx.x - d.blk0) * 256 + (int)threadIdx.x) * 4;
+  if (le >= d.numel) return false;
+  const float* p = d.slab + le;
+  float4 v[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    if (s < d.S) v[s] = *reinterpret_cast<const float4*>(p + (size_t)s * d.stride_s);
+  float4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};   // a[s % 2], like the scalar path's a[u]
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    if (s < d.S) {
+      float4& a = (s & 1) ? a1 : a0;
+      a.x += v[s].x; a.y += v[s].y; a.z += v[s].z; a.w += v[s].w;
+    }
+  g = float4{a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w};
+  e = d.dst_off + le;
+  return true;
+}
+
 __global__ __launch_bounds__(256) void slab_reduce_kernel(float* __restrict__ grad, const RedTable tab) {
   __shared__ float red[256];
+  const RedDesc& d = tab.d[red_desc(tab)];
+  if (d.vec4) {
+    int e;
+    float4 g;
+    if (slab_reduce_vec4(d, e, g)) *reinterpret_cast<float4*>(grad + e) = g;
+    return;
+  }
   int e;
   float v;
   if (slab_reduce_elem(tab, red, e, v)) grad[e] = v;
@@ -376,6 +411,27 @@ template <int KIND>
 __global__ __launch_bounds__(256) void reduce_optim_kernel(float* __restrict__ grad, const RedTable tab,
                                                            const OptimArgs a) {
   __shared__ float red[256];
+  const RedDesc& dsc = tab.d[red_desc(tab)];
+  if (dsc.vec4) {
+    int e;
+    float4 g;
+    if (slab_reduce_vec4(dsc, e, g)) {
+      *reinterpret_cast<float4*>(grad + e) = g;
+      float4 p = *reinterpret_cast<const float4*>(a.p + e);
+      float4 s0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : float4{0.f, 0.f, 0.f, 0.f};
+      float4 s1 = a.s1 ? *reinterpret_cast<const float4*>(a.s1 + e) : float4{0.f, 0.f, 0.f, 0.f};
+      const float gs = a.grad_scale;
+      opt_update<KIND>(a, a.st, p.x, g.x * gs, &s0.x, &s1.x);
+      opt_update<KIND>(a, a.st, p.y, g.y * gs, &s0.y, &s1.y);
+      opt_update<KIND>(a, a.st, p.z, g.z * gs, &s0.z, &s1.z);
+      opt_update<KIND>(a, a.st, p.w, g.w * gs, &s0.w, &s1.w);
+      *reinterpret_cast<float4*>(a.p + e) = p;
+      if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
+      if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
+    }
+    if (a.defer_pack && blockIdx.x == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
+    return;
+  }
   int e;
   float g;
   if (slab_reduce_elem(tab, red, e, g)) {
