@@ -31,6 +31,11 @@ bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT
                       hipStream_t s);
 bool launch_dense_bwd_dual(const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da,
                            hipStream_t s);
+void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s);
+size_t dense_wgrad_lds_bytes(int kg, int ntt);
+void launch_dense_dx(const DenseFwdArgs& a, int ntc, hipStream_t s);
+void launch_dense_bwd_pair(const WgradArgs& wa, int kg, int ntt, int splits, const DenseFwdArgs& da, int ntc,
+                           hipStream_t s);
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s);
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
 int gather_gx(int R);
@@ -280,6 +285,14 @@ PYBIND11_MODULE(_kernels, m) {
     check_last("dense_bwd_dual");
     return ok;
   });
+  m.def("dense_wgrad", [](const WgradArgs& a, int kg, int ntt, int splits, uintptr_t s) {
+    launch_dense_wgrad(a, kg, ntt, splits, S(s)); check_last("dense_wgrad"); });
+  m.def("dense_wgrad_lds_bytes", &dense_wgrad_lds_bytes);
+  m.def("dense_dx", [](const DenseFwdArgs& a, int ntc, uintptr_t s) {
+    launch_dense_dx(a, ntc, S(s)); check_last("dense_dx"); });
+  m.def("dense_bwd_pair", [](const WgradArgs& wa, int kg, int ntt, int splits, const DenseFwdArgs& da, int ntc,
+                             uintptr_t s) {
+    launch_dense_bwd_pair(wa, kg, ntt, splits, da, ntc, S(s)); check_last("dense_bwd_pair"); });
   m.def("dual_halo", [](const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits, uintptr_t s) {
     const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, S(s));
     check_last("dual_halo");

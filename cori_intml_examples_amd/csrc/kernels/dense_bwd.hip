@@ -1,0 +1,348 @@
+// Dense-layer backward on gfx950: the weight gradient dW = X^T dH and the input gradient
+// dX = dH W^T (routed through the previous stage's dropout / ReLU masks), designed for the
+// reference models' shapes: a large flattened width K (4,096-65,536 features), a small
+// output width N (128-512) and a batch M of 128-4,096 rows.
+//
+// Both GEMMs are tiny in FLOPs (about 0.3 us of MFMA time at batch 1024 for RPV) and are
+// bound by load latency, so the kernels are built around keeping loads in flight:
+//
+// dense_wgrad_kernel<KG, NTT>  (grid: row splits x feature groups x n groups)
+//   * a workgroup owns KG*16 features x NTT*16 outputs over a range of batch rows; its four
+//     waves take interleaved 32-row chunks and accumulate independently -- each wave stages
+//     its chunk in a PRIVATE LDS region, so the chunk loop has no workgroup barrier;
+//   * the next chunk's global loads are issued before the current chunk's MFMAs
+//     (register double buffer);
+//   * both operands have the batch (the reduction axis) outermost, so fragments are read
+//     with ds_read_b64_tr_b16 from row-major tiles whose 8-row blocks are each shifted by a
+//     further 128 B: the two 32-lane groups of the transposed read then hit disjoint banks;
+//   * the bias gradient (column sums of dH) is summed from the dH fragments the MFMAs already
+//     read (8 rows per lane), in the feature-group-0 workgroups;
+//   * the four waves' partials are summed in fixed order through LDS (deterministic) and
+//     stored as coalesced float4 rows of the [split][K][N] slab, the layout slab_reduce reads.
+//
+// dense_dx_kernel<NTC>  (grid: 64-row groups x n groups)
+//   * a wave owns 16 rows x NTC*16 columns: each dH fragment feeds NTC MFMAs;
+//   * the result goes through a per-wave LDS tile so every lane finishes with 8 consecutive
+//     columns: one 16-byte load of the saved activation (ReLU mask) and one 16-byte store of
+//     the gradient per 8 outputs (bwd_through_store8), instead of 2-byte scattered accesses.
+//
+// dense_bwd_pair_kernel runs both bodies in one launch (they read the same dH and write
+// disjoint buffers), the dX workgroups first: they are short and fill the machine while the
+// fewer, longer wgrad workgroups run.
+#include <algorithm>
+#include <stdexcept>
+
+#include "dense_body.h"
+
+namespace {
+constexpr int DW_LDA = 48;   // A tile row stride (elements): 32 features + pad
+
+__device__ __forceinline__ bf16x4 tr_read4(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, p));
+}
+
+template <int NTT>
+struct DwGeom {
+  static constexpr int LDB = (NTT * 16 > 32 ? NTT * 16 : 32) + 16;   // dH tile row stride
+  static constexpr int A_ELEMS = 32 * DW_LDA + 192;
+  static constexpr int B_ELEMS = 32 * LDB + 192;
+  static constexpr int WAVE_BYTES = (A_ELEMS + B_ELEMS) * 2;
+  static constexpr int LDR = NTT * 16 + 4;                           // fp32 reduce row stride
+};
+
+// row r of a staged 32-row tile: each block of 8 rows starts 64 elements (128 B) further on
+// than the plain stride puts it, so rows 8g+q of the lane groups g = 0/1 (and 2/3) of a
+// transposed read land in opposite bank halves (the blocks never overlap)
+__device__ __forceinline__ int dw_row(int r, int ld) { return r * ld + (r >> 3) * 64; }
+}   // namespace
+
+size_t dense_wgrad_lds_bytes(int kg, int ntt) {
+  size_t stage = 0, red = 0;
+  switch (ntt) {
+    case 1: stage = 4 * DwGeom<1>::WAVE_BYTES; red = (size_t)4 * 16 * DwGeom<1>::LDR * 4; break;
+    case 2: stage = 4 * DwGeom<2>::WAVE_BYTES; red = (size_t)4 * 16 * DwGeom<2>::LDR * 4; break;
+    case 4: stage = 4 * DwGeom<4>::WAVE_BYTES; red = (size_t)4 * 16 * DwGeom<4>::LDR * 4; break;
+    default: stage = 4 * DwGeom<8>::WAVE_BYTES; red = (size_t)4 * 16 * DwGeom<8>::LDR * 4; break;
+  }
+  (void)kg;
+  return std::max(stage, red + 16 * 128 * 4);
+}
+
+template <int KG, int NTT>
+__device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int bx, const int by, const int bz,
+                                                 char* smem) {
+  using G = DwGeom<NTT>;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, g = lane >> 4;
+  bf16* As = reinterpret_cast<bf16*>(smem) + (size_t)wave * (G::A_ELEMS + G::B_ELEMS);
+  bf16* Bs = As + G::A_ELEMS;
+  const int f0 = by * KG * 16, n0 = bz * NTT * 16;
+  const int r_begin = bx * a.px_per_split;
+  const int r_end = min(a.P, r_begin + a.px_per_split);
+  const int nchunks = max(0, (r_end - r_begin + 31) >> 5);
+  const bool do_bias = a.bslab != nullptr && by == 0;
+
+  // per-lane load slots: A pieces (row, 8 features), B pieces (row, 8 outputs)
+  bf16x8 ra[KG], rb[NTT];
+  auto issue = [&](int c) {
+    const int r0 = r_begin + c * 32;
+#pragma unroll
+    for (int u = 0; u < KG; ++u) {
+      const int pc = lane + 64 * u, row = pc / (KG * 2), q = pc - row * (KG * 2);
+      const int f = f0 + q * 8;
+      ra[u] = load_bf16x8_if(r0 + row < r_end && f < a.Cs_in, a.x + (size_t)(r0 + row) * a.Cs_in + f, a.x);
+    }
+#pragma unroll
+    for (int u = 0; u < NTT; ++u) {
+      const int pc = lane + 64 * u, row = pc / (NTT * 2), q = pc - row * (NTT * 2);
+      const int n = n0 + q * 8;
+      rb[u] = load_bf16x8_if(r0 + row < r_end && n < a.Cs_dy, a.dy + (size_t)(r0 + row) * a.Cs_dy + n, a.dy);
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int u = 0; u < KG; ++u) {
+      const int pc = lane + 64 * u, row = pc / (KG * 2), q = pc - row * (KG * 2);
+      *reinterpret_cast<bf16x8*>(As + dw_row(row, DW_LDA) + q * 8) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NTT; ++u) {
+      const int pc = lane + 64 * u, row = pc / (NTT * 2), q = pc - row * (NTT * 2);
+      *reinterpret_cast<bf16x8*>(Bs + dw_row(row, G::LDB) + q * 8) = rb[u];
+    }
+  };
+
+  f32x4 acc[KG][NTT];
+  float bsum[NTT];
+#pragma unroll
+  for (int nt = 0; nt < NTT; ++nt) {
+    bsum[nt] = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KG; ++kt) acc[kt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // fragment read rows: lane reads rows 8g + (i>>2) (lo) and +4 (hi), 4 columns at 4*(i&3)
+  const int rd = 8 * g + (i >> 2);
+  if (wave < nchunks) issue(wave);
+  for (int c = wave; c < nchunks; c += 4) {
+    stash();
+    __builtin_amdgcn_wave_barrier();
+    if (c + 4 < nchunks) issue(c + 4);
+    bf16x8 afr[KG];
+#pragma unroll
+    for (int kt = 0; kt < KG; ++kt) {
+      const bf16* p = As + dw_row(rd, DW_LDA) + kt * 16 + 4 * (i & 3);
+      afr[kt] = __builtin_shufflevector(tr_read4(p), tr_read4(p + 4 * DW_LDA), 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTT; ++nt) {
+      const bf16* p = Bs + dw_row(rd, G::LDB) + nt * 16 + 4 * (i & 3);
+      const bf16x8 bfr = __builtin_shufflevector(tr_read4(p), tr_read4(p + 4 * G::LDB), 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+      for (int kt = 0; kt < KG; ++kt) acc[kt][nt] = mfma16(afr[kt], bfr, acc[kt][nt]);
+      if (do_bias) {   // the lane's 8 rows of column nt*16+i (lane groups summed at the end)
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { s0 += bf2f(bfr[q]); s1 += bf2f(bfr[4 + q]); }
+        bsum[nt] += s0 + s1;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // fixed-order cross-wave sum (w0 + w1 + w2 + w3), one 16-feature k-tile per pass
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);                   // [4 waves][16][LDR]
+  float* bred = red + 4 * 16 * G::LDR;                           // [4 waves][4 groups][128]
+  const int ld = a.NT * 16;
+  float* slab = a.slab + (size_t)bx * a.Ktiles * 16 * ld;
+  if (do_bias) {
+#pragma unroll
+    for (int nt = 0; nt < NTT; ++nt) bred[(wave * 4 + g) * 128 + nt * 16 + i] = bsum[nt];
+  }
+#pragma unroll
+  for (int kt = 0; kt < KG; ++kt) {
+    float* rw = red + wave * 16 * G::LDR;
+#pragma unroll
+    for (int nt = 0; nt < NTT; ++nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rw[(4 * g + j) * G::LDR + nt * 16 + i] = acc[kt][nt][j];
+    __syncthreads();
+    constexpr int C4 = NTT * 4;                                  // float4 per row
+    for (int e = tid; e < 16 * C4; e += 256) {
+      const int row = e / C4, c4 = e - row * C4;
+      const int f = f0 + kt * 16 + row, n = n0 + c4 * 4;
+      f32x4 s = *reinterpret_cast<const f32x4*>(red + row * G::LDR + c4 * 4);
+#pragma unroll
+      for (int w = 1; w < 4; ++w) s += *reinterpret_cast<const f32x4*>(red + (w * 16 + row) * G::LDR + c4 * 4);
+      if (f < a.Ktiles * 16 && n < ld) *reinterpret_cast<f32x4*>(slab + (size_t)f * ld + n) = s;
+    }
+    __syncthreads();
+  }
+  if (do_bias && tid < NTT * 16 && n0 + tid < ld) {
+    float b = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) b += bred[q * 128 + tid];     // fixed order: wave-major, group
+    a.bslab[(size_t)bx * ld + n0 + tid] = b;
+  }
+}
+
+template <int NTC>
+__device__ __forceinline__ void dense_dx_body(const DenseFwdArgs& a, const int bx, const int by, char* smem) {
+  constexpr int LDE = NTC * 16 + 4;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  float* ep = reinterpret_cast<float*>(smem) + wave * 16 * LDE;
+  const int mt = bx * 4 + wave;
+  const int nt0 = by * NTC;
+  const int row = mt * 16 + r;
+  const bool rv = row < a.M;
+  const bf16* xr = a.x + (size_t)(rv ? row : 0) * a.Ks;
+  f32x4 acc[NTC];
+#pragma unroll
+  for (int nt = 0; nt < NTC; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kb = 0; kb < a.KS; kb += 4) {
+    bf16x8 af[4], bfr[4][NTC];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {   // independent, branch-free loads
+      const int ks = min(kb + u, a.KS - 1);
+      const int k0 = ks * 32 + g * 8;
+      af[u] = load_bf16x8_if(rv && k0 < a.Ks && kb + u < a.KS, xr + k0, a.x);
+#pragma unroll
+      for (int nt = 0; nt < NTC; ++nt) {
+        const int ntc = min(nt0 + nt, a.NT - 1);
+        bfr[u][nt] = load_bf16x8(a.wpk + ((size_t)(ks * a.NT + ntc) * 64 + lane) * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int nt = 0; nt < NTC; ++nt) acc[nt] = mfma16(af[u], bfr[u][nt], acc[nt]);
+  }
+  // stage [16 rows][NTC*16] fp32, re-read as 8-column runs
+#pragma unroll
+  for (int nt = 0; nt < NTC; ++nt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ep[(4 * g + j) * LDE + nt * 16 + r] = acc[nt][j];
+  __builtin_amdgcn_wave_barrier();
+  const BwdThrough& t = a.bt;
+  const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
+  const int width = t.pH * t.pW * t.pCs;
+  const int pix = t.pH * t.pW;
+  constexpr int C8 = NTC * 2;
+  for (int e = lane; e < 16 * C8; e += 64) {
+    const int rr = e / C8, c8 = e - rr * C8;
+    const int m = mt * 16 + rr, n = nt0 * 16 + c8 * 8;
+    if (m >= a.M || n >= width) continue;
+    float v[8];
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(ep + rr * LDE + c8 * 8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(ep + rr * LDE + c8 * 8 + 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[k] = lo[k]; v[4 + k] = hi[k]; }
+    const int px = n / t.pCs;
+    bwd_through_store8(t, (size_t)m * pix + px, n - px * t.pCs, v, step);
+  }
+}
+
+size_t dense_dx_lds_bytes(int ntc) { return (size_t)4 * 16 * (ntc * 16 + 4) * 4; }
+
+template <int KG, int NTT>
+__global__ __launch_bounds__(256) void dense_wgrad_kernel(const WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  dense_wgrad_body<KG, NTT>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
+template <int NTC>
+__global__ __launch_bounds__(256) void dense_dx_kernel(const DenseFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  dense_dx_body<NTC>(a, blockIdx.x, blockIdx.y, smem);
+}
+
+// dX workgroups [0, n_x) first (grid x-major over 64-row groups), then the wgrad ones
+template <int KG, int NTT, int NTC>
+__global__ __launch_bounds__(256) void dense_bwd_pair_kernel(const WgradArgs wa, const DenseFwdArgs da,
+                                                             const int n_x, const int xgx, const int wgx,
+                                                             const int wgy) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int id = blockIdx.x;
+  if (id < n_x) {
+    dense_dx_body<NTC>(da, id % xgx, id / xgx, smem);
+  } else {
+    id -= n_x;
+    const int bx = id % wgx;
+    id /= wgx;
+    dense_wgrad_body<KG, NTT>(wa, bx, id % wgy, id / wgy, smem);
+  }
+}
+
+// Host checks of the shapes the kernels assume (a mismatch would read or write out of range).
+static void dense_wgrad_check(const WgradArgs& a, int kg, int ntt, int splits) {
+  if (!((kg == 1 || kg == 2) && (ntt == 1 || ntt == 2 || ntt == 4 || ntt == 8)))
+    throw std::runtime_error("dense_wgrad: unsupported (kg, ntt)");
+  if (a.Cs_in % 8 || a.Cs_dy % 8 || a.px_per_split <= 0 || a.px_per_split % 32 ||
+      (long long)splits * a.px_per_split < a.P || a.KH != 1 || a.KW != 1)
+    throw std::runtime_error("dense_wgrad: geometry");
+}
+static void dense_dx_check(const DenseFwdArgs& a, int ntc) {
+  if (!(ntc == 1 || ntc == 2 || ntc == 4) || a.mode != 1 || a.splits != 1 || a.bt.pCs % 8 || a.Ks % 8)
+    throw std::runtime_error("dense_dx: geometry");
+}
+
+static dim3 dense_wgrad_grid(const WgradArgs& a, int kg, int ntt, int splits) {
+  return dim3(splits, (a.Ktiles + kg - 1) / kg, (a.NT + ntt - 1) / ntt);
+}
+static dim3 dense_dx_grid(const DenseFwdArgs& a, int ntc) {
+  return dim3((a.M + 63) / 64, (a.NT + ntc - 1) / ntc);
+}
+
+#define DW_CASES(X) X(1, 1) X(1, 2) X(1, 4) X(1, 8) X(2, 1) X(2, 2) X(2, 4) X(2, 8)
+
+void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s) {
+  dense_wgrad_check(a, kg, ntt, splits);
+  const dim3 grid = dense_wgrad_grid(a, kg, ntt, splits);
+  const size_t lds = dense_wgrad_lds_bytes(kg, ntt);
+#define X(KG_, NT_)                                                                 \
+  if (kg == KG_ && ntt == NT_) {                                                    \
+    hipLaunchKernelGGL((dense_wgrad_kernel<KG_, NT_>), grid, dim3(256), lds, s, a); \
+    return;                                                                         \
+  }
+  DW_CASES(X)
+#undef X
+}
+
+void launch_dense_dx(const DenseFwdArgs& a, int ntc, hipStream_t s) {
+  dense_dx_check(a, ntc);
+  const dim3 grid = dense_dx_grid(a, ntc);
+  const size_t lds = dense_dx_lds_bytes(ntc);
+  if (ntc == 1) hipLaunchKernelGGL((dense_dx_kernel<1>), grid, dim3(256), lds, s, a);
+  else if (ntc == 2) hipLaunchKernelGGL((dense_dx_kernel<2>), grid, dim3(256), lds, s, a);
+  else hipLaunchKernelGGL((dense_dx_kernel<4>), grid, dim3(256), lds, s, a);
+}
+
+template <int KG, int NTT>
+static void pair_t(const WgradArgs& wa, const DenseFwdArgs& da, int ntc, int splits, size_t lds, hipStream_t s) {
+  const dim3 wg = dense_wgrad_grid(wa, KG, NTT, splits), xg = dense_dx_grid(da, ntc);
+  const int n_x = xg.x * xg.y, n_w = wg.x * wg.y * wg.z;
+  const dim3 grid(n_x + n_w);
+  if (ntc == 1)
+    hipLaunchKernelGGL((dense_bwd_pair_kernel<KG, NTT, 1>), grid, dim3(256), lds, s, wa, da, n_x, (int)xg.x,
+                       (int)wg.x, (int)wg.y);
+  else if (ntc == 2)
+    hipLaunchKernelGGL((dense_bwd_pair_kernel<KG, NTT, 2>), grid, dim3(256), lds, s, wa, da, n_x, (int)xg.x,
+                       (int)wg.x, (int)wg.y);
+  else
+    hipLaunchKernelGGL((dense_bwd_pair_kernel<KG, NTT, 4>), grid, dim3(256), lds, s, wa, da, n_x, (int)xg.x,
+                       (int)wg.x, (int)wg.y);
+}
+
+void launch_dense_bwd_pair(const WgradArgs& wa, int kg, int ntt, int splits, const DenseFwdArgs& da, int ntc,
+                           hipStream_t s) {
+  dense_wgrad_check(wa, kg, ntt, splits);
+  dense_dx_check(da, ntc);
+  const size_t lds = std::max(dense_wgrad_lds_bytes(kg, ntt), dense_dx_lds_bytes(ntc));
+#define X(KG_, NT_)                                   \
+  if (kg == KG_ && ntt == NT_) {                      \
+    pair_t<KG_, NT_>(wa, da, ntc, splits, lds, s);    \
+    return;                                           \
+  }
+  DW_CASES(X)
+#undef X
+}

@@ -748,11 +748,20 @@ class BatchPlan:
             # the slab round trip disappears (the dense kernel is most of the model's bytes).
             direct = (g.src.C == g.src.Cs and g.N % 16 == 0 and g.src.width % 16 == 0
                       and g.src.width * g.N * 4 > (16 << 20))     # small layers keep split-K slabs
-            wa, cfg, slab, bslab = self._wgrad_args(
-                xin, 1, 1, g.src.width, 1, 1, 1, 1, 1, 0, 0, self.dense_dh[g.j], g.Ns, g.N, bs,
-                ds.dense.use_bias, direct=(store.grad.data_ptr() + 4 * sp.offset) if direct else None)
-            self.launches.append(("wgrad_dense%d" % g.j, lambda s, a=wa, c=cfg: K.wgrad(a, c[0], c[1], c[2], s),
-                                  "side"))
+            direct_ptr = (store.grad.data_ptr() + 4 * sp.offset) if direct else None
+            # dense_bwd.hip kernels (per-wave pipelined wgrad, vectorised dX epilogue) where the
+            # 8-element alignment they assume holds; the generic wgrad / split-K path otherwise
+            bwd2 = (env_flag("INTML_DENSE_BWD2", True) and g.src.width % 8 == 0 and g.Ns % 8 == 0)
+            if bwd2:
+                wa, cfg, slab, bslab = self._dense_wgrad_args(xin, g.src.width, self.dense_dh[g.j], g.Ns, g.N, bs,
+                                                              ds.dense.use_bias, direct_ptr)
+                wl = lambda s, a=wa, c=cfg: K.dense_wgrad(a, c[0], c[1], c[2], s)
+            else:
+                wa, cfg, slab, bslab = self._wgrad_args(
+                    xin, 1, 1, g.src.width, 1, 1, 1, 1, 1, 0, 0, self.dense_dh[g.j], g.Ns, g.N, bs,
+                    ds.dense.use_bias, direct=direct_ptr)
+                wl = lambda s, a=wa, c=cfg: K.wgrad(a, c[0], c[1], c[2], s)
+            self.launches.append(("wgrad_dense%d" % g.j, wl, "side"))
             w_at = len(self.launches) - 1
             S, ld = cfg[2], g.NT * 16
             descs = [] if direct else [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel,
@@ -775,11 +784,21 @@ class BatchPlan:
                 a.st = st_ptr
                 a.bt = self._bt_for(g.src)
                 dname = "dense_dx%d" % g.j
+                ntc = self._dense_dx_ntc(a) if (bwd2 and a.bt.pCs % 8 == 0 and a.Ks % 8 == 0
+                                               and not K.dense_big(a.NT, a.KS)) else 0
                 if self.side is None and env_flag("INTML_DUAL_DENSE", True):
                     # one launch for the dense wgrad and dX (independent GEMMs over dH), in the
                     # wgrad's slot (its slabs are final after it)
                     dname = "dense_bwd%d" % g.j
-                    self.launches[w_at] = (dname, lambda s, a=a, w=wa, c=cfg: self._dense_dual(w, c, a, s), "main")
+                    if ntc:
+                        fn = lambda s, a=a, w=wa, c=cfg, n=ntc: K.dense_bwd_pair(w, c[0], c[1], c[2], a, n, s)
+                    elif bwd2:
+                        fn = lambda s, a=a, w=wa, c=cfg: (K.dense_wgrad(w, c[0], c[1], c[2], s), K.dense_fwd(a, s))
+                    else:
+                        fn = lambda s, a=a, w=wa, c=cfg: self._dense_dual(w, c, a, s)
+                    self.launches[w_at] = (dname, fn, "main")
+                elif ntc:
+                    self.launches.append((dname, lambda s, a=a, n=ntc: K.dense_dx(a, n, s)))
                 else:
                     self.launches.append((dname, lambda s, a=a: K.dense_fwd(a, s)))
                 self.pack_readers.append((dname, sp.offset, sp.offset + sp.numel))
@@ -1187,6 +1206,50 @@ class BatchPlan:
         a.bslab = bslab.data_ptr() if bslab is not None else 0
         self.wgrad_slabs.append((slab, bslab))
         return a, (ktw, ntt, S), slab, bslab
+
+    def _dense_wgrad_args(self, xin, width, dh, Ns, N, bs, bias, direct=None):
+        """Dense weight gradient on dense_wgrad_kernel: KG*16 features x NTT*16 outputs per
+        workgroup, the batch split into row ranges of >= 128 rows (one 32-row chunk per wave)
+        until the launch has ~256 workgroups or the partial slabs reach their byte budget."""
+        K, dev = self.ex.K, self.ex.device
+        a = K.WgradArgs()
+        a.x = xin.data_ptr()
+        a.B, a.H, a.W, a.Cs_in = bs, 1, 1, width
+        a.Ho, a.Wo = 1, 1
+        a.Ktiles = cdiv(width, 16)
+        a.dy = dh.data_ptr()
+        a.Cs_dy = Ns
+        NT = cdiv(N, 16)
+        a.NT = NT
+        a.P = bs
+        ntt = _pow2_le(NT, 8)
+        kg = int(os.environ.get("INTML_DW_KG", "2"))
+        groups = cdiv(a.Ktiles, kg) * cdiv(NT, ntt)
+        per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
+        s_budget = max(1, (int(os.environ.get("INTML_DW_SLAB_MB", "8")) << 20) // per_split_bytes)
+        S = 1 if direct else max(1, min(s_budget, cdiv(int(os.environ.get("INTML_DW_MIN_WGS", "256")), groups),
+                                        cdiv(bs, 128)))
+        pps = cdiv(cdiv(bs, S), 32) * 32
+        S = cdiv(bs, pps)
+        a.px_per_split = pps
+        slab = None if direct else torch.zeros(S, a.Ktiles * 16, NT * 16, dtype=torch.float32, device=dev)
+        bslab = torch.zeros(S, NT * 16, dtype=torch.float32, device=dev) if bias else None
+        a.slab = direct if direct else slab.data_ptr()
+        a.bslab = bslab.data_ptr() if bslab is not None else 0
+        self.wgrad_slabs.append((slab, bslab))
+        return a, (kg, ntt, S), slab, bslab
+
+    @staticmethod
+    def _dense_dx_ntc(a):
+        """n-tiles per wave of dense_dx_kernel: the most A-fragment reuse that still leaves
+        >= INTML_DX_MIN_WGS workgroups (4 waves x 16 rows each)."""
+        if "INTML_DX_NTC" in os.environ:
+            return int(os.environ["INTML_DX_NTC"])
+        want = int(os.environ.get("INTML_DX_MIN_WGS", "512"))
+        for ntc in (4, 2):
+            if cdiv(a.M, 64) * cdiv(a.NT, ntc) >= want:
+                return ntc
+        return 1
 
     def _add_group_reduce(self):
         """Record where the group just appended has its partial slabs final."""
