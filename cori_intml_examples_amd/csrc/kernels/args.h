@@ -20,6 +20,25 @@ struct BwdThrough {
   bf16* dy = nullptr;                   // output [B, cH, cW, pCs] (or [B, pH, pW, pCs])
 };
 
+// Keras optimizer update of a flat fp32 range (optimizer kernels; also fused into the
+// reductions / the dense weight-gradient kernel).
+struct OptimArgs {
+  float* p = nullptr;
+  const float* g = nullptr;
+  float* s0 = nullptr;
+  float* s1 = nullptr;
+  int n = 0;                     // elements [lo, lo + n) are updated (lo need not be aligned)
+  int lo = 0;
+  StepState* st = nullptr;       // read: this step's scalars; written: packs_stale
+  int kind = 0;
+  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-7f, rho = 0.95f, momentum = 0.f;
+  int nesterov = 0;
+  float grad_scale = 1.f;
+  int pack_only = 0;
+  int defer_pack = 0;            // leave the re-pack to the next step's prologue (marks stale)
+  bf16* arena = nullptr;
+};
+
 // Implicit-GEMM convolution / 1x1 "dense as conv" (fwd, dgrad, dense-dX).
 struct ConvMMArgs {
   const bf16* x = nullptr;       // input activations [B, H, W, Cs_in]
@@ -127,6 +146,11 @@ struct WgradArgs {
                  // 16 = per-pixel unpool staging of pooled dY (A/B, exact)
   unsigned long long* ts = nullptr;   // diagnostics: per-workgroup [start, end] wall clock (null = off)
   unsigned long long* ts2 = nullptr;  // diagnostics: per-workgroup [16] phase stamps (null = off)
+  // dense_wgrad with ONE split and the identity layout (slab == the Keras gradient): when
+  // opt_w >= 0 the kernel applies `opt` to the weight elements opt_w + f*ld + n (and, with a
+  // bias, opt_b + n) as soon as their gradient is final -- no slab reduction for the layer
+  OptimArgs opt;
+  int opt_w = -1, opt_b = -1;
 };
 
 // Dense forward, split-K partial products: part[s][m][n]
@@ -214,22 +238,6 @@ struct PrologueArgs {
   bf16* arena = nullptr;
 };
 
-struct OptimArgs {
-  float* p = nullptr;
-  const float* g = nullptr;
-  float* s0 = nullptr;
-  float* s1 = nullptr;
-  int n = 0;                     // elements [lo, lo + n) are updated (lo need not be aligned)
-  int lo = 0;
-  StepState* st = nullptr;       // read: this step's scalars; written: packs_stale
-  int kind = 0;
-  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-7f, rho = 0.95f, momentum = 0.f;
-  int nesterov = 0;
-  float grad_scale = 1.f;
-  int pack_only = 0;
-  int defer_pack = 0;            // leave the re-pack to the next step's prologue (marks stale)
-  bf16* arena = nullptr;
-};
 
 // Slab reduction descriptors: sum split-partials into the flat fp32 grad buffer in
 // Keras layout.

@@ -94,7 +94,8 @@ PYBIND11_MODULE(_kernels, m) {
       RW(WgradArgs, Cs_dy) RW(WgradArgs, NT) RW(WgradArgs, P) RW(WgradArgs, px_per_split)
       RW(WgradArgs, KT) PTR(WgradArgs, slab) PTR(WgradArgs, bslab) RW(WgradArgs, R)
       RW(WgradArgs, blocks_per_split) PTR(WgradArgs, dy_code) PTR(WgradArgs, zero) RW(WgradArgs, dHp) RW(WgradArgs, dWp)
-      RW(WgradArgs, dbg) PTR(WgradArgs, ts) PTR(WgradArgs, ts2);
+      RW(WgradArgs, dbg) PTR(WgradArgs, ts) PTR(WgradArgs, ts2) RW(WgradArgs, opt) RW(WgradArgs, opt_w)
+      RW(WgradArgs, opt_b);
 
   py::class_<DenseFwdArgs>(m, "DenseFwdArgs")
       .def(py::init<>())

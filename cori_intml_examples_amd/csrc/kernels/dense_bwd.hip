@@ -18,7 +18,10 @@
 //   * the bias gradient (column sums of dH) is summed from the dH fragments the MFMAs already
 //     read (8 rows per lane), in the feature-group-0 workgroups;
 //   * the four waves' partials are summed in fixed order through LDS (deterministic) and
-//     stored as coalesced float4 rows of the [split][K][N] slab, the layout slab_reduce reads.
+//     stored as coalesced float4 rows of the [split][K][N] slab, the layout slab_reduce reads;
+//     with one split that slab IS the Keras gradient, and the kernel can apply the optimizer
+//     update to those elements right there (WgradArgs::opt_w), so the layer never enters
+//     the end-of-step reduction.
 //
 // dense_dx_kernel<NTC>  (grid: 64-row groups x n groups)
 //   * a wave owns 16 rows x NTC*16 columns: each dH fragment feeds NTC MFMAs;
@@ -33,6 +36,7 @@
 #include <stdexcept>
 
 #include "dense_body.h"
+#include "optim_math.h"
 
 namespace {
 constexpr int DW_LDA = 48;   // A tile row stride (elements): 32 features + pad
@@ -54,6 +58,31 @@ struct DwGeom {
 // than the plain stride puts it, so rows 8g+q of the lane groups g = 0/1 (and 2/3) of a
 // transposed read land in opposite bank halves (the blocks never overlap)
 __device__ __forceinline__ int dw_row(int r, int ld) { return r * ld + (r >> 3) * 64; }
+
+// the Keras update of one element, optimizer kind chosen at run time (wave-uniform)
+__device__ __forceinline__ void dw_opt(const OptimArgs& o, float& p, float g, float* s0, float* s1) {
+  switch (o.kind) {
+    case OPT_ADAM: opt_update<OPT_ADAM>(o, o.st, p, g, s0, s1); break;
+    case OPT_NADAM: opt_update<OPT_NADAM>(o, o.st, p, g, s0, s1); break;
+    case OPT_ADADELTA: opt_update<OPT_ADADELTA>(o, o.st, p, g, s0, s1); break;
+    case OPT_RMSPROP: opt_update<OPT_RMSPROP>(o, o.st, p, g, s0, s1); break;
+    default: opt_update<OPT_SGD>(o, o.st, p, g, s0, s1); break;
+  }
+}
+
+// fused update of 4 consecutive elements [e, e+4) whose gradient is g; p / s0 / s1 are
+// their current values (loaded early by the caller)
+__device__ __forceinline__ void dw_opt4(const OptimArgs& o, size_t e, const f32x4& g, f32x4 p, f32x4 s0, f32x4 s1) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float pq = p[q], m = s0[q], v = s1[q];
+    dw_opt(o, pq, g[q] * o.grad_scale, &m, &v);
+    p[q] = pq, s0[q] = m, s1[q] = v;
+  }
+  *reinterpret_cast<f32x4*>(o.p + e) = p;
+  if (o.s0) *reinterpret_cast<f32x4*>(o.s0 + e) = s0;
+  if (o.s1) *reinterpret_cast<f32x4*>(o.s1 + e) = s1;
+}
 }   // namespace
 
 size_t dense_wgrad_lds_bytes(int kg, int ntt) {
@@ -68,7 +97,7 @@ size_t dense_wgrad_lds_bytes(int kg, int ntt) {
   return std::max(stage, red + 16 * 128 * 4);
 }
 
-template <int KG, int NTT>
+template <int KG, int NTT, bool OPT>
 __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int bx, const int by, const int bz,
                                                  char* smem) {
   using G = DwGeom<NTT>;
@@ -120,6 +149,29 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
     for (int kt = 0; kt < KG; ++kt) acc[kt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
+  // OPT: the optimizer state of the elements this thread will finalise is loaded now, so
+  // its latency hides behind the chunk loop instead of trailing the reduction
+  const int ld = a.NT * 16;
+  constexpr int C4 = NTT * 4;                                    // float4 per 16-feature row
+  constexpr int NQ = (16 * C4 + 255) / 256;                      // float4 per thread per k-tile
+  f32x4 op[OPT ? KG : 1][NQ], om[OPT ? KG : 1][NQ], ov[OPT ? KG : 1][NQ];
+  if constexpr (OPT) {
+    const OptimArgs& o = a.opt;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < KG; ++kt)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int e = tid + 256 * q, row = e / C4, c4 = e - row * C4;
+        const int f = f0 + kt * 16 + row, n = n0 + c4 * 4;
+        const bool ok = e < 16 * C4 && f < a.Ktiles * 16 && n < ld;
+        const size_t x = ok ? (size_t)a.opt_w + (size_t)f * ld + n : 0;
+        op[kt][q] = ok ? *reinterpret_cast<const f32x4*>(o.p + x) : z;
+        om[kt][q] = (ok && o.s0) ? *reinterpret_cast<const f32x4*>(o.s0 + x) : z;
+        ov[kt][q] = (ok && o.s1) ? *reinterpret_cast<const f32x4*>(o.s1 + x) : z;
+      }
+  }
+
   // fragment read rows: lane reads rows 8g + (i>>2) (lo) and +4 (hi), 4 columns at 4*(i&3)
   const int rd = 8 * g + (i >> 2);
   if (wave < nchunks) issue(wave);
@@ -153,7 +205,6 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);                   // [4 waves][16][LDR]
   float* bred = red + 4 * 16 * G::LDR;                           // [4 waves][4 groups][128]
-  const int ld = a.NT * 16;
   float* slab = a.slab + (size_t)bx * a.Ktiles * 16 * ld;
   if (do_bias) {
 #pragma unroll
@@ -167,14 +218,19 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
 #pragma unroll
       for (int j = 0; j < 4; ++j) rw[(4 * g + j) * G::LDR + nt * 16 + i] = acc[kt][nt][j];
     __syncthreads();
-    constexpr int C4 = NTT * 4;                                  // float4 per row
-    for (int e = tid; e < 16 * C4; e += 256) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int e = tid + 256 * q;
+      if (e >= 16 * C4) break;
       const int row = e / C4, c4 = e - row * C4;
       const int f = f0 + kt * 16 + row, n = n0 + c4 * 4;
       f32x4 s = *reinterpret_cast<const f32x4*>(red + row * G::LDR + c4 * 4);
 #pragma unroll
       for (int w = 1; w < 4; ++w) s += *reinterpret_cast<const f32x4*>(red + (w * 16 + row) * G::LDR + c4 * 4);
-      if (f < a.Ktiles * 16 && n < ld) *reinterpret_cast<f32x4*>(slab + (size_t)f * ld + n) = s;
+      if (f < a.Ktiles * 16 && n < ld) {
+        *reinterpret_cast<f32x4*>(slab + (size_t)f * ld + n) = s;
+        if constexpr (OPT) dw_opt4(a.opt, (size_t)a.opt_w + (size_t)f * ld + n, s, op[kt][q], om[kt][q], ov[kt][q]);
+      }
     }
     __syncthreads();
   }
@@ -183,7 +239,17 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
 #pragma unroll
     for (int q = 0; q < 16; ++q) b += bred[q * 128 + tid];     // fixed order: wave-major, group
     a.bslab[(size_t)bx * ld + n0 + tid] = b;
+    if (OPT && a.opt_b >= 0) {
+      const OptimArgs& o = a.opt;
+      const int e = a.opt_b + n0 + tid;
+      float p = o.p[e], s0 = o.s0 ? o.s0[e] : 0.f, s1 = o.s1 ? o.s1[e] : 0.f;
+      dw_opt(o, p, b * o.grad_scale, &s0, &s1);
+      o.p[e] = p;
+      if (o.s0) o.s0[e] = s0;
+      if (o.s1) o.s1[e] = s1;
+    }
   }
+  if (OPT && a.opt.defer_pack && bx == 0 && by == 0 && bz == 0 && tid == 0) a.opt.st->packs_stale = 1;
 }
 
 template <int NTC>
@@ -244,10 +310,10 @@ __device__ __forceinline__ void dense_dx_body(const DenseFwdArgs& a, const int b
 
 size_t dense_dx_lds_bytes(int ntc) { return (size_t)4 * 16 * (ntc * 16 + 4) * 4; }
 
-template <int KG, int NTT>
+template <int KG, int NTT, bool OPT>
 __global__ __launch_bounds__(256) void dense_wgrad_kernel(const WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  dense_wgrad_body<KG, NTT>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  dense_wgrad_body<KG, NTT, OPT>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 template <int NTC>
@@ -257,7 +323,7 @@ __global__ __launch_bounds__(256) void dense_dx_kernel(const DenseFwdArgs a) {
 }
 
 // dX workgroups [0, n_x) first (grid x-major over 64-row groups), then the wgrad ones
-template <int KG, int NTT, int NTC>
+template <int KG, int NTT, bool OPT, int NTC>
 __global__ __launch_bounds__(256) void dense_bwd_pair_kernel(const WgradArgs wa, const DenseFwdArgs da,
                                                              const int n_x, const int xgx, const int wgx,
                                                              const int wgy) {
@@ -269,17 +335,20 @@ __global__ __launch_bounds__(256) void dense_bwd_pair_kernel(const WgradArgs wa,
     id -= n_x;
     const int bx = id % wgx;
     id /= wgx;
-    dense_wgrad_body<KG, NTT>(wa, bx, id % wgy, id / wgy, smem);
+    dense_wgrad_body<KG, NTT, OPT>(wa, bx, id % wgy, id / wgy, smem);
   }
 }
 
 // Host checks of the shapes the kernels assume (a mismatch would read or write out of range).
 static void dense_wgrad_check(const WgradArgs& a, int kg, int ntt, int splits) {
-  if (!((kg == 1 || kg == 2) && (ntt == 1 || ntt == 2 || ntt == 4 || ntt == 8)))
+  if (!(kg == 2 && (ntt == 1 || ntt == 2 || ntt == 4 || ntt == 8)))
     throw std::runtime_error("dense_wgrad: unsupported (kg, ntt)");
   if (a.Cs_in % 8 || a.Cs_dy % 8 || a.px_per_split <= 0 || a.px_per_split % 32 ||
       (long long)splits * a.px_per_split < a.P || a.KH != 1 || a.KW != 1)
     throw std::runtime_error("dense_wgrad: geometry");
+  if (a.opt_w >= 0 && (splits != 1 || a.opt.p == nullptr || a.opt.st == nullptr || a.opt_w % 4 ||
+                       (a.NT * 16) % 4))
+    throw std::runtime_error("dense_wgrad: fused optimizer needs one split and float4-aligned rows");
 }
 static void dense_dx_check(const DenseFwdArgs& a, int ntc) {
   if (!(ntc == 1 || ntc == 2 || ntc == 4) || a.mode != 1 || a.splits != 1 || a.bt.pCs % 8 || a.Ks % 8)
@@ -293,16 +362,17 @@ static dim3 dense_dx_grid(const DenseFwdArgs& a, int ntc) {
   return dim3((a.M + 63) / 64, (a.NT + ntc - 1) / ntc);
 }
 
-#define DW_CASES(X) X(1, 1) X(1, 2) X(1, 4) X(1, 8) X(2, 1) X(2, 2) X(2, 4) X(2, 8)
+#define DW_CASES(X) X(2, 1) X(2, 2) X(2, 4) X(2, 8)
 
 void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s) {
   dense_wgrad_check(a, kg, ntt, splits);
   const dim3 grid = dense_wgrad_grid(a, kg, ntt, splits);
   const size_t lds = dense_wgrad_lds_bytes(kg, ntt);
-#define X(KG_, NT_)                                                                 \
-  if (kg == KG_ && ntt == NT_) {                                                    \
-    hipLaunchKernelGGL((dense_wgrad_kernel<KG_, NT_>), grid, dim3(256), lds, s, a); \
-    return;                                                                         \
+#define X(KG_, NT_)                                                                         \
+  if (kg == KG_ && ntt == NT_) {                                                            \
+    if (a.opt_w >= 0) hipLaunchKernelGGL((dense_wgrad_kernel<KG_, NT_, true>), grid, dim3(256), lds, s, a); \
+    else hipLaunchKernelGGL((dense_wgrad_kernel<KG_, NT_, false>), grid, dim3(256), lds, s, a);             \
+    return;                                                                                 \
   }
   DW_CASES(X)
 #undef X
@@ -317,20 +387,19 @@ void launch_dense_dx(const DenseFwdArgs& a, int ntc, hipStream_t s) {
   else hipLaunchKernelGGL((dense_dx_kernel<4>), grid, dim3(256), lds, s, a);
 }
 
-template <int KG, int NTT>
-static void pair_t(const WgradArgs& wa, const DenseFwdArgs& da, int ntc, int splits, size_t lds, hipStream_t s) {
-  const dim3 wg = dense_wgrad_grid(wa, KG, NTT, splits), xg = dense_dx_grid(da, ntc);
+template <int KG, int NTT, bool OPT, int NTC>
+static void pair_l(const WgradArgs& wa, const DenseFwdArgs& da, int splits, size_t lds, hipStream_t s) {
+  const dim3 wg = dense_wgrad_grid(wa, KG, NTT, splits), xg = dense_dx_grid(da, NTC);
   const int n_x = xg.x * xg.y, n_w = wg.x * wg.y * wg.z;
-  const dim3 grid(n_x + n_w);
-  if (ntc == 1)
-    hipLaunchKernelGGL((dense_bwd_pair_kernel<KG, NTT, 1>), grid, dim3(256), lds, s, wa, da, n_x, (int)xg.x,
-                       (int)wg.x, (int)wg.y);
-  else if (ntc == 2)
-    hipLaunchKernelGGL((dense_bwd_pair_kernel<KG, NTT, 2>), grid, dim3(256), lds, s, wa, da, n_x, (int)xg.x,
-                       (int)wg.x, (int)wg.y);
-  else
-    hipLaunchKernelGGL((dense_bwd_pair_kernel<KG, NTT, 4>), grid, dim3(256), lds, s, wa, da, n_x, (int)xg.x,
-                       (int)wg.x, (int)wg.y);
+  hipLaunchKernelGGL((dense_bwd_pair_kernel<KG, NTT, OPT, NTC>), dim3(n_x + n_w), dim3(256), lds, s, wa, da, n_x,
+                     (int)xg.x, (int)wg.x, (int)wg.y);
+}
+
+template <int KG, int NTT, bool OPT>
+static void pair_t(const WgradArgs& wa, const DenseFwdArgs& da, int ntc, int splits, size_t lds, hipStream_t s) {
+  if (ntc == 1) pair_l<KG, NTT, OPT, 1>(wa, da, splits, lds, s);
+  else if (ntc == 2) pair_l<KG, NTT, OPT, 2>(wa, da, splits, lds, s);
+  else pair_l<KG, NTT, OPT, 4>(wa, da, splits, lds, s);
 }
 
 void launch_dense_bwd_pair(const WgradArgs& wa, int kg, int ntt, int splits, const DenseFwdArgs& da, int ntc,
@@ -340,7 +409,8 @@ void launch_dense_bwd_pair(const WgradArgs& wa, int kg, int ntt, int splits, con
   const size_t lds = std::max(dense_wgrad_lds_bytes(kg, ntt), dense_dx_lds_bytes(ntc));
 #define X(KG_, NT_)                                   \
   if (kg == KG_ && ntt == NT_) {                      \
-    pair_t<KG_, NT_>(wa, da, ntc, splits, lds, s);    \
+    if (wa.opt_w >= 0) pair_t<KG_, NT_, true>(wa, da, ntc, splits, lds, s);  \
+    else pair_t<KG_, NT_, false>(wa, da, ntc, splits, lds, s);               \
     return;                                           \
   }
   DW_CASES(X)

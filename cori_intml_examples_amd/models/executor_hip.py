@@ -739,6 +739,13 @@ class BatchPlan:
         self.red_groups.append((lo, hi, descs))
         self._add_group_reduce()
         self.wgrad_slabs = []
+        self.dense_fused_opt = []          # (WgradArgs, params) updated inside dense_wgrad
+        # opt-in: the dense layer's optimizer update inside its (one-split) wgrad kernel.  Measured
+        # slower on RPV at batch 128: the 128 wgrad workgroups move the layer's 14 MB of optimizer
+        # state at per-CU bandwidth (wgrad 6.1 -> 9.7 us) while the end-of-step reduction, which
+        # spreads it over thousands of workgroups, only drops 10.8 -> 8.2 us
+        self.dense_opt_ok = (ex.reducer is None and self.side is None and not self.early_optim
+                             and env_flag("INTML_FUSE_OPTIM", True) and env_flag("INTML_DENSE_OPT", False))
 
         for g, ds in reversed(list(zip(ex.denses, ex.plan.denses))):
             xin = self._src_buf(g.src)
@@ -752,9 +759,23 @@ class BatchPlan:
             # dense_bwd.hip kernels (per-wave pipelined wgrad, vectorised dX epilogue) where the
             # 8-element alignment they assume holds; the generic wgrad / split-K path otherwise
             bwd2 = (env_flag("INTML_DENSE_BWD2", True) and g.src.width % 8 == 0 and g.Ns % 8 == 0)
+            fused_opt = False
             if bwd2:
                 wa, cfg, slab, bslab = self._dense_wgrad_args(xin, g.src.width, self.dense_dh[g.j], g.Ns, g.N, bs,
                                                               ds.dense.use_bias, direct_ptr)
+                # one split + identity layout: the kernel's fixed-order sum IS the Keras
+                # gradient -- write it in place and apply the optimizer there (single GPU,
+                # fused-optimizer step), so the layer skips the end-of-step reduction
+                fused_opt = (self.dense_opt_ok and cfg[2] == 1 and g.src.C == g.src.Cs and g.N % 16 == 0
+                             and sp.offset % 4 == 0)
+                if fused_opt:
+                    grad = store.grad.data_ptr()
+                    wa.slab = grad + 4 * sp.offset
+                    wa.opt = ex._optim_args(False, defer_pack=True)
+                    wa.opt_w = sp.offset
+                    if ds.dense.use_bias:
+                        wa.bslab = grad + 4 * store.spec(ds.dense, "bias").offset
+                        wa.opt_b = store.spec(ds.dense, "bias").offset
                 wl = lambda s, a=wa, c=cfg: K.dense_wgrad(a, c[0], c[1], c[2], s)
             else:
                 wa, cfg, slab, bslab = self._wgrad_args(
@@ -764,13 +785,16 @@ class BatchPlan:
             self.launches.append(("wgrad_dense%d" % g.j, wl, "side"))
             w_at = len(self.launches) - 1
             S, ld = cfg[2], g.NT * 16
-            descs = [] if direct else [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset, sp.numel,
-                                        RED_FLATW, 0, 0, g.src.C, g.N, g.src.Cs)]
+            descs = [] if (direct or fused_opt) else [(slab.data_ptr(), wa.Ktiles * 16 * ld, S, ld, sp.offset,
+                                                        sp.numel, RED_FLATW, 0, 0, g.src.C, g.N, g.src.Cs)]
             lo, hi = sp.offset, sp.offset + sp.numel
             if ds.dense.use_bias:
                 bp_ = store.spec(ds.dense, "bias")
-                descs.append((bslab.data_ptr(), ld, S, ld, bp_.offset, bp_.numel, RED_BIAS, 0, 0, 0, 0, 0))
+                if not fused_opt:
+                    descs.append((bslab.data_ptr(), ld, S, ld, bp_.offset, bp_.numel, RED_BIAS, 0, 0, 0, 0, 0))
                 hi = max(hi, bp_.offset + bp_.numel)
+            if fused_opt:
+                self.dense_fused_opt.append((wa, hi - lo))
             self.red_groups.append((lo, hi, descs))
             self._add_group_reduce()
             if g.KSb:
@@ -1223,7 +1247,7 @@ class BatchPlan:
         a.NT = NT
         a.P = bs
         ntt = _pow2_le(NT, 8)
-        kg = int(os.environ.get("INTML_DW_KG", "2"))
+        kg = 2
         groups = cdiv(a.Ktiles, kg) * cdiv(NT, ntt)
         per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
         s_budget = max(1, (int(os.environ.get("INTML_DW_SLAB_MB", "8")) << 20) // per_split_bytes)
@@ -1273,8 +1297,15 @@ class BatchPlan:
             limit = 1 << 62 if one else int(os.environ.get("INTML_BUCKET_BYTES", 1 << 20))
             # ... with the optimizer fused into it when its table covers every parameter
             covered = sum(d[5] for _, _, ds in self.red_groups for d in ds)
+            covered += sum(n for _, n in self.dense_fused_opt)
             self.optim_fused = (one and not self.early_optim and covered == ex.store.numel
                                 and env_flag("INTML_FUSE_OPTIM", True))
+            if not self.optim_fused:
+                # the step ends with a full optimizer launch after all: the dense layers keep
+                # writing their gradient in place, but leave the update to it
+                for wa, _ in self.dense_fused_opt:
+                    wa.opt_w, wa.opt_b = -1, -1
+                self.dense_fused_opt = []
             bucket_groups, cur, nb = [], [], 0
             for gi, (lo, hi) in enumerate(groups):
                 cur.append(gi)

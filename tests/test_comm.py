@@ -61,15 +61,19 @@ def test_native_comm_engine_gpu(tmp_path):
     # (adaptive buckets: the 2.2 MB RPV gradient is ONE fused bucket, linear graph)
     assert cap["n_comm_launches"] == 2 * len(cap["buckets"]) == 2
     assert rep["rccl_nranks"] == 1
-    # size-1 all-reduce is exact: both DP modes agree bit for bit; against the single-GPU
-    # step (whose optimizer is fused into the gradient reduction) only fp contraction differs
+    # size-1 all-reduce is exact: both DP modes agree bit for bit.  Against the single-GPU
+    # step (optimizer fused into the gradient reduction / the dense wgrad) only fp
+    # contraction differs -- but Adam turns a last-ulp difference of a near-zero gradient
+    # into up to a full +-lr step, so bound the distribution (99.9% of weights within 1e-5)
+    # and the worst element by 2 lr (4 steps at lr 1e-3), not the max alone
     assert rep["train"]["captured_vs_segmented"] == 0.0, rep["train"]
-    assert cap["max_abs_diff"] < 1e-4, cap
-    assert not seg["comm_in_graph"] and seg["max_abs_diff"] < 1e-4, seg
+    for r in (cap, seg):
+        assert r["p999_abs_diff"] < 1e-5 and r["max_abs_diff"] < 2e-3, r
+    assert not seg["comm_in_graph"], seg
     assert rep["train"]["bf16_wire"]["rel_diff"] < 0.05, rep["train"]["bf16_wire"]
     xg = rep["train"]["xgmi"]
     assert xg["active"] and xg["launches"] == ["xgmi_allreduce_optim_b0"], xg
-    assert xg["max_abs_diff"] < 1e-4, xg
+    assert xg["p999_abs_diff"] < 1e-5 and xg["max_abs_diff"] < 2e-3, xg
     assert rep["abort_raises"] and rep["healthy"], rep
 
 
