@@ -37,6 +37,7 @@ void launch_dense_dx(const DenseFwdArgs& a, int ntc, hipStream_t s);
 void launch_dense_bwd_pair(const WgradArgs& wa, int kg, int ntt, int splits, const DenseFwdArgs& da, int ntc,
                            hipStream_t s);
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s);
+int conv_stack_threads();
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
 int gather_gx(int R);
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s);
@@ -301,6 +302,7 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.attr("MAX_STACK") = MAX_STACK;
   m.attr("MAX_STACK_SPLIT") = MAX_STACK_SPLIT;
+  m.attr("STACK_THREADS") = conv_stack_threads();
   m.def("conv_stack_fwd", [](const ConvStackArgs& a, uintptr_t s) {
     launch_conv_stack_fwd(a, S(s)); check_last("conv_stack_fwd"); });
   m.def("slab_reduce", [](uintptr_t grad, int lo, int hi, const RedTable& t, uintptr_t s) {

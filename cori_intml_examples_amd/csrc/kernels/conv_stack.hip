@@ -18,7 +18,7 @@
 // halo rows the next layer's range needs (host-computed, ConvStackArgs::rows).  With two
 // bands per image the batch-128 launch fills all 256 CUs for ~35% recomputed conv1 rows.
 //
-// Per layer (8 waves): m-tiles are 16 output pixels (or 4 pooling windows x 4 positions,
+// Per layer (12 waves): m-tiles are 16 output pixels (or 4 pooling windows x 4 positions,
 // so the 2x2 max-pool is register-local: an MFMA accumulator row group is one window),
 // TM m-tiles x NT n-tiles per wave; A fragments are one ds_read_b128 per k-step from the
 // halo image (two ds_read_b64 for the 4-channel input), B fragments come from the layer's
@@ -29,7 +29,10 @@
 // per-layer kernels.
 #include "args.h"
 
-#define STACK_THREADS 512
+// 12 waves (3 per SIMD): measured 25.4 -> 24.8 us (B=128) and 125.7 -> 115.0 us (B=1024)
+// over 8 waves -- the per-layer tile loops are latency-bound, one workgroup per CU (LDS);
+// 16 waves would cap the kernel at 128 VGPRs and spill
+#define STACK_THREADS 768
 #define STACK_WAVES (STACK_THREADS / 64)
 #define LDS __attribute__((address_space(3)))
 
@@ -380,7 +383,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   // Weight packs -> LDS.  Layer 0's synchronously; the later layers' are loaded into
   // registers now (issued after the image, so waiting for the image does not wait for them)
   // and written to LDS only before layer 1 -- their latency hides behind layer 0.
-  constexpr int PF = 8;
+  constexpr int PF = (4096 + STACK_THREADS - 1) / STACK_THREADS;
   // vectors of layers 1, 2, 3 (static indices: the kernarg loads hoist out of the loops)
   const int nv1 = A.n > 1 ? A.L[1].KS * A.L[1].NT * 64 : 0;
   const int nv2 = A.n > 2 ? A.L[2].KS * A.L[2].NT * 64 : 0;
@@ -605,6 +608,8 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     // (no barrier: the next layer writes `codes` / the other buffer only after its own)
   }
 }
+
+int conv_stack_threads() { return STACK_THREADS; }
 
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s) {
   auto k = conv_stack_fwd_kernel;

@@ -34,12 +34,13 @@ fn = [f for (n, f, *_) in bp.launches if n == "conv_stack_fwd"][0]
 a = fn.__defaults__[0]
 nblk = a.B * a.splits
 print("conv_stack: B=%d splits=%d blocks=%d lds_bytes=%d layers=%d" % (a.B, a.splits, nblk, a.lds_bytes, a.n))
-ts = torch.zeros(nblk * 8 * 32, dtype=torch.int64, device=dev)
+nw = ex.K.STACK_THREADS // 64                 # waves per workgroup (stamp rows per block)
+ts = torch.zeros(nblk * nw * 32, dtype=torch.int64, device=dev)
 a.ts = ts.data_ptr()
 for _ in range(20):
     fn(s)
 torch.cuda.synchronize()
-raw = ts.view(nblk, 8, 32).cpu().numpy().astype(np.float64)
+raw = ts.view(nblk, nw, 32).cpu().numpy().astype(np.float64)
 t = raw[:, :, :16] * 0.01   # 100 MHz -> us
 clk = raw[:, :, 16:]
 last_i = 1 + 4 * a.n
