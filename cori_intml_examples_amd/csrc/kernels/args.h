@@ -263,6 +263,16 @@ struct RedTable {
   RedDesc d[MAX_RED];
 };
 
+// Optional extra workgroups of the dual conv backward launch: the fused reduction + optimizer
+// of an EARLY bucket (gradients final before that launch, weights no later kernel of the step
+// reads), run in n_r workgroups of the same grid (after the conv ones, or before: rfirst).
+struct DualExtra {
+  RedTable rt;
+  OptimArgs ro;
+  float* grad = nullptr;
+  int n_r = 0, rfirst = 0;
+};
+
 // Fused data-parallel all-reduce + optimizer over xGMI peer memory (xgmi.hip).  Every rank
 // owns chunk r = [r*chunk, (r+1)*chunk) of the flat gradient.  One launch per step:
 //   1. push: workgroup w sends its slice [w*sub, (w+1)*sub) of EVERY chunk j to owner j's

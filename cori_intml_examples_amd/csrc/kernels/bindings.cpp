@@ -28,7 +28,7 @@ int dense_groups(int M, int NT, int KS);
 bool dense_big(int NT, int KS);
 void launch_head(const HeadArgs& a, hipStream_t s);
 bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits,
-                      hipStream_t s);
+                      const DualExtra& x, hipStream_t s);
 bool launch_dense_bwd_dual(const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da,
                            hipStream_t s);
 void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s);
@@ -295,11 +295,22 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("dense_bwd_pair", [](const WgradArgs& wa, int kg, int ntt, int splits, const DenseFwdArgs& da, int ntc,
                              uintptr_t s) {
     launch_dense_bwd_pair(wa, kg, ntt, splits, da, ntc, S(s)); check_last("dense_bwd_pair"); });
-  m.def("dual_halo", [](const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits, uintptr_t s) {
-    const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, S(s));
-    check_last("dual_halo");
-    return ok;
-  });
+  m.def(
+      "dual_halo",
+      [](const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits, uintptr_t s,
+         const RedTable* rt, const OptimArgs* ro, uintptr_t rgrad, int rfirst) {
+        DualExtra x;
+        if (rt && ro && rt->nblocks > 0) {
+          x.rt = *rt, x.ro = *ro, x.grad = reinterpret_cast<float*>(rgrad);
+          x.n_r = rt->nblocks, x.rfirst = rfirst;
+        }
+        const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, x, S(s));
+        check_last("dual_halo");
+        return ok;
+      },
+      py::arg("ca"), py::arg("ntc"), py::arg("wa"), py::arg("MT"), py::arg("NTT"), py::arg("splits"), py::arg("s"),
+      py::arg("rt") = nullptr, py::arg("ro") = nullptr, py::arg("rgrad") = 0, py::arg("rfirst") = 0,
+      "dual wgrad + dgrad launch; with (rt, ro, rgrad) it also runs that table's reduction + optimizer");
   m.attr("MAX_STACK") = MAX_STACK;
   m.attr("MAX_STACK_SPLIT") = MAX_STACK_SPLIT;
   m.attr("STACK_THREADS") = conv_stack_threads();

@@ -7,7 +7,8 @@
 // co-scheduled, the dgrad workgroups fill the CUs the wgrad ones leave idle and the step pays
 // one kernel boundary (launch ramp + drain + L2 writeback, ~5 us here) instead of two.
 // Wgrad workgroups come first: they are the long pole, so they are dispatched first.
-// The LDS request is the max of the two bodies' needs.
+// The LDS request is the max of the two bodies' needs.  Optionally the launch also carries an
+// early bucket's reduction + optimizer (DualExtra) in extra workgroups.
 #include <algorithm>
 
 #include "dual_halo_body.h"
@@ -18,14 +19,14 @@ size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT);
 // Returns false (nothing launched) when the pair is not a supported combination; the caller
 // then launches the two kernels separately.
 bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits,
-                      hipStream_t s) {
+                      const DualExtra& x, hipStream_t s) {
   if (ca.Cs_in == 4 || wa.Cs_in == 4 || ca.KS <= 2) return false;   // 4-channel / tiny-K variants
   const int cgy = (ca.NT + ntc - 1) / ntc;
   const int cgx = ca.B * ((ca.Ho + ca.R - 1) / ca.R);
   const dim3 wg(splits, (wa.NT + NTT - 1) / NTT, (wa.Ktiles + MT - 1) / MT);
   const int mtw = (MT + (wa.bslab ? 1 : 0) + 3) / 4;
   const size_t lds = std::max(conv_halo_lds_bytes(ca, ntc), wgrad_halo_lds_bytes(wa, MT, NTT));
-  if (lds > 160 * 1024) return false;
+  if (lds > 160 * 1024 || (x.n_r && lds < 1024)) return false;
   // dgrad m-tiles per wave per pass: the TM in {4, 2} that minimises the busiest wave's
   // tile count over the block (ties -> larger TM: more fragment reuse); TM = 1 only when
   // the block has <= 4 tiles (measured: TM 1 loses its fragment reuse on longer blocks)
@@ -40,10 +41,10 @@ bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT
     if (load < best) { best = load; tm = t; }
   }
   switch (ntc) {
-    case 1: return dual_launch_n1(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, s);
-    case 2: return dual_launch_n2(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, s);
-    case 4: return dual_launch_n4(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, s);
-    case 8: return dual_launch_n8(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, s);
+    case 1: return dual_launch_n1(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, x, s);
+    case 2: return dual_launch_n2(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, x, s);
+    case 4: return dual_launch_n4(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, x, s);
+    case 8: return dual_launch_n8(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, x, s);
   }
   return false;
 }

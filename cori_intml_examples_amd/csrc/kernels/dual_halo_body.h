@@ -3,12 +3,22 @@
 #pragma once
 #include "conv_halo_body.h"
 #include "wgrad_halo_body.h"
+#include "reduce_body.h"
 
 template <int NTC, int MTW, int NTT, int TM>
 __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, const WgradArgs wa, const int MT,
-                                                        const int n_w, const int wgx, const int wgy, const int cgx) {
+                                                        const int n_w, const int wgx, const int wgy, const int cgx,
+                                                        const DualExtra x) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int id = blockIdx.x;
+  if (x.n_r) {   // early-bucket reduction + optimizer workgroups
+    const int r = x.rfirst ? id : id - (int)gridDim.x + x.n_r;
+    if (r >= 0 && r < x.n_r) {
+      reduce_optim_block_rt(x.grad, x.rt, x.ro, r, reinterpret_cast<float*>(smem));
+      return;
+    }
+    if (x.rfirst) id -= x.n_r;
+  }
   if (wa.ts && threadIdx.x == 0) wa.ts[2 * blockIdx.x] = wall_clock64();
   if (id < n_w) {
     const int bx = id % wgx;
@@ -26,26 +36,27 @@ __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, con
 
 template <int NTC, int MTW, int NTT, int TM>
 static void dual_t(const ConvMMArgs& ca, const WgradArgs& wa, int MT, dim3 wg, int cgx, int cgy, size_t lds,
-                   hipStream_t s) {
+                   const DualExtra& x, hipStream_t s) {
   auto k = dual_halo_kernel<NTC, MTW, NTT, TM>;
   if (lds > 65536) hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int n_w = wg.x * wg.y * wg.z;
-  hipLaunchKernelGGL(k, dim3(n_w + cgx * cgy), dim3(256), lds, s, ca, wa, MT, n_w, (int)wg.x, (int)wg.y, cgx);
+  hipLaunchKernelGGL(k, dim3(n_w + cgx * cgy + x.n_r), dim3(256), lds, s, ca, wa, MT, n_w, (int)wg.x, (int)wg.y, cgx,
+                     x);
 }
 
 // tm: m-tiles per wave per pass of the dgrad body (TM_DEFAULT, or 1 / 2 for NTC <= 2 when
 // that evens out the four waves' tile counts on small row blocks)
 template <int NTC>
 static bool dual_w(const ConvMMArgs& ca, const WgradArgs& wa, int MT, int NTT, int mtw, int tm, dim3 wg, int cgx,
-                   int cgy, size_t lds, hipStream_t s) {
+                   int cgy, size_t lds, const DualExtra& x, hipStream_t s) {
   constexpr int TMD = NTC >= 8 ? 2 : 4;
 #define C(M_, N_)                                                          \
   if (mtw <= M_ && NTT == N_) {                                            \
     if constexpr (NTC <= 2) {                                              \
-      if (tm == 1) { dual_t<NTC, M_, N_, 1>(ca, wa, MT, wg, cgx, cgy, lds, s); return true; } \
-      if (tm == 2) { dual_t<NTC, M_, N_, 2>(ca, wa, MT, wg, cgx, cgy, lds, s); return true; } \
+      if (tm == 1) { dual_t<NTC, M_, N_, 1>(ca, wa, MT, wg, cgx, cgy, lds, x, s); return true; } \
+      if (tm == 2) { dual_t<NTC, M_, N_, 2>(ca, wa, MT, wg, cgx, cgy, lds, x, s); return true; } \
     }                                                                      \
-    dual_t<NTC, M_, N_, TMD>(ca, wa, MT, wg, cgx, cgy, lds, s);            \
+    dual_t<NTC, M_, N_, TMD>(ca, wa, MT, wg, cgx, cgy, lds, x, s);            \
     return true;                                                           \
   }
   C(1, 1) C(2, 1) C(4, 1) C(1, 2) C(2, 2) C(4, 2) C(1, 4) C(2, 4) C(4, 4) C(1, 8) C(2, 8)
@@ -55,7 +66,7 @@ static bool dual_w(const ConvMMArgs& ca, const WgradArgs& wa, int MT, int NTT, i
 
 #define DUAL_N_DECL(N)                                                                                        \
   bool dual_launch_n##N(const ConvMMArgs& ca, const WgradArgs& wa, int MT, int NTT, int mtw, int tm, dim3 wg, \
-                        int cgx, int cgy, size_t lds, hipStream_t s)
+                        int cgx, int cgy, size_t lds, const DualExtra& x, hipStream_t s)
 DUAL_N_DECL(1);
 DUAL_N_DECL(2);
 DUAL_N_DECL(4);

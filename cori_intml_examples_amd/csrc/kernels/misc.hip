@@ -12,6 +12,7 @@
 //                            packs the MFMA kernels read scattered out in the same pass
 #include "args.h"
 #include "optim_math.h"
+#include "reduce_body.h"
 
 // Step bookkeeping (one thread): iteration counter, LR decay and the optimizer's
 // bias-correction scalars for this step.  (The data cursor is advanced by the head kernel,
@@ -80,114 +81,19 @@ __device__ __forceinline__ void gather_block(const GatherArgs& a, const StepStat
     for (int c = threadIdx.x; c < C; c += 256) a.yb[(size_t)row * C + c] = ys[(size_t)src * C + c];
 }
 
-// ---------------------------------------------------------------------------------------
-// Each descriptor owns a contiguous range of workgroups; a workgroup covers E = 256/tpe
-// consecutive elements: thread t -> element t % E (consecutive lanes read consecutive
-// addresses of one slab: coalesced) and split-lane t / E (the tpe split-lanes of an
-// element sum interleaved subsets of <= 4 of the S slabs, loads all in flight: the
-// reduction is one memory round trip deep however many slabs there are).  The tpe
-// partials are combined by a fixed-order LDS tree -> bitwise reproducible.
-// Returns true on the thread that holds the final sum of element `dst` (in `val`).
-__device__ __forceinline__ bool slab_reduce_elem(const RedTable& tab, float* red, int& dst, float& val) {
-  int di = 0;
-  while (di + 1 < tab.n && (int)blockIdx.x >= tab.d[di + 1].blk0) ++di;
-  const RedDesc& d = tab.d[di];
-  const int tpe = d.tpe;
-  const int E = 256 / tpe;
-  const int el = (int)threadIdx.x % E;
-  const int lane = (int)threadIdx.x / E;
-  const int le = ((int)blockIdx.x - d.blk0) * E + el;
-  float acc = 0.f;
-  const bool in = le < d.numel;
-  if (in) {
-    size_t src;
-    if (d.type == RED_CONVW) {   // keras (ky,kx,ci,co) -> slab[k = tap*Cs + ci][n = co]
-      const int co = le % d.Cout;
-      const int t2 = le / d.Cout;
-      const int ci = t2 % d.Cin;
-      const int tap = t2 / d.Cin;
-      src = (size_t)(tap * d.Cs + ci) * d.ld + co;
-    } else if (d.type == RED_FLATW) {   // keras (k, n) -> slab[padded k][n]
-      const int n = le % d.Cout;
-      const int k = le / d.Cout;
-      src = (size_t)flat_keras_to_padded(k, d.Cin, d.Cs) * d.ld + n;
-    } else {   // RED_BIAS / plain: slab[s][le]
-      src = (size_t)le;
-    }
-    const float* p = d.slab + src;
-    const size_t st = (size_t)d.stride_s;
-    // 8 independent loads per round (all issued before the first add), fixed summation order
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int s = lane;
-    for (; s + 7 * tpe < d.S; s += 8 * tpe) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(s + u * tpe) * st];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] += v[u];
-    }
-#pragma unroll
-    for (int u = 0; u < 7; ++u)
-      if (s + u * tpe < d.S) a[u] += p[(size_t)(s + u * tpe) * st];
-    acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-  }
-  dst = d.dst_off + le;
-  if (tpe == 1) {
-    val = acc;
-    return in;
-  }
-  // fixed-order tree over the tpe split-lanes (bitwise reproducible)
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int off = tpe >> 1; off > 0; off >>= 1) {
-    if (lane < off) red[threadIdx.x] += red[threadIdx.x + off * E];
-    __syncthreads();
-  }
-  if (lane != 0 || !in) return false;
-  val = red[el];
-  return true;
-}
-
-// vec4 descriptors (identity layout): thread -> 4 consecutive elements, float4 slab loads in
-// fixed split order (the same per-element order as slab_reduce_elem with tpe = 1).
-__device__ __forceinline__ int red_desc(const RedTable& tab) {
-  int di = 0;
-  while (di + 1 < tab.n && (int)blockIdx.x >= tab.d[di + 1].blk0) ++di;
-  return di;
-}
-
-__device__ __forceinline__ bool slab_reduce_vec4(const RedDesc& d, int& e, float4& g) {
-  const int le = (((int)blockIdx.x - d.blk0) * 256 + (int)threadIdx.x) * 4;
-  if (le >= d.numel) return false;
-  const float* p = d.slab + le;
-  float4 v[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-    if (s < d.S) v[s] = *reinterpret_cast<const float4*>(p + (size_t)s * d.stride_s);
-  float4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};   // a[s % 2], like the scalar path's a[u]
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-    if (s < d.S) {
-      float4& a = (s & 1) ? a1 : a0;
-      a.x += v[s].x; a.y += v[s].y; a.z += v[s].z; a.w += v[s].w;
-    }
-  g = float4{a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w};
-  e = d.dst_off + le;
-  return true;
-}
-
 __global__ __launch_bounds__(256) void slab_reduce_kernel(float* __restrict__ grad, const RedTable tab) {
   __shared__ float red[256];
-  const RedDesc& d = tab.d[red_desc(tab)];
+  const int blk = blockIdx.x;
+  const RedDesc& d = tab.d[red_desc(tab, blk)];
   if (d.vec4) {
     int e;
     float4 g;
-    if (slab_reduce_vec4(d, e, g)) *reinterpret_cast<float4*>(grad + e) = g;
+    if (slab_reduce_vec4(d, blk, e, g)) *reinterpret_cast<float4*>(grad + e) = g;
     return;
   }
   int e;
   float v;
-  if (slab_reduce_elem(tab, red, e, v)) grad[e] = v;
+  if (slab_reduce_elem(tab, blk, red, e, v)) grad[e] = v;
 }
 
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s) {
@@ -403,47 +309,14 @@ void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Final slab reduction fused with the optimizer (single GPU: nothing sits between them).
-// The thread that produces an element's gradient applies the Keras update to it at once:
-// the optimizer's own launch and its re-read of the gradient go away.  Used only when the
-// reduction table covers every parameter (no gradient written directly by its kernel).
+// Final slab reduction fused with the optimizer (single GPU: nothing sits between them);
+// the body is reduce_optim_block (reduce_body.h), also run by the early-bucket workgroups
+// of the dual conv backward launch.
 template <int KIND>
 __global__ __launch_bounds__(256) void reduce_optim_kernel(float* __restrict__ grad, const RedTable tab,
                                                            const OptimArgs a) {
   __shared__ float red[256];
-  const RedDesc& dsc = tab.d[red_desc(tab)];
-  if (dsc.vec4) {
-    int e;
-    float4 g;
-    if (slab_reduce_vec4(dsc, e, g)) {
-      *reinterpret_cast<float4*>(grad + e) = g;
-      float4 p = *reinterpret_cast<const float4*>(a.p + e);
-      float4 s0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : float4{0.f, 0.f, 0.f, 0.f};
-      float4 s1 = a.s1 ? *reinterpret_cast<const float4*>(a.s1 + e) : float4{0.f, 0.f, 0.f, 0.f};
-      const float gs = a.grad_scale;
-      opt_update<KIND>(a, a.st, p.x, g.x * gs, &s0.x, &s1.x);
-      opt_update<KIND>(a, a.st, p.y, g.y * gs, &s0.y, &s1.y);
-      opt_update<KIND>(a, a.st, p.z, g.z * gs, &s0.z, &s1.z);
-      opt_update<KIND>(a, a.st, p.w, g.w * gs, &s0.w, &s1.w);
-      *reinterpret_cast<float4*>(a.p + e) = p;
-      if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
-      if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
-    }
-    if (a.defer_pack && blockIdx.x == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
-    return;
-  }
-  int e;
-  float g;
-  if (slab_reduce_elem(tab, red, e, g)) {
-    grad[e] = g;
-    float p = a.p[e];
-    float s0 = a.s0 ? a.s0[e] : 0.f, s1 = a.s1 ? a.s1[e] : 0.f;
-    opt_update<KIND>(a, a.st, p, g * a.grad_scale, &s0, &s1);
-    a.p[e] = p;
-    if (a.s0) a.s0[e] = s0;
-    if (a.s1) a.s1[e] = s1;
-  }
-  if (a.defer_pack && blockIdx.x == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
+  reduce_optim_block<KIND>(grad, tab, a, blockIdx.x, red);
 }
 
 void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, hipStream_t s) {

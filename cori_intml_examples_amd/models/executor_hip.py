@@ -500,6 +500,7 @@ class BatchPlan:
         self.opt_stream = torch.cuda.Stream(device=dev) if self.early_optim else None
         self.opt_at = []
         self.optim_fused = False           # set by _build_reduce
+        self.early_red = None              # (dual launch name, RedTable, span): set by _build_reduce
         # Native RCCL data plane: the bucket all-reduces are part of the launch sequence (on
         # their own comm stream) and captured with the rest of the step into ONE HIP graph.
         red = ex.reducer
@@ -874,7 +875,8 @@ class BatchPlan:
                     # replaces the wgrad launch in place (its slabs are final after it)
                     ntc = self._halo_cfg(a, g.NTd, False, dual=True)
                     dname = "wgrad_dgrad_conv%d" % g.i
-                    self.launches[w_at] = (dname, lambda s, a=a, n=ntc, w=wa, c=cfg: self._dual(a, n, w, c, s), "main")
+                    self.launches[w_at] = (dname, lambda s, a=a, n=ntc, w=wa, c=cfg, nm=dname: self._dual(a, n, w, c, s, nm),
+                                           "main")
                 else:
                     self.launches.append((dname, self._conv_launch(a, g.NTd, False)))
                 self.pack_readers.append((dname, sp.offset, sp.offset + sp.numel))
@@ -1061,11 +1063,20 @@ class BatchPlan:
             K.wgrad(wa, cfg[0], cfg[1], cfg[2], s)
             K.dense_fwd(da, s)
 
-    def _dual(self, a, ntc, wa, cfg, s):
-        K = self.ex.K
-        if not K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s):   # unsupported combination
+    def _dual(self, a, ntc, wa, cfg, s, name=None):
+        K, ex = self.ex.K, self.ex
+        early = self.early_red if (self.early_red is not None and self.early_red[0] == name) else None
+        if early is not None:   # this launch also carries the early bucket's reduction + optimizer
+            opt, grad = ex._optim_args(False, defer_pack=True), ex.store.grad.data_ptr()
+            ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, early[1], opt, grad,
+                             int(env_flag("INTML_EARLY_REDUCE_FIRST", False)))
+        else:
+            ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s)
+        if not ok:   # unsupported combination
             K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
             K.conv_halo(a, ntc, s)
+            if early is not None:
+                K.reduce_optim(ex.store.grad.data_ptr(), early[1], ex._optim_args(False, defer_pack=True), s)
 
     def _halo_cfg(self, a, NT, pool, dual=False):
         """Pick n-tiles per workgroup (weight LDS slice) and R output rows per block: the
@@ -1306,8 +1317,11 @@ class BatchPlan:
                 for wa, _ in self.dense_fused_opt:
                     wa.opt_w, wa.opt_b = -1, -1
                 self.dense_fused_opt = []
+            early = self._early_groups() if self.optim_fused else []
             bucket_groups, cur, nb = [], [], 0
             for gi, (lo, hi) in enumerate(groups):
+                if gi in early:
+                    continue
                 cur.append(gi)
                 nb += (hi - lo) * 4
                 if nb >= limit:
@@ -1346,9 +1360,45 @@ class BatchPlan:
         self.launches, self.bucket_ready = splice_bucket_launches(
             self.launches, inserts,
             [("reduce_b%d", lambda k: (lambda s: self._launch_bucket_reduce(k, s)), "side")] + extra)
-        check_bucket_cover([(lo, hi) for lo, hi, _ in self.bucket_tables], ex.store.numel)
+        spans = [(lo, hi) for lo, hi, _ in self.bucket_tables]
+        if self.early_red is not None:
+            spans.append(self.early_red[2])
+        check_bucket_cover(spans, ex.store.numel)
         if self.early_optim:
             self._insert_optim()
+
+    def _early_groups(self):
+        """Single-GPU fused-optimizer step: the slab groups whose gradients are final before
+        the first dual conv backward launch (the head and dense layers) are reduced and
+        updated by extra workgroups OF that launch (DualExtra) instead of in the end-of-step
+        reduction -- their latency-bound reduce + update then overlaps the conv backward.
+        Only groups no later launch reads the weights of (pack readers), as one contiguous
+        parameter span.  Sets self.early_red = (launch name, RedTable, (lo, hi))."""
+        self.early_red = None
+        if not env_flag("INTML_EARLY_REDUCE", True):
+            return []
+        names = [it[0] for it in self.launches]
+        t = next((i for i, nm in enumerate(names) if nm.startswith("wgrad_dgrad_conv")), None)
+        if t is None:
+            return []
+        early = [gi for gi in range(len(self.red_groups)) if self.red_ready[gi] <= t]
+        late_readers = [(rlo, rhi) for nm, rlo, rhi in self.pack_readers if nm not in names[:t]]
+        early = [gi for gi in early if not any(rlo < self.red_groups[gi][1] and rhi > self.red_groups[gi][0]
+                                               for rlo, rhi in late_readers)]
+        if not early:
+            return []
+        lo = min(self.red_groups[gi][0] for gi in early)
+        hi = max(self.red_groups[gi][1] for gi in early)
+        if sum(self.red_groups[gi][1] - self.red_groups[gi][0] for gi in early) != hi - lo:
+            return []                                  # not one contiguous span
+        descs = [d for gi in early for d in self.red_groups[gi][2]]
+        if not descs or len(descs) > 16:
+            return []
+        tab = self.ex.K.RedTable()
+        for d in sorted(descs, key=lambda d: -d[2]):
+            tab.add(*d)
+        self.early_red = (names[t], tab, (lo, hi))
+        return early
 
     def _launch_optim_comm(self, k, stream):
         """Keras update of bucket k's parameters on the comm stream, right after its
