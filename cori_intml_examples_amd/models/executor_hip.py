@@ -500,7 +500,7 @@ class BatchPlan:
         self.opt_stream = torch.cuda.Stream(device=dev) if self.early_optim else None
         self.opt_at = []
         self.optim_fused = False           # set by _build_reduce
-        self.early_red = None              # (dual launch name, RedTable, span): set by _build_reduce
+        self.early_red = {}                # dual launch name -> (RedTable, span): set by _build_reduce
         # Native RCCL data plane: the bucket all-reduces are part of the launch sequence (on
         # their own comm stream) and captured with the rest of the step into ONE HIP graph.
         red = ex.reducer
@@ -1065,10 +1065,10 @@ class BatchPlan:
 
     def _dual(self, a, ntc, wa, cfg, s, name=None):
         K, ex = self.ex.K, self.ex
-        early = self.early_red if (self.early_red is not None and self.early_red[0] == name) else None
-        if early is not None:   # this launch also carries the early bucket's reduction + optimizer
+        early = (self.early_red or {}).get(name)
+        if early is not None:   # this launch also carries an early bucket's reduction + optimizer
             opt, grad = ex._optim_args(False, defer_pack=True), ex.store.grad.data_ptr()
-            ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, early[1], opt, grad,
+            ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, early[0], opt, grad,
                              int(env_flag("INTML_EARLY_REDUCE_FIRST", False)))
         else:
             ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s)
@@ -1076,7 +1076,7 @@ class BatchPlan:
             K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
             K.conv_halo(a, ntc, s)
             if early is not None:
-                K.reduce_optim(ex.store.grad.data_ptr(), early[1], ex._optim_args(False, defer_pack=True), s)
+                K.reduce_optim(ex.store.grad.data_ptr(), early[0], ex._optim_args(False, defer_pack=True), s)
 
     def _halo_cfg(self, a, NT, pool, dual=False):
         """Pick n-tiles per workgroup (weight LDS slice) and R output rows per block: the
@@ -1361,44 +1361,49 @@ class BatchPlan:
             self.launches, inserts,
             [("reduce_b%d", lambda k: (lambda s: self._launch_bucket_reduce(k, s)), "side")] + extra)
         spans = [(lo, hi) for lo, hi, _ in self.bucket_tables]
-        if self.early_red is not None:
-            spans.append(self.early_red[2])
+        spans += [span for _, span in (self.early_red or {}).values()]
         check_bucket_cover(spans, ex.store.numel)
         if self.early_optim:
             self._insert_optim()
 
     def _early_groups(self):
-        """Single-GPU fused-optimizer step: the slab groups whose gradients are final before
-        the first dual conv backward launch (the head and dense layers) are reduced and
-        updated by extra workgroups OF that launch (DualExtra) instead of in the end-of-step
-        reduction -- their latency-bound reduce + update then overlaps the conv backward.
-        Only groups no later launch reads the weights of (pack readers), as one contiguous
-        parameter span.  Sets self.early_red = (launch name, RedTable, (lo, hi))."""
-        self.early_red = None
+        """Single-GPU fused-optimizer step: slab groups whose gradients are final before a dual
+        conv backward launch (the head and dense layers before the first one, each conv layer
+        before the next) are reduced and updated by extra workgroups OF that launch
+        (DualExtra) instead of in the end-of-step reduction -- their latency-bound reduce +
+        update overlaps the conv backward.  Only groups no later launch reads the weights of
+        (pack readers), each launch's as one contiguous parameter span.  Sets
+        self.early_red = {launch name: (RedTable, (lo, hi))}; returns the groups assigned."""
+        self.early_red = {}
         if not env_flag("INTML_EARLY_REDUCE", True):
             return []
         names = [it[0] for it in self.launches]
-        t = next((i for i, nm in enumerate(names) if nm.startswith("wgrad_dgrad_conv")), None)
-        if t is None:
-            return []
-        early = [gi for gi in range(len(self.red_groups)) if self.red_ready[gi] <= t]
-        late_readers = [(rlo, rhi) for nm, rlo, rhi in self.pack_readers if nm not in names[:t]]
-        early = [gi for gi in early if not any(rlo < self.red_groups[gi][1] and rhi > self.red_groups[gi][0]
-                                               for rlo, rhi in late_readers)]
-        if not early:
-            return []
-        lo = min(self.red_groups[gi][0] for gi in early)
-        hi = max(self.red_groups[gi][1] for gi in early)
-        if sum(self.red_groups[gi][1] - self.red_groups[gi][0] for gi in early) != hi - lo:
-            return []                                  # not one contiguous span
-        descs = [d for gi in early for d in self.red_groups[gi][2]]
-        if not descs or len(descs) > 16:
-            return []
-        tab = self.ex.K.RedTable()
-        for d in sorted(descs, key=lambda d: -d[2]):
-            tab.add(*d)
-        self.early_red = (names[t], tab, (lo, hi))
-        return early
+        duals = [i for i, nm in enumerate(names) if nm.startswith("wgrad_dgrad_conv")]
+        # every dual launch carrying the previous layer's bucket (conv2's in dual conv1, ...) is
+        # opt-in: measured 3% slower on RPV (conv2's many-split slabs stretch dual conv1's tail
+        # by ~3 us, more than the end-of-step reduction sheds)
+        if not env_flag("INTML_EARLY_REDUCE_ALL", False):
+            duals = duals[:1]
+        taken = []
+        for t in duals:
+            late_readers = [(rlo, rhi) for nm, rlo, rhi in self.pack_readers if nm not in names[:t]]
+            grp = [gi for gi in range(len(self.red_groups)) if gi not in taken and self.red_ready[gi] <= t
+                   and not any(rlo < self.red_groups[gi][1] and rhi > self.red_groups[gi][0]
+                               for rlo, rhi in late_readers)]
+            if not grp:
+                continue
+            lo = min(self.red_groups[gi][0] for gi in grp)
+            hi = max(self.red_groups[gi][1] for gi in grp)
+            descs = [d for gi in grp for d in self.red_groups[gi][2]]
+            if (sum(self.red_groups[gi][1] - self.red_groups[gi][0] for gi in grp) != hi - lo
+                    or not descs or len(descs) > 16):
+                continue                                   # not one contiguous span / table
+            tab = self.ex.K.RedTable()
+            for d in sorted(descs, key=lambda d: -d[2]):
+                tab.add(*d)
+            self.early_red[names[t]] = (tab, (lo, hi))
+            taken += grp
+        return taken
 
     def _launch_optim_comm(self, k, stream):
         """Keras update of bucket k's parameters on the comm stream, right after its
