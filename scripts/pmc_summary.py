@@ -9,7 +9,7 @@ import sys
 from collections import defaultdict
 
 KEEP = ("conv_stack", "dual_halo", "wgrad_halo", "reduce_optim", "dense_", "head_kernel", "prologue",
-        "conv_halo", "wgrad_tile", "conv_tile", "optim_kernel", "slab_reduce", "xgmi")
+        "conv_halo", "wgrad_tile", "conv_tile", "optim_kernel", "slab_reduce", "xgmi", "dense_wgrad", "dense_dx")
 
 
 def main(paths):
