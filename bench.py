@@ -18,6 +18,9 @@ itself): the line reports the rank count the RCCL communicator reports, the grad
 bucket sizes, per-rank step-time p50/max, a cross-rank checksum of the trained weights
 and the exposed communication time (the same step without DP, same N, timed right after);
 the process exits with status 3 if the checksums differ or RCCL saw the wrong rank count.
+Before the timed run, unless ``INTML_XGMI`` pins it, a short probe times the full DP step on
+both data planes (fused xGMI kernel vs bucketed RCCL) and the faster one is timed
+(``probe_data_planes``; the probe numbers are in the self-check).
 
 ``--via-fit`` times what users run instead: ``apps.rpv.train_model(...)`` epochs
 (Keras fit loop, Horovod callbacks, optional ``--lr-warmup-epochs``), training images only.
@@ -129,6 +132,34 @@ def weight_checksum(model):
     return [float(m.sum()), float(m.abs().sum()), float((m * m).sum())]
 
 
+def probe_data_planes(args, size, dev, g, B, chunk):
+    """Data-plane autotune at N > 1 (the Horovod-autotune analogue for the one choice that
+    matters here): when ``INTML_XGMI`` is unset, time a short probe of the full DP step on
+    each data plane -- the fused xGMI all-reduce + optimizer kernel, and the bucketed RCCL
+    all-reduces with the overlapped per-bucket optimizer -- MAX over ranks, and keep the
+    faster one for the timed run (``INTML_XGMI`` is set so every later build agrees).  Both
+    probes are complete training steps; the choice is collective (same numbers on every
+    rank).  Returns {plane: ms/step} of the probes, or None if there was nothing to choose."""
+    from cori_intml_examples_amd.parallel import hvd
+    forced = os.environ.get("INTML_PLANE_PROBE", "0") == "1"     # also at N = 1 (loopback test)
+    if (size < 2 and not forced) or "INTML_XGMI" in os.environ or args.via_fit:
+        return None
+    probe = max(chunk * 6, 48)
+    res = {}
+    for plane, env in (("xgmi", "1"), ("rccl", "0")):
+        os.environ["INTML_XGMI"] = env
+        model, shape, ncls, *_ = build(args, size, True, dev)
+        hvd.broadcast_global_variables(0, model=model)
+        data = synthetic(max(args.samples, B * 4), shape, ncls, model._executor, dev, g)
+        e, _ = time_steps(model, data, B, probe, min(args.warmup, 16), chunk, g, dev)
+        # the reducer sets the xGMI plane up at its first step (collective self-test + vote)
+        on = plane == "rccl" or getattr(model._executor.reducer, "xgmi", None) is not None
+        res[plane] = round((max(hvd.allgather(e)) if size > 1 else e) / probe * 1e3, 4) if on else None
+        del model, data
+    os.environ["INTML_XGMI"] = "1" if res["xgmi"] is not None and res["xgmi"] <= res["rccl"] else "0"
+    return res
+
+
 def run_fit(args, model, shape, ncls, size, dp):
     """Time `apps.rpv.train_model` epochs (the recipe path: Keras fit loop + Horovod
     callbacks); the first epoch (graph capture) is untimed."""
@@ -225,10 +256,11 @@ def main():
     B = args.batch
     # INTML_DP_FORCE=1 runs the full data-parallel step (RCCL all-reduces in the graph) at N=1
     dp = size > 1 or os.environ.get("INTML_DP_FORCE", "0") not in ("0", "")
-    model, shape, ncls, cfg_name, metric, baseline = build(args, size, dp, dev)
-    ex = model._executor
     chunk = max(1, args.steps_per_graph)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    plane_probe = probe_data_planes(args, size, dev, g, B, chunk) if dp else None
+    model, shape, ncls, cfg_name, metric, baseline = build(args, size, dp, dev)
+    ex = model._executor
 
     if args.via_fit:
         elapsed, steps, per_step = run_fit(args, model, shape, ncls, size, dp)
@@ -262,6 +294,7 @@ def main():
             "weight_checksum": sums[0],
             "step_ms_p50_per_rank": [round(r["p50"], 4) for r in rstats],
             "step_ms_max_per_rank": [round(r["max"], 4) for r in rstats],
+            "plane_probe_ms_per_step": plane_probe,
         }
         ok = selfcheck["weights_identical"] and (comm is None or selfcheck["rccl_nranks"] == size)
         if not args.no_dp_delta and not args.via_fit:

@@ -95,6 +95,28 @@ def build_h5(verbose=False):
     return out
 
 
+def build_h5_sanitized(out_dir, verbose=False):
+    """Host-sanitizer build of the HDF5 module (AddressSanitizer + UndefinedBehaviorSanitizer,
+    aborting on the first report) into ``out_dir/_h5lite<EXT>``.  The module reads
+    user-supplied checkpoint and dataset files, so it is the C++ that gets sanitized;
+    ``tests/test_sanitizers.py`` runs the HDF5 round-trip tests against it in a child process
+    with the ASan runtime preloaded.  Returns the path, or None without libhdf5."""
+    src = os.path.join(CSRC, "io", "h5lite.cpp")
+    inc, lib = os.path.join(HDF5_ROOT, "include"), os.path.join(HDF5_ROOT, "lib")
+    if not os.path.exists(os.path.join(inc, "hdf5.h")):
+        return None
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "_h5lite" + EXT)
+    cxx = shutil.which("g++") or "c++"
+    _run([cxx, "-O2", "-g", "-shared", "-fPIC", "-std=c++17", "-fno-omit-frame-pointer",
+          "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", src, "-o", out,
+          "-I" + inc] + _py_includes()
+         # libhdf5 by path, no -L: a -L into the conda tree would resolve the sanitizer
+         # runtimes to its older copies instead of the compiler's own
+         + [os.path.join(lib, "libhdf5.so"), "-Wl,-rpath," + lib], verbose)
+    return out
+
+
 def comm_so_path():
     return os.path.join(HERE, "_comm" + EXT)
 
