@@ -18,9 +18,10 @@ itself): the line reports the rank count the RCCL communicator reports, the grad
 bucket sizes, per-rank step-time p50/max, a cross-rank checksum of the trained weights
 and the exposed communication time (the same step without DP, same N, timed right after);
 the process exits with status 3 if the checksums differ or RCCL saw the wrong rank count.
-Before the timed run, unless ``INTML_XGMI`` pins it, a short probe times the full DP step on
-both data planes (fused xGMI kernel vs bucketed RCCL) and the faster one is timed
-(``probe_data_planes``; the probe numbers are in the self-check).
+Before the timed run, unless ``INTML_XGMI`` / ``INTML_BUCKET_BYTES`` pin it, a short probe
+times the full DP step on each data plane (fused xGMI kernel, one RCCL all-reduce, forked
+RCCL buckets overlapping the backward) and the fastest is timed (``probe_data_planes``; the
+probe numbers and the choice are in the self-check).
 
 ``--via-fit`` times what users run instead: ``apps.rpv.train_model(...)`` epochs
 (Keras fit loop, Horovod callbacks, optional ``--lr-warmup-epochs``), training images only.
@@ -133,30 +134,43 @@ def weight_checksum(model):
 
 
 def probe_data_planes(args, size, dev, g, B, chunk):
-    """Data-plane autotune at N > 1 (the Horovod-autotune analogue for the one choice that
-    matters here): when ``INTML_XGMI`` is unset, time a short probe of the full DP step on
-    each data plane -- the fused xGMI all-reduce + optimizer kernel, and the bucketed RCCL
-    all-reduces with the overlapped per-bucket optimizer -- MAX over ranks, and keep the
-    faster one for the timed run (``INTML_XGMI`` is set so every later build agrees).  Both
-    probes are complete training steps; the choice is collective (same numbers on every
-    rank).  Returns {plane: ms/step} of the probes, or None if there was nothing to choose."""
+    """Data-plane autotune at N > 1 (the Horovod-autotune analogue for the choice that matters
+    here; SURVEY.md §5.1 item 3 "benchmark it against RCCL and keep the winner"): unless
+    ``INTML_XGMI`` / ``INTML_BUCKET_BYTES`` pin it, time a short probe of the full DP step on
+    each candidate data plane --
+      xgmi         the fused two-shot xGMI all-reduce + optimizer kernel (one bucket),
+      rccl         one RCCL all-reduce of the whole gradient at the end of the backward,
+      rccl_forked  1 MiB buckets in backward order, each all-reduce forked onto the comm
+                   stream as soon as its gradients are reduced (overlaps the conv backward),
+    MAX over ranks, and keep the fastest for the timed run (its env is set, so every later
+    build agrees).  Every probe is complete training steps; the choice is collective (the same
+    numbers on every rank).  Returns {plane: ms/step}, or None if there was nothing to choose."""
     from cori_intml_examples_amd.parallel import hvd
     forced = os.environ.get("INTML_PLANE_PROBE", "0") == "1"     # also at N = 1 (loopback test)
-    if (size < 2 and not forced) or "INTML_XGMI" in os.environ or args.via_fit:
+    if ((size < 2 and not forced) or args.via_fit or "INTML_XGMI" in os.environ
+            or "INTML_BUCKET_BYTES" in os.environ):
         return None
+    cands = (("xgmi", {"INTML_XGMI": "1"}), ("rccl", {"INTML_XGMI": "0"}),
+             ("rccl_forked", {"INTML_XGMI": "0", "INTML_BUCKET_BYTES": str(1 << 20)}))
     probe = max(chunk * 6, 48)
     res = {}
-    for plane, env in (("xgmi", "1"), ("rccl", "0")):
-        os.environ["INTML_XGMI"] = env
-        model, shape, ncls, *_ = build(args, size, True, dev)
-        hvd.broadcast_global_variables(0, model=model)
-        data = synthetic(max(args.samples, B * 4), shape, ncls, model._executor, dev, g)
-        e, _ = time_steps(model, data, B, probe, min(args.warmup, 16), chunk, g, dev)
-        # the reducer sets the xGMI plane up at its first step (collective self-test + vote)
-        on = plane == "rccl" or getattr(model._executor.reducer, "xgmi", None) is not None
-        res[plane] = round((max(hvd.allgather(e)) if size > 1 else e) / probe * 1e3, 4) if on else None
-        del model, data
-    os.environ["INTML_XGMI"] = "1" if res["xgmi"] is not None and res["xgmi"] <= res["rccl"] else "0"
+    for plane, env in cands:
+        os.environ.update(env)
+        try:
+            model, shape, ncls, *_ = build(args, size, True, dev)
+            hvd.broadcast_global_variables(0, model=model)
+            data = synthetic(max(args.samples, B * 4), shape, ncls, model._executor, dev, g)
+            e, _ = time_steps(model, data, B, probe, min(args.warmup, 16), chunk, g, dev)
+            # the reducer sets the xGMI plane up at its first step (collective self-test + vote)
+            on = plane != "xgmi" or getattr(model._executor.reducer, "xgmi", None) is not None
+            res[plane] = round((max(hvd.allgather(e)) if size > 1 else e) / probe * 1e3, 4) if on else None
+            del model, data
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+    best = min((v, k) for k, v in res.items() if v is not None)[1]
+    os.environ.update(dict(cands)[best])
+    res["chosen"] = best
     return res
 
 
