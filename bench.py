@@ -162,13 +162,22 @@ def probe_data_planes(args, size, dev, g, B, chunk):
             data = synthetic(max(args.samples, B * 4), shape, ncls, model._executor, dev, g)
             e, _ = time_steps(model, data, B, probe, min(args.warmup, 16), chunk, g, dev)
             # the reducer sets the xGMI plane up at its first step (collective self-test + vote)
-            on = plane != "xgmi" or getattr(model._executor.reducer, "xgmi", None) is not None
-            res[plane] = round((max(hvd.allgather(e)) if size > 1 else e) / probe * 1e3, 4) if on else None
+            x = getattr(model._executor.reducer, "xgmi", None)
+            on = plane != "xgmi" or x is not None
+            # a plane is only eligible if it trained correctly here: no timed-out wait and
+            # bit-identical weights on every rank after the probe steps
+            sane = [weight_checksum(model), bool(x is None or int(x.err.item()) == 0)]
+            sane = hvd.allgather(sane) if size > 1 else [sane]
+            ok = all(c == sane[0][0] and f for c, f in sane)
+            res[plane] = (round((max(hvd.allgather(e)) if size > 1 else e) / probe * 1e3, 4)
+                          if on and ok else None)
+            if not ok:
+                res[plane + "_rejected"] = "weights differ across ranks or a wait timed out"
             del model, data
         finally:
             for k in env:
                 os.environ.pop(k, None)
-    best = min((v, k) for k, v in res.items() if v is not None)[1]
+    best = min(((v, k) for k, v in res.items() if isinstance(v, float)), default=(0, "rccl"))[1]
     os.environ.update(dict(cands)[best])
     res["chosen"] = best
     return res
