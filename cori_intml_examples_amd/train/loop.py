@@ -38,21 +38,40 @@ def _split_validation(x, y, validation_split, validation_data):
     return x, y, None, None
 
 
+def shard_indices(n: int, rank: int, size: int, shuffle: bool, seed: int, epoch: int) -> torch.Tensor:
+    """Rank ``rank``'s sample indices for ``epoch``: its disjoint ``n // size`` slice of a
+    permutation every rank draws identically (``seed`` is rank 0's, broadcast; the epoch is
+    mixed in, so the shards change every epoch).  Unshuffled: the contiguous block
+    ``[rank * per, (rank + 1) * per)``, the fixed-shard layout."""
+    per = n // size
+    if shuffle:
+        g = torch.Generator(device="cpu")
+        g.manual_seed((seed * 1000003 + 7919 * (epoch + 1)) & 0x7FFFFFFFFFFF)
+        order = torch.randperm(n, generator=g)
+    else:
+        order = torch.arange(n)
+    return order[rank * per:(rank + 1) * per]
+
+
 def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_split, validation_data,
              shuffle, initial_epoch):
     from ..parallel import state as dp_state
     ex = model._executor
     x, y, vx, vy = _split_validation(x, y, validation_split, validation_data)
 
-    # data-parallel sharding (default) or the reference's replicated semantics
+    # data-parallel sharding (default) or the reference's replicated semantics.  Sharded: every
+    # rank keeps the WHOLE training set resident (HBM is not the constraint for these data
+    # sets) and takes its disjoint 1/size slice of an epoch permutation that all ranks draw
+    # from the same seed -- a distributed sampler that reshards every epoch, so the n % size
+    # samples left out differ from epoch to epoch instead of being dropped for good.
     dp = dp_state.current()
+    shard = None
     if dp is not None and dp.size > 1 and dp.shard_data and getattr(model.optimizer, "distributed", False):
-        n = len(x)
-        per = n // dp.size
-        x = x[dp.rank * per:(dp.rank + 1) * per]
-        y = y[dp.rank * per:(dp.rank + 1) * per]
+        from ..parallel import dist as _dist
+        shard = (dp.rank, dp.size, int(_dist.broadcast_object(int(model._seed) & 0x7FFFFFFF, 0)))
 
     train = ex.upload(x, y)
+    n_local = train.n // shard[1] if shard else train.n
     val = ex.upload(vx, vy) if vx is not None else None
     do_val = val is not None
 
@@ -64,7 +83,7 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
     metrics = list(out_labels) + (["val_" + n for n in out_labels] if do_val else [])
     cb.set_model(model)
     cb.set_params({"batch_size": batch_size, "epochs": epochs, "steps": None,
-                   "samples": train.n, "verbose": verbose, "do_validation": do_val,
+                   "samples": n_local, "verbose": verbose, "do_validation": do_val,
                    "metrics": metrics})
     for c in cb:
         c.validation_data = (vx, vy) if do_val else None
@@ -74,9 +93,9 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
     steps_per_replay = max(1, int(os.environ.get("INTML_STEPS_PER_GRAPH", "8")))
 
     if do_val and verbose:
-        print("Train on %d samples, validate on %d samples" % (train.n, val.n))
+        print("Train on %d samples, validate on %d samples" % (n_local, val.n))
     elif verbose:
-        print("Train on %d samples" % train.n)
+        print("Train on %d samples" % n_local)
 
     from ..farm.engine import should_stop as farm_should_stop
     gen = torch.Generator(device="cpu")
@@ -84,22 +103,24 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
     cb.on_train_begin()
     for epoch in range(initial_epoch, epochs):
         cb.on_epoch_begin(epoch, {})
-        if shuffle:
+        if shard:
+            perm = shard_indices(train.n, shard[0], shard[1], shuffle, shard[2], epoch).to(ex.device)
+        elif shuffle:
             perm = torch.randperm(train.n, generator=gen).to(ex.device)
         else:
             perm = torch.arange(train.n, device=ex.device)
         ex.reset_metrics()
-        nb = (train.n + batch_size - 1) // batch_size
+        nb = (n_local + batch_size - 1) // batch_size
         # Without per-batch callbacks, runs of full batches go to the device as chunks of
         # `chunk` steps (one HIP-graph replay each); the partial tail batch runs alone.
         chunk = 1 if (need_batch_logs or need_batch_begin) else steps_per_replay
         b = 0
         while b < nb:
             pos = b * batch_size
-            bs = min(batch_size, train.n - pos)
+            bs = min(batch_size, n_local - pos)
             k = 1
             if chunk > 1 and bs == batch_size:
-                k = max(1, min(chunk, (train.n - pos) // batch_size))
+                k = max(1, min(chunk, (n_local - pos) // batch_size))
             if k > 1:
                 ex.train_steps(train, perm, pos, bs, k)
                 b += k

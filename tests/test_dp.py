@@ -7,6 +7,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -77,3 +78,29 @@ def test_train_rpv_cli_two_ranks(tmp_path):
     assert len(foms[0]) == 1 and foms[0] == foms[1]     # weights + averaged metrics agree
     assert "rank 0/2" in outs[0] and "rank 1/2" in outs[1]
     assert "Total params" in outs[0] and "Total params" not in outs[1]   # rank-0 summary only
+
+
+def test_shard_indices_disjoint_cover_and_reshard():
+    """Distributed sampler of fit(): per epoch the ranks' slices are disjoint, equal-sized,
+    drawn from one permutation; shards change across epochs (the n % size left-outs too)."""
+    from cori_intml_examples_amd.train.loop import shard_indices
+    n, size = 1003, 4
+    seen_left_out = set()
+    prev = None
+    for epoch in range(3):
+        parts = [shard_indices(n, r, size, True, 12345, epoch) for r in range(size)]
+        assert all(len(p) == n // size for p in parts)
+        allidx = np.concatenate([p.numpy() for p in parts])
+        assert len(set(allidx.tolist())) == len(allidx)            # disjoint
+        assert allidx.min() >= 0 and allidx.max() < n
+        left = set(range(n)) - set(allidx.tolist())
+        assert len(left) == n % size
+        seen_left_out |= left
+        if prev is not None:
+            assert not np.array_equal(prev, parts[0].numpy())     # reshuffled shard
+        prev = parts[0].numpy()
+    assert len(seen_left_out) > n % size                             # not the same samples forever
+    # same seed + epoch -> the same slices on every rank (no communication needed per epoch)
+    assert np.array_equal(shard_indices(n, 2, size, True, 7, 5).numpy(), shard_indices(n, 2, size, True, 7, 5).numpy())
+    # unshuffled: the contiguous fixed-shard layout
+    assert np.array_equal(shard_indices(10, 1, 3, False, 0, 0).numpy(), np.arange(3, 6))
