@@ -396,9 +396,11 @@ class HipExecutor(Executor):
             self._bound_data = key
             self._perm_obj = None
         if perm is not None and perm is not self._perm_obj:
-            if self._perm_buf is None or self._perm_buf.numel() < data.n:
+            # (a DP rank's epoch slice of the sampler permutation is shorter than the data set)
+            m = min(int(perm.numel()), data.n)
+            if self._perm_buf is None or self._perm_buf.numel() < max(data.n, 1):
                 self._perm_buf = torch.empty(max(data.n, 1), dtype=torch.int32, device=self.device)
-            self._perm_buf[:data.n].copy_(perm.to(device=self.device, dtype=torch.int32))
+            self._perm_buf[:m].copy_(perm[:m].to(device=self.device, dtype=torch.int32))
             self._st_i64[K.STEP_STATE_DATA_OFFSET // 8 + 2] = self._perm_buf.data_ptr()
             self._perm_obj = perm
         use = 1 if perm is not None else 0
