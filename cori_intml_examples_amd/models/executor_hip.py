@@ -1098,15 +1098,22 @@ class BatchPlan:
         W_in = (Wo - 1) * a.stride + a.KW
         step = 2 if pool else 1
         gy = cdiv(NT, ntc)
+        # Balanced blocks: the fewest row blocks per image (c) that satisfy the limits, each
+        # cdiv(Ho, c) rows -- not the largest R with a short remainder block.  Measured on
+        # MNIST's 26-row dgrad (co-scheduled with its wgrad): 15 + 11-row blocks 156 us/step,
+        # 13 + 13 125 us; the RPV layers divide evenly and are unchanged.
         best = step
-        for R in range(step, Ho + 1, step):
+        for c in range(1, Ho + 1):
+            R = cdiv(cdiv(Ho, c), step) * step
             if R * Wo > 512:
-                break
+                continue
             halo = ((R - 1) * a.stride + a.KH) * W_in * a.Cs_in * 2
             if halo + KS * ntc * 1024 > 80 * 1024:
-                break
-            if a.B * cdiv(Ho, R) * gy >= want:
-                best = R          # largest block that still leaves >= `want` workgroups
+                continue
+            if a.B * cdiv(Ho, R) * gy < want:
+                continue         # too few workgroups: more, smaller blocks
+            best = R
+            break
         a.R = best
         lds = K_lds = self.ex.K.conv_halo_lds_bytes(a, ntc)
         if lds > 150 * 1024:
