@@ -11,12 +11,18 @@ from cori_intml_examples_amd.apps import zoo
 os.environ["INTML_GRAPHS"] = "0"
 dev = torch.device("cuda", 0)
 B = 128
-model = zoo.rpv_cnn((64, 64, 3), conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.2, optimizer="Adam",
-                    lr=1e-3, device=dev)
-ex = model._executor
-ex.use_graphs = False
 rs = np.random.RandomState(0)
-d = ex.upload(rs.rand(B * 4, 64, 64, 3).astype(np.float32), (rs.rand(B * 4) > 0.5).astype(np.float32))
+if os.environ.get("MODEL", "rpv") == "mnist":
+    model = zoo.mnist_cnn(32, 64, 128, 0.25, 0.5, lr=1.0, device=dev)
+    ex = model._executor
+    ex.use_graphs = False
+    d = ex.upload(rs.rand(B * 4, 28, 28, 1).astype(np.float32), np.eye(10, dtype=np.float32)[rs.randint(0, 10, B * 4)])
+else:
+    model = zoo.rpv_cnn((64, 64, 3), conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.2, optimizer="Adam",
+                        lr=1e-3, device=dev)
+    ex = model._executor
+    ex.use_graphs = False
+    d = ex.upload(rs.rand(B * 4, 64, 64, 3).astype(np.float32), (rs.rand(B * 4) > 0.5).astype(np.float32))
 ex.train_step(d, torch.arange(d.n, device=dev), 0, B)
 torch.cuda.synchronize()
 bp = ex._plans[(B, "train")]
