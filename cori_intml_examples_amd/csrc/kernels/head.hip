@@ -68,6 +68,70 @@ __device__ __forceinline__ float dense_epi_group(const DenseEpiArgs& e, int m, i
   return a0 + a1;
 }
 
+// 16-lane group reductions (lanes 0..15 of a wave; xor offsets < 16 stay inside the group)
+__device__ __forceinline__ float grp16_sum(float v) {
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+// max value and its lowest index (the serial loop's strict '>' keeps the first maximum)
+__device__ __forceinline__ void grp16_argmax(float& v, int& i) {
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(v, off);
+    const int oi = __shfl_xor(i, off);
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+}
+
+// Softmax + Keras categorical_crossentropy (clip of the renormalised probabilities) and its
+// gradient, lane n = class n.  Same formulas as the serial head path; sums are 16-lane trees.
+template <int NM>
+__device__ __forceinline__ void softmax_cce_lanes(const HeadArgs& a, const float (&z)[NM], int lane, int row,
+                                                  int rw, int N, const float* ysh_row, const float* bsh,
+                                                  float* dz_row, float* met_row) {
+  const bool live = row < a.M;
+  const int n = lane & 15;
+  const bool cls = live && lane < 16 && n < N;
+  float zn = 0.f;
+#pragma unroll
+  for (int j = 0; j < NM; ++j)
+    if (j == n) zn = z[j];
+  zn += bsh[n];
+  float mx = cls ? zn : -__builtin_inff();
+  int am = cls ? n : 1 << 20;
+  grp16_argmax(mx, am);
+  const float e = cls ? expf(zn - mx) : 0.f;
+  const float s = grp16_sum(e);
+  const float p = e / s;
+  if (cls && a.probs) a.probs[(size_t)row * N + n] = p;
+  float loss = 0.f, dzn = 0.f, correct = 0.f;
+  if (a.y) {
+    const float eps = 1e-7f;
+    const float ps = grp16_sum(cls ? p : 0.f);
+    const float yn = cls ? ysh_row[n] : 0.f;
+    const float q = p / ps;
+    const bool inr = (q >= eps) && (q <= 1.f - eps);
+    const float qc = fminf(fmaxf(q, eps), 1.f - eps);
+    const float ln = cls ? -yn * logf(qc) : 0.f;
+    float gn = (cls && inr) ? -yn / qc : 0.f;
+    const float gq = grp16_sum(gn * (cls ? q : 0.f));
+    gn = (gn - gq) / ps;
+    const float pg = grp16_sum(cls ? p * gn : 0.f);
+    dzn = cls ? p * (gn - pg) : 0.f;
+    loss = grp16_sum(ln);
+    float ymx = cls ? yn : -__builtin_inff();
+    int ay = cls ? n : 1 << 20;
+    grp16_argmax(ymx, ay);
+    correct = (live && am == ay) ? 1.f : 0.f;
+  }
+  if (lane < NM) dz_row[lane] = dzn * a.inv_bs;
+  if (lane == 0) {
+    met_row[0] = live ? loss : 0.f;
+    met_row[1] = correct;
+  }
+}
+
 #define HEAD_STAMP(i)                                                                 \
   if (a.ts && threadIdx.x == 0) a.ts[(size_t)blockIdx.x * 8 + (i)] = wall_clock64();
 
@@ -164,14 +228,23 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
         if (n < N) z[n] += hv * (wlds ? wsh[k * N + n] : a.w[(size_t)k * N + n]);
     }
   }
+  // the NM chains unconditionally (z[n >= N] is 0) and interleaved: 6 dependent cross-lane
+  // rounds instead of N guarded chains of 6 (each chain's order is unchanged)
 #pragma unroll
-  for (int n = 0; n < NM; ++n) {
-    if (n < N) {
+  for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) z[n] += __shfl_xor(z[n], off);
+    for (int n = 0; n < NM; ++n) z[n] += __shfl_xor(z[n], off);
+  }
+  HEAD_STAMP(7);
+  if constexpr (NM > 1) {
+    if (a.act == 2 && row_wave) {
+      // softmax + categorical cross-entropy, one class per lane (lanes 0..15 of the row's
+      // wave; every lane holds all logits after the reduction above).  The serial lane-0
+      // version spent ~5 us per row in dependent exp / log / divide chains.
+      softmax_cce_lanes<NM>(a, z, lane, row, rw, N, &ysh[rw][0], bsh, &dz_s[rw][0], &met[rw][0]);
     }
   }
-  if (lane == 0 && row_wave) {
+  if (lane == 0 && row_wave && (NM == 1 || a.act != 2)) {
     float dz[NM];
 #pragma unroll
     for (int n = 0; n < NM; ++n) dz[n] = 0.f;

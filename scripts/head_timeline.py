@@ -40,5 +40,6 @@ t = t[t[:, 0] > 0]
 t0 = t[:, 0].min()
 print("head: %d blocks, start spread med %.2f max %.2f us, span %.2f us" % (
     len(t), np.median(t[:, 0] - t0), (t[:, 0] - t0).max(), (t[:, 6] - t0).max()))
+print("  dot+shuffles       +%.2f us (median, inside dot+loss)" % np.median(t[:, 7] - t[:, 1]))
 for i, lab in enumerate(["epilogue+w stage", "dot+loss", "barrier", "metrics atomics", "dW slab", "bwd-through"]):
     print("  %-18s +%.2f us (median)" % (lab, np.median(t[:, i + 1] - t[:, i])))
