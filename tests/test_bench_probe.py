@@ -1,0 +1,74 @@
+"""bench.py's data-plane probe (N > 1): picks the fastest eligible plane, sets its env for the
+timed run, rejects a plane whose probe left the ranks' weights different, and stays out of
+the way when INTML_XGMI / INTML_BUCKET_BYTES pin the plane.  CPU, with the model build,
+the timing and the collectives stubbed (the real path needs >= 2 GPUs)."""
+import os
+import sys
+import types
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from cori_intml_examples_amd.parallel import hvd  # noqa: E402
+
+
+@pytest.fixture
+def probe_env(monkeypatch):
+    for k in ("INTML_XGMI", "INTML_BUCKET_BYTES", "INTML_PLANE_PROBE"):
+        # setenv first so teardown restores the original state even though the probe itself
+        # writes these variables
+        monkeypatch.setenv(k, "")
+        monkeypatch.delenv(k)
+    cost = {"xgmi": 10.0, "rccl": 11.0, "rccl_forked": 12.0}
+    sums = {"bad": set()}
+
+    def plane():
+        if os.environ.get("INTML_XGMI") == "1":
+            return "xgmi"
+        return "rccl_forked" if os.environ.get("INTML_BUCKET_BYTES") else "rccl"
+
+    def build(args, size, dp, dev):
+        x = types.SimpleNamespace(err=types.SimpleNamespace(item=lambda: 0)) if plane() == "xgmi" else None
+        m = types.SimpleNamespace(_executor=types.SimpleNamespace(reducer=types.SimpleNamespace(xgmi=x)),
+                                  plane=plane())
+        return m, (64, 64, 3), 1, "cfg", "metric", None
+
+    monkeypatch.setattr(bench, "build", build)
+    monkeypatch.setattr(bench, "synthetic", lambda *a, **k: None)
+    monkeypatch.setattr(bench, "time_steps", lambda m, *a, **k: (cost[m.plane] * 1e-3, [1.0]))
+    monkeypatch.setattr(bench, "weight_checksum", lambda m: [1.0, 2.0, 3.0])
+    monkeypatch.setattr(hvd, "broadcast_global_variables", lambda *a, **k: None)
+
+    def allgather(v):   # two ranks; rank 1's weights differ for the planes marked bad
+        if isinstance(v, list) and len(v) == 2 and isinstance(v[0], list):
+            other = [[9.0, 2.0, 3.0], True] if plane() in sums["bad"] else v
+            return [v, other]
+        return [v, v]
+
+    monkeypatch.setattr(hvd, "allgather", allgather)
+    args = types.SimpleNamespace(via_fit=False, samples=1024, warmup=30)
+    return cost, sums, args
+
+
+def test_probe_picks_fastest_and_sets_env(probe_env):
+    cost, _, args = probe_env
+    cost.update(xgmi=12.0, rccl=11.0, rccl_forked=10.0)
+    r = bench.probe_data_planes(args, 2, None, None, 128, 8)
+    assert r["chosen"] == "rccl_forked"
+    assert os.environ["INTML_XGMI"] == "0" and os.environ["INTML_BUCKET_BYTES"] == str(1 << 20)
+
+
+def test_probe_rejects_divergent_plane(probe_env):
+    cost, sums, args = probe_env
+    sums["bad"].add("xgmi")                    # fastest, but its ranks ended with different weights
+    r = bench.probe_data_planes(args, 2, None, None, 128, 8)
+    assert r["xgmi"] is None and "xgmi_rejected" in r and r["chosen"] == "rccl"
+    assert os.environ["INTML_XGMI"] == "0" and "INTML_BUCKET_BYTES" not in os.environ
+
+
+def test_probe_respects_pinned_plane(probe_env, monkeypatch):
+    _, _, args = probe_env
+    monkeypatch.setenv("INTML_XGMI", "1")
+    assert bench.probe_data_planes(args, 2, None, None, 128, 8) is None
+    assert bench.probe_data_planes(args, 1, None, None, 128, 8) is None
