@@ -25,6 +25,15 @@ probe numbers and the choice are in the self-check).
 
 ``--via-fit`` times what users run instead: ``apps.rpv.train_model(...)`` epochs
 (Keras fit loop, Horovod callbacks, optional ``--lr-warmup-epochs``), training images only.
+
+HPO trials/hour (BASELINE.json's second metric) rides on the same JSON line as ``"hpo"``:
+rank 0 starts a task farm on every visible GPU BEFORE anything touches the GPU (engines are
+child processes; nothing is forked from a GPU-initialised process), the training bench runs
+and is timed while the engines idle, the data-parallel group shuts down, and then the farm
+runs the DistHPO_mnist random search (``DistHPO_mnist.ipynb:137-255``: 64 trials, 16 epochs,
+60k samples, valid_frac 0.17, batch 128, load-balanced over the engines), capped at
+``--hpo-budget`` seconds including engine start-up (a capped run reports the trials it
+finished).  ``--no-hpo`` skips it.
 """
 from __future__ import annotations
 
@@ -142,6 +151,8 @@ def probe_data_planes(args, size, dev, g, B, chunk):
       rccl         one RCCL all-reduce of the whole gradient at the end of the backward,
       rccl_forked  1 MiB buckets in backward order, each all-reduce forked onto the comm
                    stream as soon as its gradients are reduced (overlaps the conv backward),
+      hybrid       the dense bucket's RCCL all-reduce forked onto the comm stream (overlaps the
+                   conv backward) + the small conv bucket through the fused xGMI kernel,
     MAX over ranks, and keep the fastest for the timed run (its env is set, so every later
     build agrees).  Every probe is complete training steps; the choice is collective (the same
     numbers on every rank).  Returns {plane: ms/step}, or None if there was nothing to choose."""
@@ -150,8 +161,9 @@ def probe_data_planes(args, size, dev, g, B, chunk):
     if ((size < 2 and not forced) or args.via_fit or "INTML_XGMI" in os.environ
             or "INTML_BUCKET_BYTES" in os.environ):
         return None
-    cands = (("xgmi", {"INTML_XGMI": "1"}), ("rccl", {"INTML_XGMI": "0"}),
-             ("rccl_forked", {"INTML_XGMI": "0", "INTML_BUCKET_BYTES": str(1 << 20)}))
+    cands = (("xgmi", {"INTML_XGMI": "xgmi"}), ("rccl", {"INTML_XGMI": "rccl"}),
+             ("rccl_forked", {"INTML_XGMI": "rccl", "INTML_BUCKET_BYTES": str(1 << 20)}),
+             ("hybrid", {"INTML_XGMI": "hybrid", "INTML_BUCKET_BYTES": str(1 << 20)}))
     probe = max(chunk * 6, 48)
     res = {}
     for plane, env in cands:
@@ -163,7 +175,7 @@ def probe_data_planes(args, size, dev, g, B, chunk):
             e, _ = time_steps(model, data, B, probe, min(args.warmup, 16), chunk, g, dev)
             # the reducer sets the xGMI plane up at its first step (collective self-test + vote)
             x = getattr(model._executor.reducer, "xgmi", None)
-            on = plane != "xgmi" or x is not None
+            on = plane not in ("xgmi", "hybrid") or x is not None
             # a plane is only eligible if it trained correctly here: no timed-out wait and
             # bit-identical weights on every rank after the probe steps
             sane = [weight_checksum(model), bool(x is None or int(x.err.item()) == 0)]
@@ -236,6 +248,66 @@ def run_hpo(args, extra):
     return 0
 
 
+class InlineHpo:
+    """The DistHPO_mnist random search on a task farm, started before the training bench
+    touches the GPU and run after it (see the module docstring)."""
+
+    TRIALS, EPOCHS, SAMPLES, BATCH, VALID_FRAC = 64, 16, 60000, 128, 0.17
+
+    def __init__(self, engines_per_gpu: int, budget_s: float):
+        from cori_intml_examples_amd import farm
+        self.t0 = time.time()
+        self.budget_s = budget_s
+        self.n_gpu = farm.detect_gpus()
+        self.engines = max(1, self.n_gpu) * engines_per_gpu
+        self.cl = farm.start_cluster(self.engines, cluster_id="bench_hpo_%d" % os.getpid(),
+                                     cpu_only=self.n_gpu == 0, timeout=min(120.0, budget_s))
+        self.startup_s = time.time() - self.t0
+
+    def run(self):
+        import cloudpickle
+        sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+        import hpo_throughput
+        from cori_intml_examples_amd.hpo import random_search as rs
+        cloudpickle.register_pickle_by_value(hpo_throughput)
+        t1 = time.time()
+        capped, done = False, []
+        try:
+            with self.cl.client() as c:
+                trials = rs.mnist_trials(self.TRIALS)
+                ars = rs.submit_trials(c.load_balanced_view(), hpo_throughput.trial_mnist, trials,
+                                       n_train=self.SAMPLES, batch_size=self.BATCH, n_epochs=self.EPOCHS,
+                                       valid_frac=self.VALID_FRAC)
+                deadline = t1 + max(1.0, self.budget_s - self.startup_s)
+                while not all(a.ready() for a in ars) and time.time() < deadline:
+                    time.sleep(0.25)
+                t2 = time.time()
+                capped = not all(a.ready() for a in ars)
+                done = [r for r in rs.collect([a for a in ars if a.ready()]) if r]
+                for a in ars:
+                    if not a.ready():
+                        a.abort()
+        finally:
+            self.cl.stop()
+        wall = self.startup_s + (t2 - t1)
+        best = min((min(r["val_loss"]) for r in done), default=None)
+        return {"metric": "HPO trials/hour (DistHPO_mnist random search)",
+                "trials_per_hour": round(len(done) / wall * 3600, 1), "trials_done": len(done),
+                "trials_submitted": self.TRIALS, "capped": capped, "n_gpus": self.n_gpu,
+                "engines_per_gpu": self.engines // max(1, self.n_gpu), "epochs": self.EPOCHS,
+                "samples": self.SAMPLES, "valid_frac": self.VALID_FRAC, "batch": self.BATCH,
+                "wall_s": round(wall, 2), "startup_s": round(self.startup_s, 2),
+                "mean_trial_s": round(sum(r["t1"] - r["t0"] for r in done) / max(1, len(done)), 3),
+                "best_val_loss": best, "budget_s": self.budget_s,
+                "data": "synthetic MNIST (60k), resident per engine; random-init weights"}
+
+    def stop(self):
+        try:
+            self.cl.stop()
+        except Exception:     # noqa: BLE001
+            pass
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -258,6 +330,10 @@ def main():
                          "second metric): mnist = 64 DistHPO_mnist trials spread over the node's GPUs, "
                          "rpv = DistWidgetHPO_rpv-style 8 concurrent RPV trials, cray = genetic search over "
                          "2-rank DP train_rpv evaluations; extra flags after -- go to benchmarks/hpo_throughput.py")
+    ap.add_argument("--no-hpo", action="store_true",
+                    help="skip the DistHPO_mnist trials/hour measurement reported as 'hpo' on the JSON line")
+    ap.add_argument("--hpo-budget", type=float, default=90.0, help="seconds for the inline HPO, start-up included")
+    ap.add_argument("--hpo-engines-per-gpu", type=int, default=4)
     args, extra = ap.parse_known_args()
     if args.hpo:
         return run_hpo(args, extra)
@@ -265,6 +341,15 @@ def main():
         ap.error("unrecognized arguments: %s" % " ".join(extra))
     if args.no_graphs:
         os.environ["INTML_GRAPHS"] = "0"
+    # rank 0 starts the HPO farm now, before this process initialises the GPU
+    inline_hpo = None
+    if not args.no_hpo and not args.via_fit and int(os.environ.get("RANK", "0")) == 0:
+        try:
+            inline_hpo = InlineHpo(args.hpo_engines_per_gpu, args.hpo_budget)
+            import atexit
+            atexit.register(inline_hpo.stop)      # no engine outlives a failed bench
+        except Exception as e:   # noqa: BLE001 -- the training metric must not depend on it
+            print("inline HPO farm failed to start: %s" % e, file=sys.stderr, flush=True)
 
     import torch
     from cori_intml_examples_amd.parallel import hvd
@@ -307,9 +392,16 @@ def main():
         red = ex.reducer
         sums = hvd.allgather(weight_checksum(model)) if size > 1 else [weight_checksum(model)]
         rstats = hvd.allgather(stats) if size > 1 else [stats]
+        from cori_intml_examples_amd.parallel.dist import data_plane
+        xk = getattr(red, "xgmi_bucket", None)
         selfcheck = {
-            "data_plane": ("xgmi-fused-allreduce+optim" if getattr(red, "xgmi", None) is not None else
+            "data_plane": (("xgmi-fused-allreduce+optim" if len(red.buckets) == 1 else
+                            "hybrid: rccl buckets %s + xgmi-fused bucket %d" % (list(range(xk)), xk))
+                           if xk is not None else
                            "rccl-native" if comm is not None else ("torch-" + str(st.backend))),
+            # what a fit() / train_rpv run without the probe uses (INTML_XGMI unset)
+            "default_plane": "rccl-native" if comm is not None else ("torch-" + str(st.backend)),
+            "env_plane": data_plane(),
             "rccl_nranks": comm.nranks if comm is not None else None,
             "world_size": size,
             "bucket_bytes": [4 * (hi - lo) for lo, hi in red.buckets] if red is not None else None,
@@ -350,6 +442,15 @@ def main():
 
     ms = elapsed / steps * 1e3
     value = size * B * steps / elapsed
+    # every rank leaves the data-parallel group; rank 0 then runs the HPO on the farm
+    hvd.shutdown()
+    hpo_rec = None
+    if inline_hpo is not None:
+        try:
+            hpo_rec = inline_hpo.run()
+        except Exception as e:   # noqa: BLE001
+            inline_hpo.stop()
+            hpo_rec = {"error": str(e)[:300]}
     if rank == 0:
         out = {"metric": metric,
                "value": round(value, 1), "unit": "images/s", "n_gpus": size, "steps": steps,
@@ -368,8 +469,9 @@ def main():
             out["config"]["lr_warmup_epochs"] = args.lr_warmup_epochs
         if selfcheck is not None:
             out["selfcheck"] = selfcheck
+        if hpo_rec is not None:
+            out["hpo"] = hpo_rec
         print(json.dumps(out), flush=True)
-    hvd.shutdown()
     if not ok:
         print("bench self-check FAILED: %s" % json.dumps(selfcheck), file=sys.stderr, flush=True)
         sys.exit(3)

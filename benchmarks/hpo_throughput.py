@@ -197,8 +197,12 @@ def main(argv=None):
         "mean_train_s": round(sum(r["train_s"] for r in ok) / max(1, len(ok)), 3),
         "mean_data_s": round(sum(r["data_s"] for r in ok) / max(1, len(ok)), 3),
         "mean_trial_s": round(sum(r["t1"] - r["t0"] for r in ok) / max(1, len(ok)), 3),
-        "vs_baseline": round(per_hour / REF_EVALS_PER_HOUR, 2) if a.model == "rpv" else None,
-        "baseline": "41.2 evals/hour (CrayHPO_rpv, 32 nodes)" if a.model == "rpv" else "no wall-clock recorded",
+        # no like-for-like reference: CrayHPO_rpv's 41.2 evals/hour are 4-node DATA-PARALLEL
+        # evaluations (batch 64/rank), these are single-GPU trials -- compare per evaluation
+        # with --mode cray instead
+        "vs_baseline": None,
+        "baseline": ("not comparable: the reference's 41.2 evals/hour (CrayHPO_rpv) are 4-rank DP evaluations"
+                     if a.model == "rpv" else "no wall-clock recorded"),
         "data": "synthetic %s, resident per engine" % ("RPV (1-channel 64x64)" if a.model == "rpv" else "MNIST")}
     print(json.dumps(rec), flush=True)
     return rec

@@ -42,8 +42,8 @@ def main(argv=None):
         cbs = [hvd.callbacks.BroadcastGlobalVariablesCallback(0), hvd.callbacks.MetricAverageCallback()]
     h = model.fit(x, y, batch_size=a.batch_size, epochs=a.epochs, validation_split=a.valid_frac,
                   verbose=a.verbose if hvd.rank() == 0 else 0, callbacks=cbs)
-    vl = h.history["val_loss"]
-    print("FoM:", min(vl) if a.fom == "best" else vl[-1])
+    from ..hpo.evaluator import figure_of_merit
+    print("FoM:", figure_of_merit(h.history["val_loss"], a.fom))
     sys.stdout.flush()
     hvd.shutdown()
     return h

@@ -87,10 +87,9 @@ def main(argv=None):
     history = train_model(model, train_input=train_input, train_labels=train_labels, valid_input=valid_input,
                           valid_labels=valid_labels, batch_size=args.batch_size, n_epochs=args.n_epochs,
                           verbose=args.verbose, use_horovod=True)
-    if args.fom == "best":
-        print("FoM:", min(history.history["val_loss"]))
-    elif args.fom == "last":
-        print("FoM:", history.history["val_loss"][-1])
+    if args.fom in ("best", "last"):
+        from ..hpo.evaluator import figure_of_merit
+        print("FoM:", figure_of_merit(history.history["val_loss"], args.fom))
     sys.stdout.flush()
 
     if hvd.rank() == 0 and args.n_test > 0:

@@ -271,6 +271,13 @@ struct DualExtra {
   OptimArgs ro;
   float* grad = nullptr;
   int n_r = 0, rfirst = 0;
+  // Chained wgrad (ntt2 > 0): each dgrad workgroup, right after writing its block of dP
+  // (the gradient wrt the previous stage's output), runs the PREVIOUS layer's weight
+  // gradient over exactly the conv rows that block feeds (w2.blocks_per_split wgrad blocks
+  // starting at block bx * bps, one slab per dgrad block) -- the first conv layer's wgrad
+  // needs no launch of its own, and dP is re-read from this CU's own stores.
+  WgradArgs w2;
+  int MT2 = 0, ntt2 = 0;
 };
 
 // Fused data-parallel all-reduce + optimizer over xGMI peer memory (xgmi.hip).  Every rank
@@ -283,23 +290,24 @@ struct DualExtra {
 //      whole reduced gradient (identical inputs -> identical weights on every rank).
 // Flags carry a per-workgroup sequence number (ctr[w] + 1), so they never need resetting.
 // Communication memory is uncached device memory shared by IPC handles; every wait is
-// bounded (spin_limit polls) and sets *err instead of hanging.
+// bounded in time (timeout_ticks) and sets *err instead of hanging.
 #define XGMI_MAX_RANKS 8
 #define XGMI_MAX_WG 256
 struct XgmiArgs {
   int rank = 0, size = 1;
-  int n = 0;                     // gradient elements (bucket [0, n))
+  int n = 0;                     // gradient elements of the bucket (grad points at its start)
   int chunk = 0;                 // elements per owner chunk (multiple of 4)
   int sub = 0;                   // elements per workgroup slice of a chunk (multiple of 4)
-  int spin_limit = 1 << 22;
+  long long timeout_ticks = 0;   // bounded waits: give up after this many wall_clock64 ticks (100 MHz)
   int mode = 1;                  // 0: sum only (reduced gradient -> grad); 1: + optimizer
   int fence = 1;                 // system-scope release/acquire fences around the flags
-  float* grad = nullptr;         // local flat gradient (read in 1, reduced sum written in 3)
+  float* grad = nullptr;         // local bucket gradient (read in 1, reduced sum written in 2/3)
   float* inbox[XGMI_MAX_RANKS] = {};     // rank j's inbox [P][chunk] (as mapped here)
   float* outbox[XGMI_MAX_RANKS] = {};    // rank j's outbox [P * chunk] = reduced gradient
   unsigned* flag1[XGMI_MAX_RANKS] = {};  // rank j's phase-1 flags [XGMI_MAX_WG][P]
   unsigned* flag2[XGMI_MAX_RANKS] = {};  // rank j's phase-2 flags [XGMI_MAX_WG][P]
+  unsigned* abort_[XGMI_MAX_RANKS] = {}; // rank j's sticky abort word (set by any rank that gives up)
   unsigned* ctr = nullptr;       // [XGMI_MAX_WG] local sequence counters
-  int* err = nullptr;            // set to 1 + phase on a timed-out wait
-  OptimArgs opt;
+  int* err = nullptr;            // phase (1, 2) of a timed-out wait; 3 = a peer aborted
+  OptimArgs opt;                 // p / s0 / s1 point at the bucket's first element
 };

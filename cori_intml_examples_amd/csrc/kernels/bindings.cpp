@@ -298,11 +298,20 @@ PYBIND11_MODULE(_kernels, m) {
   m.def(
       "dual_halo",
       [](const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits, uintptr_t s,
-         const RedTable* rt, const OptimArgs* ro, uintptr_t rgrad, int rfirst) {
+         const RedTable* rt, const OptimArgs* ro, uintptr_t rgrad, int rfirst, const WgradArgs* w2, int MT2,
+         int ntt2) {
         DualExtra x;
         if (rt && ro && rt->nblocks > 0) {
           x.rt = *rt, x.ro = *ro, x.grad = reinterpret_cast<float*>(rgrad);
           x.n_r = rt->nblocks, x.rfirst = rfirst;
+        }
+        if (w2 && ntt2 > 0) {
+          const int R_d = ca.R, P = w2->Ho / ca.Ho;
+          // the chained wgrad's blocks must tile exactly the rows of the dgrad blocks
+          if (P * ca.Ho != w2->Ho || ca.Ho % R_d || (P * R_d) % w2->R || w2->blocks_per_split != P * R_d / w2->R ||
+              w2->stride != 1 || w2->B != ca.B)
+            throw std::invalid_argument("dual_halo: chained wgrad geometry does not tile the dgrad blocks");
+          x.w2 = *w2, x.MT2 = MT2, x.ntt2 = ntt2;
         }
         const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, x, S(s));
         check_last("dual_halo");
@@ -310,7 +319,9 @@ PYBIND11_MODULE(_kernels, m) {
       },
       py::arg("ca"), py::arg("ntc"), py::arg("wa"), py::arg("MT"), py::arg("NTT"), py::arg("splits"), py::arg("s"),
       py::arg("rt") = nullptr, py::arg("ro") = nullptr, py::arg("rgrad") = 0, py::arg("rfirst") = 0,
-      "dual wgrad + dgrad launch; with (rt, ro, rgrad) it also runs that table's reduction + optimizer");
+      py::arg("w2") = nullptr, py::arg("MT2") = 0, py::arg("ntt2") = 0,
+      "dual wgrad + dgrad launch; with (rt, ro, rgrad) it also runs that table's reduction + optimizer; "
+      "with (w2, MT2, ntt2) each dgrad workgroup then runs the previous layer's wgrad over its rows");
   m.attr("MAX_STACK") = MAX_STACK;
   m.attr("MAX_STACK_SPLIT") = MAX_STACK_SPLIT;
   m.attr("STACK_THREADS") = conv_stack_threads();
@@ -328,14 +339,16 @@ PYBIND11_MODULE(_kernels, m) {
   py::class_<XgmiArgs>(m, "XgmiArgs")
       .def(py::init<>())
       RW(XgmiArgs, rank) RW(XgmiArgs, size) RW(XgmiArgs, n) RW(XgmiArgs, chunk) RW(XgmiArgs, sub)
-      RW(XgmiArgs, spin_limit) RW(XgmiArgs, mode) RW(XgmiArgs, fence) PTR(XgmiArgs, grad) PTR(XgmiArgs, ctr) PTR(XgmiArgs, err)
+      RW(XgmiArgs, timeout_ticks) RW(XgmiArgs, mode) RW(XgmiArgs, fence) PTR(XgmiArgs, grad) PTR(XgmiArgs, ctr) PTR(XgmiArgs, err)
       RW(XgmiArgs, opt)
-      .def("set_peer", [](XgmiArgs& a, int j, uintptr_t inbox, uintptr_t outbox, uintptr_t f1, uintptr_t f2) {
+      .def("set_peer", [](XgmiArgs& a, int j, uintptr_t inbox, uintptr_t outbox, uintptr_t f1, uintptr_t f2,
+                          uintptr_t ab) {
         if (j < 0 || j >= XGMI_MAX_RANKS) throw std::out_of_range("peer index");
         a.inbox[j] = reinterpret_cast<float*>(inbox);
         a.outbox[j] = reinterpret_cast<float*>(outbox);
         a.flag1[j] = reinterpret_cast<unsigned*>(f1);
         a.flag2[j] = reinterpret_cast<unsigned*>(f2);
+        a.abort_[j] = reinterpret_cast<unsigned*>(ab);
       });
   m.def("xgmi_grid", &xgmi_grid);
   m.def("xgmi_allreduce", [](const XgmiArgs& a, uintptr_t s) {
@@ -343,8 +356,10 @@ PYBIND11_MODULE(_kernels, m) {
     if (a.chunk % 4 || a.sub % 4 || a.sub <= 0 || (long long)a.chunk * a.size < a.n) throw std::invalid_argument("xgmi geometry");
     if (xgmi_grid(a) > XGMI_MAX_WG) throw std::invalid_argument("xgmi grid > XGMI_MAX_WG");
     for (int j = 0; j < a.size; ++j)
-      if (!a.inbox[j] || !a.outbox[j] || !a.flag1[j] || !a.flag2[j]) throw std::invalid_argument("xgmi peer not set");
+      if (!a.inbox[j] || !a.outbox[j] || !a.flag1[j] || !a.flag2[j] || !a.abort_[j])
+        throw std::invalid_argument("xgmi peer not set");
     if (!a.grad || !a.ctr || !a.err || (a.mode == 1 && (!a.opt.p || !a.opt.st))) throw std::invalid_argument("xgmi null pointer");
+    if (a.timeout_ticks <= 0) throw std::invalid_argument("xgmi timeout_ticks must be > 0");
     launch_xgmi_allreduce(a, S(s));
     check_last("xgmi_allreduce");
   });

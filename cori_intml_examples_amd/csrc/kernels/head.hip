@@ -321,7 +321,12 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
     // per-workgroup sums in a fixed row order, then order-independent integer atomics
     // spread over 16 slots: 128 workgroups on one address serialise at the L2 (~2 us)
     long long* slot = a.st->metric_slots[blockIdx.x & 15];
-    atomicAdd((unsigned long long*)&slot[0], (unsigned long long)llrint((double)ls * 4294967296.0));
+    // a non-finite loss (diverged trial) or one beyond the fixed-point range (|sum| >= 2^30
+    // per workgroup) cannot be converted: count it in the slot's spare word instead, and the
+    // host reports the loss as NaN (llrint of NaN/inf is undefined and would read as finite)
+    const bool loss_ok = isfinite(ls) && fabsf(ls) < 1073741824.f;
+    if (loss_ok) atomicAdd((unsigned long long*)&slot[0], (unsigned long long)llrint((double)ls * 4294967296.0));
+    else atomicAdd((unsigned long long*)&slot[3], 1ull);
     atomicAdd((unsigned long long*)&slot[1], (unsigned long long)llrintf(cs));
     atomicAdd((unsigned long long*)&slot[2], (unsigned long long)rows_here);
   }

@@ -39,13 +39,7 @@ template <int MTW, int NTT, bool CS4>
 static void wh_t(const WgradArgs& a, int MT, dim3 grid, size_t lds, hipStream_t s) {
   // few workgroups streaming several blocks each: pipeline their staging; a large grid
   // already hides it with resident workgroups (and keeps the lower VGPR count)
-  // INTML_WGRAD_PIPE=0/1 forces the choice (measurement knob)
-  static const int force = [] {
-    const char* e = getenv("INTML_WGRAD_PIPE");
-    return e && *e ? atoi(e) : -1;
-  }();
-  const bool pipe = force >= 0 ? (force > 0 && a.blocks_per_split > 1)
-                               : (grid.x * grid.y * grid.z < 512 && a.blocks_per_split > 1);
+  const bool pipe = grid.x * grid.y * grid.z < 512 && a.blocks_per_split > 1;
   auto k = pipe ? wgrad_halo_kernel<MTW, NTT, CS4, true> : wgrad_halo_kernel<MTW, NTT, CS4, false>;
   if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a, MT);

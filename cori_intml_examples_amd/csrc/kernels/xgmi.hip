@@ -21,6 +21,13 @@ namespace {
 
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+__device__ __forceinline__ unsigned sys_load(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Lanes 0..P-1 of wave 0 each raise flag `slot` of rank `lane` to seq.
 __device__ __forceinline__ void signal_all(unsigned* const* flags, int slot, int P, unsigned seq, int fence) {
   drain_stores();
@@ -31,29 +38,39 @@ __device__ __forceinline__ void signal_all(unsigned* const* flags, int slot, int
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       drain_stores();
     }
-    __hip_atomic_store(flags[t] + slot, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    sys_store(flags[t] + slot, seq);
   }
 }
 
 // Wait until local flags [base, base + P) all reach seq (lanes 0..P-1 poll one each).
-// Returns false (and sets *err) if a flag does not arrive within spin_limit polls.
-__device__ __forceinline__ bool wait_all(const unsigned* flags, int P, unsigned seq, int limit, int* err,
-                                         int phase, int fence) {
+// Bounded in TIME (wall_clock64, 100 MHz), not in polls.  On a timeout the lane records
+// `phase` in err and raises the sticky abort word of EVERY rank: a peer that is merely late
+// must never match a later step's flags against this step's data, so every later launch on
+// every rank exits at its first instruction (the host raises on the error word).  A rank that
+// sees the abort word while waiting gives up at once (err 3) instead of waiting out its own
+// timeout.  Returns false on either.
+__device__ __forceinline__ bool wait_all(const XgmiArgs& a, const unsigned* flags, unsigned seq, int phase) {
   __shared__ int s_ok;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, P = a.size;
   if (t == 0) s_ok = 1;
   __syncthreads();
   if (t < P) {
-    int spins = 0;
-    while (__hip_atomic_load(flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
-      if (++spins > limit) {
+    const unsigned long long t0 = wall_clock64();
+    while (sys_load(flags + t) < seq) {
+      if (sys_load(a.abort_[a.rank])) {
         s_ok = 0;
-        __hip_atomic_store(err, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      if ((long long)(wall_clock64() - t0) > a.timeout_ticks) {
+        s_ok = 0;
+        __hip_atomic_store(a.err, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int j = 0; j < P; ++j) sys_store(a.abort_[j], 1u);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (fence) {
+    if (a.fence) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       drain_stores();
     }
@@ -72,12 +89,57 @@ __device__ __forceinline__ float4 load4_guarded(const float* p, long long idx, l
   return v;
 }
 
+// grad[idx .. idx+4) = g4 (the reduced SUM) and, in mode 1, the Keras update of those
+// parameters with the 1/size average folded in (elements past n skipped)
+template <int KIND>
+__device__ __forceinline__ void finish4(const XgmiArgs& a, float* __restrict__ grad, long long idx, long long n,
+                                        const float4 g4) {
+  if (idx >= n) return;
+  const OptimArgs& o = a.opt;
+  if (idx + 4 <= n) {       // float4 path (idx, C, k multiples of 4: 16-byte aligned)
+    *reinterpret_cast<float4*>(grad + idx) = g4;
+    if (a.mode == 1) {
+      float4 p4 = *reinterpret_cast<const float4*>(o.p + idx);
+      float4 m4 = o.s0 ? *reinterpret_cast<const float4*>(o.s0 + idx) : float4{0.f, 0.f, 0.f, 0.f};
+      float4 v4 = o.s1 ? *reinterpret_cast<const float4*>(o.s1 + idx) : float4{0.f, 0.f, 0.f, 0.f};
+      const float gs = o.grad_scale;
+      opt_update<KIND>(o, o.st, p4.x, g4.x * gs, &m4.x, &v4.x);
+      opt_update<KIND>(o, o.st, p4.y, g4.y * gs, &m4.y, &v4.y);
+      opt_update<KIND>(o, o.st, p4.z, g4.z * gs, &m4.z, &v4.z);
+      opt_update<KIND>(o, o.st, p4.w, g4.w * gs, &m4.w, &v4.w);
+      *reinterpret_cast<float4*>(o.p + idx) = p4;
+      if (o.s0) *reinterpret_cast<float4*>(o.s0 + idx) = m4;
+      if (o.s1) *reinterpret_cast<float4*>(o.s1 + idx) = v4;
+    }
+    return;
+  }
+  const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+  for (int e = 0; e < (int)(n - idx); ++e) {
+    grad[idx + e] = gv[e];
+    if (a.mode == 1) {
+      float pe = o.p[idx + e];
+      float s0 = o.s0 ? o.s0[idx + e] : 0.f, s1 = o.s1 ? o.s1[idx + e] : 0.f;
+      opt_update<KIND>(o, o.st, pe, gv[e] * o.grad_scale, &s0, &s1);
+      o.p[idx + e] = pe;
+      if (o.s0) o.s0[idx + e] = s0;
+      if (o.s1) o.s1[idx + e] = s1;
+    }
+  }
+}
+
 template <int KIND>
 __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
   __shared__ unsigned s_seq;
+  __shared__ int s_abort;
   const int w = blockIdx.x, t = threadIdx.x;
-  if (t == 0) s_seq = a.ctr[w] + 1u;
+  if (t == 0) {
+    s_seq = a.ctr[w] + 1u;
+    // sticky abort (a rank timed out in an earlier launch): touch nothing, keep the counters
+    s_abort = sys_load(a.abort_[a.rank]) != 0u;
+    if (s_abort) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   __syncthreads();
+  if (s_abort) return;
   const unsigned seq = s_seq;
   const int P = a.size, r = a.rank, C = a.chunk;
   const int k0 = w * a.sub, k1 = min(k0 + a.sub, C);
@@ -86,88 +148,64 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
   // Every phase first loads all P float4 of a thread into registers, then stores: the
   // compiler cannot reorder loads across stores to possibly-aliasing pointers, and each
   // uncached / remote access costs microseconds, so they must all be in flight together.
+  // The owner's own chunk never leaves cached memory: it is not pushed to the own inbox
+  // (phase 2 reads it from grad), and its reduced sum + update are written straight to grad
+  // in phase 2 (not round-tripped through the own outbox) -- at P = 1 (loopback) the kernel
+  // touches no uncached memory besides the flags.
   float* __restrict__ grad = a.grad;
 
-  // 1. push my slice of every chunk to its owner's inbox row r
-  for (int k = k0 + 4 * t; k < k1; k += 1024) {
-    float4 v[XGMI_MAX_RANKS];
-#pragma unroll
-    for (int j = 0; j < XGMI_MAX_RANKS; ++j)
-      if (j < P) v[j] = load4_guarded(grad, (long long)j * C + k, n);
-#pragma unroll
-    for (int j = 0; j < XGMI_MAX_RANKS; ++j)
-      if (j < P) *reinterpret_cast<float4*>(a.inbox[j] + (size_t)r * C + k) = v[j];
-  }
-  signal_all(a.flag1, w * P + r, P, seq, a.fence);
-
-  // 2. reduce my chunk's slice over the P rows in rank order, push it to every outbox
-  bool ok = wait_all(a.flag1[r] + w * P, P, seq, a.spin_limit, a.err, 1, a.fence);
-  if (ok) {
-    const float* __restrict__ in = a.inbox[r];
+  // 1. push my slice of every OTHER rank's chunk to its owner's inbox row r
+  if (P > 1) {
     for (int k = k0 + 4 * t; k < k1; k += 1024) {
       float4 v[XGMI_MAX_RANKS];
 #pragma unroll
+      for (int j = 0; j < XGMI_MAX_RANKS; ++j)
+        if (j < P && j != r) v[j] = load4_guarded(grad, (long long)j * C + k, n);
+#pragma unroll
+      for (int j = 0; j < XGMI_MAX_RANKS; ++j)
+        if (j < P && j != r) *reinterpret_cast<float4*>(a.inbox[j] + (size_t)r * C + k) = v[j];
+    }
+  }
+  signal_all(a.flag1, w * P + r, P, seq, a.fence);
+
+  // 2. reduce my chunk's slice over the P rows in rank order (my own row from grad), push
+  //    it to every other rank's outbox, and finish my own chunk in place
+  if (!wait_all(a, a.flag1[r] + w * P, seq, 1)) return;
+  {
+    const float* __restrict__ in = a.inbox[r];
+    for (int k = k0 + 4 * t; k < k1; k += 1024) {
+      const long long own = (long long)r * C + k;
+      float4 v[XGMI_MAX_RANKS];
+#pragma unroll
       for (int q = 0; q < XGMI_MAX_RANKS; ++q)
-        if (q < P) v[q] = *reinterpret_cast<const float4*>(in + (size_t)q * C + k);
+        if (q < P) v[q] = q == r ? load4_guarded(grad, own, n) : *reinterpret_cast<const float4*>(in + (size_t)q * C + k);
       float4 s4 = v[0];
 #pragma unroll
       for (int q = 1; q < XGMI_MAX_RANKS; ++q)
         if (q < P) { s4.x += v[q].x; s4.y += v[q].y; s4.z += v[q].z; s4.w += v[q].w; }
 #pragma unroll
       for (int j = 0; j < XGMI_MAX_RANKS; ++j)
-        if (j < P) *reinterpret_cast<float4*>(a.outbox[j] + (size_t)r * C + k) = s4;
+        if (j < P && j != r) *reinterpret_cast<float4*>(a.outbox[j] + (size_t)r * C + k) = s4;
+      finish4<KIND>(a, grad, own, n, s4);
     }
   }
   signal_all(a.flag2, w * P + r, P, seq, a.fence);
 
-  // 3. the whole reduced gradient is in my outbox: record it and update the parameters
-  ok = wait_all(a.flag2[r] + w * P, P, seq, a.spin_limit, a.err, 2, a.fence) && ok;
-  if (ok) {
+  // 3. every other chunk's reduced sum is in my outbox: record it and update the parameters
+  if (!wait_all(a, a.flag2[r] + w * P, seq, 2)) return;
+  if (P > 1) {
     const float* __restrict__ red = a.outbox[r];
-    const OptimArgs& o = a.opt;
     for (int k = k0 + 4 * t; k < k1; k += 1024) {
       float4 g[XGMI_MAX_RANKS];
 #pragma unroll
       for (int q = 0; q < XGMI_MAX_RANKS; ++q)
-        if (q < P) g[q] = *reinterpret_cast<const float4*>(red + (size_t)q * C + k);
+        if (q < P && q != r) g[q] = *reinterpret_cast<const float4*>(red + (size_t)q * C + k);
 #pragma unroll
-      for (int q = 0; q < XGMI_MAX_RANKS; ++q) {
-        const long long idx = (long long)q * C + k;
-        if (q >= P || idx >= n) continue;
-        const float4 g4 = g[q];
-        if (idx + 4 <= n) {       // float4 path (idx, C, k multiples of 4: 16-byte aligned)
-          *reinterpret_cast<float4*>(grad + idx) = g4;
-          if (a.mode == 1) {
-            float4 p4 = *reinterpret_cast<const float4*>(o.p + idx);
-            float4 m4 = o.s0 ? *reinterpret_cast<const float4*>(o.s0 + idx) : float4{0.f, 0.f, 0.f, 0.f};
-            float4 v4 = o.s1 ? *reinterpret_cast<const float4*>(o.s1 + idx) : float4{0.f, 0.f, 0.f, 0.f};
-            const float gs = o.grad_scale;
-            opt_update<KIND>(o, o.st, p4.x, g4.x * gs, &m4.x, &v4.x);
-            opt_update<KIND>(o, o.st, p4.y, g4.y * gs, &m4.y, &v4.y);
-            opt_update<KIND>(o, o.st, p4.z, g4.z * gs, &m4.z, &v4.z);
-            opt_update<KIND>(o, o.st, p4.w, g4.w * gs, &m4.w, &v4.w);
-            *reinterpret_cast<float4*>(o.p + idx) = p4;
-            if (o.s0) *reinterpret_cast<float4*>(o.s0 + idx) = m4;
-            if (o.s1) *reinterpret_cast<float4*>(o.s1 + idx) = v4;
-          }
-          continue;
-        }
-        const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
-        for (int e = 0; e < (int)(n - idx); ++e) {
-          grad[idx + e] = gv[e];
-          if (a.mode == 1) {
-            float pe = o.p[idx + e];
-            float s0 = o.s0 ? o.s0[idx + e] : 0.f, s1 = o.s1 ? o.s1[idx + e] : 0.f;
-            opt_update<KIND>(o, o.st, pe, gv[e] * o.grad_scale, &s0, &s1);
-            o.p[idx + e] = pe;
-            if (o.s0) o.s0[idx + e] = s0;
-            if (o.s1) o.s1[idx + e] = s1;
-          }
-        }
-      }
+      for (int q = 0; q < XGMI_MAX_RANKS; ++q)
+        if (q < P && q != r) finish4<KIND>(a, grad, (long long)q * C + k, n, g[q]);
     }
-    if (a.mode == 1 && o.defer_pack && w == 0 && t == 0) o.st->packs_stale = 1;
   }
+  if (a.mode == 1 && a.opt.defer_pack && w == 0 && t == 0) a.opt.st->packs_stale = 1;
   if (t == 0) a.ctr[w] = seq;
 }
 

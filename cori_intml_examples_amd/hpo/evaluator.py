@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import os
 import queue
+import math
 import re
 import shlex
 import socket
@@ -40,6 +41,21 @@ def parse_fom(text: str) -> Optional[float]:
     """Last ``FoM: <float>`` in ``text`` (every DP rank prints it; they agree)."""
     m = _FOM.findall(text or "")
     return float(m[-1]) if m else None
+
+
+def figure_of_merit(val_losses: Sequence[float], mode: str = "best") -> float:
+    """The FoM a training CLI prints (``train_rpv.py:76-79``): the min ("best") or last
+    validation loss.  Non-finite epochs (a diverged trial's NaN/inf losses) never win the
+    min -- Python's ``min`` with a NaN in the list is order-dependent -- and a run with no
+    finite epoch (or a non-finite last epoch in "last" mode) scores NaN, which the
+    evaluators and the genetic optimizer rank worst."""
+    vals = [float(v) for v in val_losses]
+    if not vals:
+        return float("nan")
+    if mode == "last":
+        return vals[-1] if math.isfinite(vals[-1]) else float("nan")
+    fin = [v for v in vals if math.isfinite(v)]
+    return min(fin) if fin else float("nan")
 
 
 def run_group(cmd: Sequence[str], env=None, timeout: Optional[float] = None, cwd=None,

@@ -24,7 +24,7 @@ import torch
 
 from ..ops.hip import kernels
 from ..ops.rng import keep_threshold
-from ..utils.env import env_flag
+from ..utils.env import env_flag, tune
 from .executor_base import DeviceData, Executor, prepare_targets
 from .plan import Plan
 
@@ -124,54 +124,35 @@ def splice_bucket_launches(launches, inserts, per_bucket):
         out.extend(launches[pos:at])
         pos = at
         for pat, make, tag in per_bucket:
-            out.append((pat % k, make(k), tag))
+            fn = make(k)
+            if fn is not None:          # a factory returns None for buckets it does not apply to
+                out.append((pat % k, fn, tag))
         ready[k] = len(out)
     out.extend(launches[pos:])
     return out, ready
 
 
-def stream_program(tags, side=False, opt=False, comm=True):
+def stream_program(tags, comm=True):
     """The stream schedule of a launch sequence, as a list of ops:
-    ("run", stream, i)  launch i on "main" / "side" / "opt" / "comm";
+    ("run", stream, i)  launch i on "main" / "comm";
     ("wait", dst, src)  make stream dst wait for everything issued so far on src.
 
-    'main' launches run in order on the current stream.  'side' launches (weight gradients,
-    slab reductions) run on the side stream when there is one (else on main), each after the
-    latest main launch before it.  'comm' launches fork the comm stream after everything
-    issued so far (main and side: the bucket's slab reduction) -- RCCL and the bucket's
-    optimizer run there while main continues the backward.  'opt' launches (early per-bucket
-    optimizer) wait for all three.  Every used stream is joined back into main at the end.
-    ``comm=False``: comm launches run in order on main (a linear graph)."""
-    ops, used = [], set()
-    main_moved = True
+    'main' launches (any tag other than 'comm': 'side' marks the launches that only feed a
+    slab reduction) run in order on the current stream.  'comm' launches fork the comm
+    stream after everything issued so far (the bucket's slab reduction) -- RCCL and the
+    bucket's optimizer run there while main continues the backward -- and the comm stream
+    is joined back into main at the end.  ``comm=False``: comm launches run in order on main
+    (a linear graph)."""
+    ops, used = [], False
     for i, tag in enumerate(tags):
-        if tag == "side" and side:
-            if main_moved:
-                ops.append(("wait", "side", "main"))
-                main_moved = False
-            ops.append(("run", "side", i))
-            used.add("side")
-        elif tag == "opt":
-            if not opt:
-                continue
-            ops.append(("wait", "opt", "main"))
-            for src in ("side", "comm"):
-                if src in used:
-                    ops.append(("wait", "opt", src))
-            ops.append(("run", "opt", i))
-            used.add("opt")
-        elif tag == "comm" and comm:
+        if tag == "comm" and comm:
             ops.append(("wait", "comm", "main"))
-            if "side" in used:
-                ops.append(("wait", "comm", "side"))
             ops.append(("run", "comm", i))
-            used.add("comm")
+            used = True
         else:
             ops.append(("run", "main", i))
-            main_moved = True
-    for src in ("side", "opt", "comm"):
-        if src in used:
-            ops.append(("wait", "main", src))
+    if used:
+        ops.append(("wait", "main", "comm"))
     return ops
 
 
@@ -456,7 +437,9 @@ class HipExecutor(Executor):
         # exact; integer sums over the slots are order-independent
         o = self.K.STEP_STATE_METRICS_OFFSET // 8
         v = self.state.view(torch.int64)[o:o + 4 * self.K.STEP_STATE_METRIC_SLOTS].view(-1, 4).sum(0).tolist()
-        return [v[0] / 4294967296.0, float(v[1]), float(v[2])]
+        # v[3] counts head workgroups whose loss was non-finite or out of fixed-point range:
+        # the loss is then NaN (sticky until reset_metrics), never a finite garbage value
+        return [v[0] / 4294967296.0 if v[3] == 0 else float("nan"), float(v[1]), float(v[2])]
 
     def reset_metrics(self):
         o = self.K.STEP_STATE_METRICS_OFFSET // 8
@@ -474,7 +457,7 @@ class HipExecutor(Executor):
         pl, pc, pn = self._metrics_prev
         self._metrics_prev = (ls, cs, n)
         dn = max(n - pn, 1.0)
-        return (ls - pl) / dn, (cs - pc) / dn
+        return (ls - pl) / dn, (cs - pc) / dn   # NaN propagates once the flag is set
 
     def synchronize(self):
         torch.cuda.synchronize(self.device)
@@ -492,23 +475,16 @@ class BatchPlan:
         self.graph = None
         self.multi_graphs: Dict[int, torch.cuda.CUDAGraph] = {}   # k -> graph of k steps
         self.dp_graphs = None
-        self.side = torch.cuda.Stream(device=dev) if env_flag("INTML_TWO_STREAMS", False) else None
-        # opt-in: per-bucket optimizer (+ weight re-pack) on its own stream as soon as the
-        # bucket's gradients are final and no later backward kernel reads its packs, so the
-        # dense layer's update overlaps the conv backward.  Measured slower on one MI355X
-        # (the memory-bound update steals HBM bandwidth from the concurrent wgrad and the
-        # split launches cost more than they hide: RPV 200 -> 229 us, legacy 1.42 -> 1.44 ms)
-        self.early_optim = self.training and env_flag("INTML_EARLY_OPTIM", False)
-        self.opt_stream = torch.cuda.Stream(device=dev) if self.early_optim else None
-        self.opt_at = []
+        # (a second compute stream for the weight gradients and a per-bucket early optimizer
+        # stream were measured slower on one MI355X and removed: docs/ARCHITECTURE.md §6)
         self.optim_fused = False           # set by _build_reduce
         self.early_red = {}                # dual launch name -> (RedTable, span): set by _build_reduce
         # Native RCCL data plane: the bucket all-reduces are part of the launch sequence (on
         # their own comm stream) and captured with the rest of the step into ONE HIP graph.
         red = ex.reducer
         self.comm_in_graph = (self.training and red is not None and getattr(red, "capturable", False)
-                              and red.active and env_flag("INTML_COMM_CAPTURE", True))
-        # INTML_COMM_FORK=0: the captured all-reduces stay on the main stream (a linear graph:
+                              and red.active and tune("comm_capture", True))
+        # tune comm_fork=0: the captured all-reduces stay on the main stream (a linear graph:
         # no cross-queue edges, whose graph-launch cost is several us each, but no overlap)
         # (default: fork only when there is more than one bucket to overlap; set in _build_reduce)
         self.comm_fork = None
@@ -516,8 +492,7 @@ class BatchPlan:
         # ... and each bucket's optimizer update follows its all-reduce on the comm stream (the
         # 1/size average folded in), so the dense bucket's update overlaps the conv backward and
         # only the last bucket's (small) update is on the step's tail
-        self.optim_on_comm = (self.comm_in_graph and not self.early_optim
-                              and env_flag("INTML_DP_OPTIM_ON_COMM", True))
+        self.optim_on_comm = self.comm_in_graph and tune("dp_optim_on_comm", True)
         z = lambda *s, dt=BF16: torch.zeros(*s, dtype=dt, device=dev)
         self.xb = z(bs, ex.in_H * ex.in_W * ex.in_Cs)
         self.yb = z(bs, ex.plan.head.N, dt=torch.float32)
@@ -618,20 +593,12 @@ class BatchPlan:
         # one prologue launch: gather + the previous update's weight re-pack (training: always,
         # except with per-bucket optimizers that pack themselves; eval/predict: only if an
         # optimizer ran since the last pack) + the step bookkeeping
-        stack = self._conv_stack_args(training) if env_flag("INTML_CONV_STACK", True) else None
-        if stack is not None and env_flag("INTML_STACK_DIRECT", False) and self._stack_xrows(stack):
-            # opt-in: the conv stack reads each image straight from the dataset (same row rule
-            # as the gather) and writes the batch buffer for the backward itself, the prologue
-            # gathers only the targets (measured neutral on the RPV step: the prologue's 1 us
-            # moves into the conv stack's staging)
-            stack.src_mode = 1 if training else 2
-            stack.xout = self.xb.data_ptr()
-            ga.skip_x = 1
+        stack = self._conv_stack_args(training) if tune("conv_stack", True) else None
         pa = K.PrologueArgs()
         pa.sb, pa.ga = sb, ga
         pa.gather_gx = 1 if ga.skip_x else K.gather_gx(ga.R)
         pa.gather_blocks = pa.gather_gx * bs
-        pa.pack_mode = (0 if self.early_optim else 1) if training else 2
+        pa.pack_mode = 1 if training else 2
         pa.master = store.master.data_ptr()
         pa.arena = ex.arena.data_ptr()
         self.launches.append(("prologue", lambda s, a=pa: K.prologue(a, ex.pack_table, s)))
@@ -690,7 +657,7 @@ class BatchPlan:
                 e.drop_scale = 1.0 / (1.0 - g.rate)
             e.seed, e.stream_id, e.st = ex.seed, g.stream, st_ptr
             if (g.j == len(ex.denses) - 1 and ex.head_src.kind == "dense" and g.Ns <= K.head_epi_max()
-                    and env_flag("INTML_FUSE_HEAD", True)):
+                    and tune("fuse_head", True)):
                 # the head launch (one row per workgroup, the row's split groups in parallel)
                 # reduces this layer's partials itself: one kernel boundary fewer
                 head_epi = e
@@ -747,8 +714,7 @@ class BatchPlan:
         # slower on RPV at batch 128: the 128 wgrad workgroups move the layer's 14 MB of optimizer
         # state at per-CU bandwidth (wgrad 6.1 -> 9.7 us) while the end-of-step reduction, which
         # spreads it over thousands of workgroups, only drops 10.8 -> 8.2 us
-        self.dense_opt_ok = (ex.reducer is None and self.side is None and not self.early_optim
-                             and env_flag("INTML_FUSE_OPTIM", True) and env_flag("INTML_DENSE_OPT", False))
+        self.dense_opt_ok = ex.reducer is None and tune("fuse_optim", True) and tune("dense_opt", False)
 
         for g, ds in reversed(list(zip(ex.denses, ex.plan.denses))):
             xin = self._src_buf(g.src)
@@ -761,7 +727,7 @@ class BatchPlan:
             direct_ptr = (store.grad.data_ptr() + 4 * sp.offset) if direct else None
             # dense_bwd.hip kernels (per-wave pipelined wgrad, vectorised dX epilogue) where the
             # 8-element alignment they assume holds; the generic wgrad / split-K path otherwise
-            bwd2 = (env_flag("INTML_DENSE_BWD2", True) and g.src.width % 8 == 0 and g.Ns % 8 == 0)
+            bwd2 = tune("dense_bwd2", True) and g.src.width % 8 == 0 and g.Ns % 8 == 0
             fused_opt = False
             if bwd2:
                 wa, cfg, slab, bslab = self._dense_wgrad_args(xin, g.src.width, self.dense_dh[g.j], g.Ns, g.N, bs,
@@ -813,7 +779,7 @@ class BatchPlan:
                 dname = "dense_dx%d" % g.j
                 ntc = self._dense_dx_ntc(a) if (bwd2 and a.bt.pCs % 8 == 0 and a.Ks % 8 == 0
                                                and not K.dense_big(a.NT, a.KS)) else 0
-                if self.side is None and env_flag("INTML_DUAL_DENSE", True):
+                if tune("dual_dense", True):
                     # one launch for the dense wgrad and dX (independent GEMMs over dH), in the
                     # wgrad's slot (its slabs are final after it)
                     dname = "dense_bwd%d" % g.j
@@ -830,9 +796,24 @@ class BatchPlan:
                     self.launches.append((dname, lambda s, a=a: K.dense_fwd(a, s)))
                 self.pack_readers.append((dname, sp.offset, sp.offset + sp.numel))
 
+        self.chain = {}            # dual launch name -> (WgradArgs, MT, NTT) of a chained wgrad
+        dual_args = {}             # conv index -> (dual launch name, its dgrad ConvMMArgs, ntc)
         for g, cs in reversed(list(zip(ex.convs, ex.plan.convs))):
             xin = self.xb if g.i == 0 else self.conv_out[g.i - 1]
-            if self._wide(g.Cs_in, g.KS, g.NT):
+            chain = None
+            if g.i == 0 and 1 in dual_args and g.Cs_in == 4 and g.stride == 1 and tune("chain_wgrad", True):
+                dname1, da1, ntc1 = dual_args[1]
+                rows = self._chain_rows(g, da1)
+                if (rows is not None and ntc1 == 1 and cdiv(da1.NT, ntc1) == 1 and g.NT <= 1
+                        and cdiv(g.KH * g.KW * g.Cs_in, 16) + (1 if cs.conv.use_bias else 0) <= 4):
+                    chain = (rows[0], rows[1], bs * (da1.Ho // da1.R))
+            if chain is not None:
+                # the first layer's wgrad runs inside the layer-2 dual launch (DualExtra::w2):
+                # its slabs are final after that launch
+                wa, cfg, slab, bslab = self._wgrad_halo_args(xin, g, bs, cs.conv.use_bias, chain=chain)
+                self.chain[dname1] = (wa, cfg[0], cfg[1])
+                assert self.launches[-1][0] == dname1     # ready with the dual launch
+            elif self._wide(g.Cs_in, g.KS, g.NT):
                 wa, cfg, slab, bslab = self._wgrad_tile_args(xin, g, bs, cs.conv.use_bias)
                 self.launches.append(("wgrad_conv%d" % g.i, lambda s, a=wa, c=cfg: K.wgrad_tile(a, c[0], s),
                                       "side"))
@@ -870,13 +851,14 @@ class BatchPlan:
                 a.st = st_ptr
                 a.bt = self._bt_for(Src("conv", prev.i, prev.Cout, prev.Cs_out, prev.Hp, prev.Wp))
                 dname = "dgrad_conv%d" % g.i
-                dual = (self.side is None and env_flag("INTML_DUAL_HALO", True)
+                dual = (tune("dual_halo", True)
                         and not self._wide(g.Cs_in, g.KS, g.NT) and not self._wide(a.Cs_in, a.KS, g.NTd))
                 if dual:
                     # one launch for the layer's wgrad and dgrad (independent GEMMs sharing dY):
                     # replaces the wgrad launch in place (its slabs are final after it)
                     ntc = self._halo_cfg(a, g.NTd, False, dual=True)
                     dname = "wgrad_dgrad_conv%d" % g.i
+                    dual_args[g.i] = (dname, a, ntc)
                     self.launches[w_at] = (dname, lambda s, a=a, n=ntc, w=wa, c=cfg, nm=dname: self._dual(a, n, w, c, s, nm),
                                            "main")
                 else:
@@ -899,7 +881,7 @@ class BatchPlan:
                 return None
 
         # row bands per image: enough workgroups to cover the 256 CUs at small batches
-        want = int(os.environ.get("INTML_STACK_SPLITS", "0")) or cdiv(256, self.bs)
+        want = tune("stack_splits", 0) or cdiv(256, self.bs)
         splits = max(1, min(K.MAX_STACK_SPLIT, want))
         while splits > 1 and self._stack_rows(convs, splits) is None:
             splits -= 1
@@ -916,7 +898,7 @@ class BatchPlan:
         a.B, a.n, a.seed, a.st = self.bs, n, ex.seed, ex.state.data_ptr()
         a.off_w, a.off_codes, a.lds_bytes = off_w, off_codes, lds
         a.off_bias = off_bias
-        a.dbg = int(os.environ.get("INTML_STACK_DBG", "0"))
+        a.dbg = tune("stack_dbg", 0)
         a.set_buf_offsets(off_b0, off_b1)
         a.splits = splits
         for l in range(n):
@@ -944,32 +926,6 @@ class BatchPlan:
             a.set_layer(i, L)
         self.stack_splits = splits
         return a
-
-    def _stack_xrows(self, a):
-        """Partition of the input rows over the conv stack's bands for the in-place read
-        (each band copies its share to the batch buffer): band sp takes the input rows
-        centred on its owned conv rows, the first band from row 0, the last to row H.
-        False (keep the prologue gather) unless every share lies in its staged halo rows."""
-        g = self.ex.convs[0]
-        P = 2 if g.pool else 1
-        off = (g.KH - 1) // 2 - g.pad_t
-        S = a.splits
-        rows = self._stack_rows(self.ex.convs, S)
-        prev = 0
-        spans = []
-        for sp in range(S):
-            c0, c1, own0, own1, ib, ih = rows[0][sp]
-            lo = 0 if sp == 0 else P * own0 + off
-            hi = g.H if sp == S - 1 else P * own1 + off
-            if lo != prev or hi < lo or lo < ib or hi > ib + ih:
-                return False
-            spans.append((lo, hi))
-            prev = hi
-        if prev != g.H:
-            return False
-        for sp, (lo, hi) in enumerate(spans):
-            a.set_xrows(sp, lo, hi)
-        return True
 
     @staticmethod
     def _stack_rows(convs, splits):
@@ -1053,7 +1009,7 @@ class BatchPlan:
             ntc = 8 if NT > 4 else (4 if NT > 2 else 2)
             if K.conv_tile_lds_bytes(ntc) > 150 * 1024:
                 raise NotImplementedError("conv tile LDS")
-            if env_flag("INTML_CONV_GLDS", True):
+            if tune("conv_glds", True):
                 a.zero = self._zero_buf().data_ptr()
             return lambda s, a=a, n=ntc: K.conv_tile(a, n, s)
         ntc = self._halo_cfg(a, NT, pool)
@@ -1071,9 +1027,15 @@ class BatchPlan:
         if early is not None:   # this launch also carries an early bucket's reduction + optimizer
             opt, grad = ex._optim_args(False, defer_pack=True), ex.store.grad.data_ptr()
             ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, early[0], opt, grad,
-                             int(env_flag("INTML_EARLY_REDUCE_FIRST", False)))
+                             0)
         else:
-            ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s)
+            ch = self.chain.get(name)
+            if ch is not None:
+                ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, w2=ch[0], MT2=ch[1], ntt2=ch[2])
+                if not ok:
+                    raise RuntimeError("dual_halo: chained wgrad combination not instantiated (%s)" % name)
+            else:
+                ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s)
         if not ok:   # unsupported combination
             K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
             K.conv_halo(a, ntc, s)
@@ -1085,11 +1047,11 @@ class BatchPlan:
         largest block that still leaves >= `want` workgroups (a dgrad co-scheduled with its
         wgrad in one launch wants fewer, longer workgroups: each stages the whole weight
         slice, and the launch should fit the CUs in one wave)."""
-        want = int(os.environ.get("INTML_DGRAD_MIN_WGS", "256") if dual else os.environ.get("INTML_HALO_MIN_WGS", "512"))
+        want = tune("dgrad_min_wgs", 256) if dual else tune("halo_min_wgs", 512)
         KS = a.KS
         # co-scheduled dgrad: one n-tile per workgroup and whole-image blocks (measured on the
         # RPV stack: each workgroup stages half the weights, the launch fits the CUs in one wave)
-        ntc = int(os.environ.get("INTML_DGRAD_NTC", "1")) if dual else 8
+        ntc = tune("dgrad_ntc", 1) if dual else 8
         while ntc > 1 and (ntc > NT or KS * ntc > 64):
             ntc //= 2
         if KS * ntc > 96:
@@ -1135,8 +1097,8 @@ class BatchPlan:
             a.dHp, a.dWp = g.Hp, g.Wp
         a.NT = g.NT
         ntc = 8 if g.NT > 4 else (4 if g.NT > 2 else 2)
-        ntc = min(ntc, int(os.environ.get("INTML_WGRAD_TILE_NTC", ntc)))
-        if env_flag("INTML_CONV_GLDS", True):
+        ntc = min(ntc, tune("wgrad_tile_ntc", ntc))
+        if tune("conv_glds", True):
             a.zero = self._zero_buf().data_ptr()
         P = bs * g.Ho * g.Wo
         a.P = P
@@ -1152,7 +1114,29 @@ class BatchPlan:
         self.wgrad_slabs.append((slab, bslab))
         return a, (ntc, None, S), slab, bslab
 
-    def _wgrad_halo_args(self, xin, g, bs, bias):
+    def _chain_rows(self, g, da):
+        """Rows per block of a first-layer wgrad chained onto the dgrad blocks of ``da`` (the
+        layer-2 dual launch): the largest divisor of the conv rows one dgrad block feeds whose
+        block stays within ~512 pixels and the kernel's register staging pipeline; None if
+        the dgrad blocks cannot be tiled (see DualExtra in args.h)."""
+        if da.Ho <= 0 or g.Ho % da.Ho or da.Ho % da.R:
+            return None
+        P = g.Ho // da.Ho
+        rows = P * da.R
+        W_in = (g.Wo - 1) * g.stride + g.KW
+        cpp = g.Cs_in // 4
+        for r in range(rows, 0, -1):
+            if rows % r or r * g.Wo > 512:
+                continue
+            nch_x = ((r - 1) * g.stride + g.KH) * W_in * cpp
+            nch_y = cdiv(r * g.Wo, 32) * 32 * 2
+            if nch_x <= 1024 and nch_y <= 1024:
+                return r, rows // r
+        return None
+
+    def _wgrad_halo_args(self, xin, g, bs, bias, chain=None):
+        """``chain`` = (R, blocks_per_split, splits): the geometry of a wgrad chained onto a
+        dual launch's dgrad blocks (one slab per dgrad block) instead of the standalone one."""
         K, dev = self.ex.K, self.ex.device
         a = K.WgradArgs()
         a.x = xin.data_ptr()
@@ -1175,9 +1159,8 @@ class BatchPlan:
         # rows per block: ~256 pixels, at most 8 rows (measured best at batch 128 for the
         # RPV and MNIST stacks), bounded LDS
         W_in = (g.Wo - 1) * g.stride + g.KW
-        pxs = os.environ.get("INTML_WGRAD_BLOCK_PX", "256").split(",")
-        px = int(pxs[min(g.i, len(pxs) - 1)])
-        R = max(1, min(g.Ho, px // max(1, g.Wo), int(os.environ.get("INTML_WGRAD_MAX_ROWS", "8"))))
+        px = tune("wgrad_block_px%d" % g.i, tune("wgrad_block_px", 256))
+        R = max(1, min(g.Ho, px // max(1, g.Wo), tune("wgrad_max_rows", 8)))
         # prefer the largest R whose block staging fits the kernel's register pipeline
         # (<= 4 X-halo and 4 dY chunks per thread, wgrad_halo_body.h WH_PX / WH_PY)
         cpp = g.Cs_in // (4 if g.Cs_in == 4 else 8)
@@ -1193,15 +1176,19 @@ class BatchPlan:
                 break
         while R > 1 and (((R - 1) * g.stride + g.KH) * W_in * g.Cs_in * 2 > 64 * 1024):
             R -= 1
-        a.R = R
-        nblocks = bs * cdiv(g.Ho, R)
-        groups = cdiv(NT, NTT) * cdiv(a.Ktiles, MT)
-        per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
-        s_budget = max(1, (8 << 20) // per_split_bytes)
-        cap = int(os.environ.get("INTML_WGRAD_SPLITS", "1024"))
-        S = max(1, min(nblocks, s_budget, max(1, cap // groups)))
-        bps = cdiv(nblocks, S)
-        S = cdiv(nblocks, bps)
+        if chain is not None:
+            R, bps, S = chain
+            a.R = R
+        else:
+            a.R = R
+            nblocks = bs * cdiv(g.Ho, R)
+            groups = cdiv(NT, NTT) * cdiv(a.Ktiles, MT)
+            per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
+            s_budget = max(1, (8 << 20) // per_split_bytes)
+            cap = tune("wgrad_splits", 1024)
+            S = max(1, min(nblocks, s_budget, max(1, cap // groups)))
+            bps = cdiv(nblocks, S)
+            S = cdiv(nblocks, bps)
         a.blocks_per_split = bps
         lds = K.wgrad_halo_lds_bytes(a, MT, NTT)
         if lds > 150 * 1024:
@@ -1270,8 +1257,8 @@ class BatchPlan:
         kg = 2
         groups = cdiv(a.Ktiles, kg) * cdiv(NT, ntt)
         per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
-        s_budget = max(1, (int(os.environ.get("INTML_DW_SLAB_MB", "8")) << 20) // per_split_bytes)
-        S = 1 if direct else max(1, min(s_budget, cdiv(int(os.environ.get("INTML_DW_MIN_WGS", "256")), groups),
+        s_budget = max(1, (tune("dw_slab_mb", 8) << 20) // per_split_bytes)
+        S = 1 if direct else max(1, min(s_budget, cdiv(tune("dw_min_wgs", 256), groups),
                                         cdiv(bs, 128)))
         pps = cdiv(cdiv(bs, S), 32) * 32
         S = cdiv(bs, pps)
@@ -1286,10 +1273,10 @@ class BatchPlan:
     @staticmethod
     def _dense_dx_ntc(a):
         """n-tiles per wave of dense_dx_kernel: the most A-fragment reuse that still leaves
-        >= INTML_DX_MIN_WGS workgroups (4 waves x 16 rows each)."""
-        if "INTML_DX_NTC" in os.environ:
-            return int(os.environ["INTML_DX_NTC"])
-        want = int(os.environ.get("INTML_DX_MIN_WGS", "512"))
+        >= tune dx_min_wgs workgroups (4 waves x 16 rows each)."""
+        if tune("dx_ntc", 0):
+            return tune("dx_ntc", 0)
+        want = tune("dx_min_wgs", 512)
         for ntc in (4, 2):
             if cdiv(a.M, 64) * cdiv(a.NT, ntc) >= want:
                 return ntc
@@ -1313,13 +1300,12 @@ class BatchPlan:
             # single stream, no all-reduce to overlap: ONE reduction launch at the end of the
             # backward (each launch boundary costs ~5 us here), if the descriptors fit a table
             ndesc = sum(len(d) for _, _, d in self.red_groups)
-            one = self.side is None and ndesc <= 16
+            one = ndesc <= 16
             limit = 1 << 62 if one else int(os.environ.get("INTML_BUCKET_BYTES", 1 << 20))
             # ... with the optimizer fused into it when its table covers every parameter
             covered = sum(d[5] for _, _, ds in self.red_groups for d in ds)
             covered += sum(n for _, n in self.dense_fused_opt)
-            self.optim_fused = (one and not self.early_optim and covered == ex.store.numel
-                                and env_flag("INTML_FUSE_OPTIM", True))
+            self.optim_fused = one and covered == ex.store.numel and tune("fuse_optim", True)
             if not self.optim_fused:
                 # the step ends with a full optimizer launch after all: the dense layers keep
                 # writing their gradient in place, but leave the update to it
@@ -1351,29 +1337,32 @@ class BatchPlan:
             self.bucket_tables.append((lo, hi, tab))
             inserts.append((max(self.red_ready[i] for i in bg), k))
         extra = []
-        fused = self.comm_in_graph and getattr(reducer, "xgmi", None) is not None
-        if fused:
-            # xGMI all-reduce + optimizer in one kernel on the main stream (linear graph)
-            self.comm_fork, self.optim_on_comm = False, True
-            extra.append(("xgmi_allreduce_optim_b%d",
-                          lambda k: (lambda s: reducer.launch_fused(
-                              ex.store.grad, ex._optim_args(False, defer_pack=True), s)), "main"))
-        elif self.comm_in_graph:
-            fork = os.environ.get("INTML_COMM_FORK")
-            self.comm_fork = (fork not in ("0", "false", "False")) if fork else len(bucket_groups) > 1
+        xk = getattr(reducer, "xgmi_bucket", None) if self.comm_in_graph else None
+        if self.comm_in_graph:
+            rccl_buckets = [k for k in range(len(bucket_groups)) if k != xk]
+            # fork the comm stream only when an RCCL bucket has later backward work to overlap
+            fork = tune("comm_fork", "")
+            self.comm_fork = ((fork not in ("0", "false", "False")) if fork
+                              else any(k < len(bucket_groups) - 1 for k in rccl_buckets))
             if self.comm_fork:
                 self.comm_stream = torch.cuda.Stream(device=ex.device)
-            extra.append(("allreduce_b%d", lambda k: (lambda s: reducer.launch(k, ex.store.grad, s)), "comm"))
+            if xk is not None:
+                self.optim_on_comm = True
+            extra.append(("allreduce_b%d", lambda k: None if k == xk else
+                          (lambda s: reducer.launch(k, ex.store.grad, s)), "comm"))
             if self.optim_on_comm:
-                extra.append(("optim_b%d", lambda k: (lambda s: self._launch_optim_comm(k, s)), "comm"))
+                extra.append(("optim_b%d", lambda k: None if k == xk else
+                              (lambda s: self._launch_optim_comm(k, s)), "comm"))
+            # the xGMI bucket: all-reduce + Keras update in one kernel on the main stream
+            extra.append(("xgmi_allreduce_optim_b%d", lambda k: None if k != xk else
+                          (lambda s: reducer.launch_fused(ex.store.grad, ex._optim_args(False, defer_pack=True), s)),
+                          "main"))
         self.launches, self.bucket_ready = splice_bucket_launches(
             self.launches, inserts,
             [("reduce_b%d", lambda k: (lambda s: self._launch_bucket_reduce(k, s)), "side")] + extra)
         spans = [(lo, hi) for lo, hi, _ in self.bucket_tables]
         spans += [span for _, span in (self.early_red or {}).values()]
         check_bucket_cover(spans, ex.store.numel)
-        if self.early_optim:
-            self._insert_optim()
 
     def _early_groups(self):
         """Single-GPU fused-optimizer step: slab groups whose gradients are final before a dual
@@ -1384,15 +1373,13 @@ class BatchPlan:
         (pack readers), each launch's as one contiguous parameter span.  Sets
         self.early_red = {launch name: (RedTable, (lo, hi))}; returns the groups assigned."""
         self.early_red = {}
-        if not env_flag("INTML_EARLY_REDUCE", True):
+        if not tune("early_reduce", True):
             return []
         names = [it[0] for it in self.launches]
-        duals = [i for i, nm in enumerate(names) if nm.startswith("wgrad_dgrad_conv")]
-        # every dual launch carrying the previous layer's bucket (conv2's in dual conv1, ...) is
-        # opt-in: measured 3% slower on RPV (conv2's many-split slabs stretch dual conv1's tail
-        # by ~3 us, more than the end-of-step reduction sheds)
-        if not env_flag("INTML_EARLY_REDUCE_ALL", False):
-            duals = duals[:1]
+        # only the FIRST dual launch carries a bucket: every dual launch carrying the previous
+        # layer's bucket (conv2's in dual conv1, ...) measured 3% slower on RPV (conv2's
+        # many-split slabs stretch dual conv1's tail by ~3 us, more than the reduction sheds)
+        duals = [i for i, nm in enumerate(names) if nm.startswith("wgrad_dgrad_conv")][:1]
         taken = []
         for t in duals:
             late_readers = [(rlo, rhi) for nm, rlo, rhi in self.pack_readers if nm not in names[:t]]
@@ -1425,52 +1412,14 @@ class BatchPlan:
             self._no_packs = ex.K.PackTable()
         ex.K.optim(a, self._no_packs, stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
 
-    def _insert_optim(self):
-        """One ("optim_b<k>", ..., "opt") launch per bucket at the first point where the
-        bucket's gradients are final (its slab reduction) and every backward launch that
-        reads one of its layers' packs (dense dX, conv dgrad) has been issued."""
-        K = self.ex.K
-        index = {item[0]: i for i, item in enumerate(self.launches)}
-        forks = []
-        self.opt_tables = []
-        for k, (lo, hi, _) in enumerate(self.bucket_tables):
-            at = self.bucket_ready[k]
-            for name, rlo, rhi in self.pack_readers:
-                if rlo < hi and rhi > lo:
-                    at = max(at, index[name] + 1)
-            forks.append((at, k))
-            tab = K.PackTable()
-            for d in self.ex.pack_descs:
-                if lo <= d[0] < hi:
-                    tab.add(*d)
-            self.opt_tables.append(tab)
-        launches, pos = [], 0
-        self.opt_at = [0] * len(forks)
-        for at, k in sorted(forks):
-            launches.extend(self.launches[pos:at])
-            pos = at
-            self.opt_at[k] = len(launches)
-            launches.append(("optim_b%d" % k, lambda s, k=k: self._launch_optim_bucket(k, s), "opt"))
-        launches.extend(self.launches[pos:])
-        self.launches = launches
-
-    def _launch_optim_bucket(self, k, s):
-        ex = self.ex
-        lo, hi, _ = self.bucket_tables[k]
-        a = ex._optim_args(False)           # built at launch/capture time: current grad_scale
-        a.lo, a.n = lo, hi - lo
-        ex.K.optim(a, self.opt_tables[k], s)
-
     # ---------------------------------------------------------------- execution
     def _run_seq(self, lo: int = 0, hi: Optional[int] = None):
         """Launch [lo, hi) on the streams ``stream_program`` assigns (concurrent chains that
         join main at the end)."""
         items = self.launches[lo:hi]
         tags = [it[2] if len(it) > 2 else "main" for it in items]
-        streams = {"main": torch.cuda.current_stream(), "side": self.side, "opt": self.opt_stream,
-                   "comm": self.comm_stream}
-        for op in stream_program(tags, side=self.side is not None, opt=self.opt_stream is not None,
-                                 comm=self.comm_stream is not None):
+        streams = {"main": torch.cuda.current_stream(), "comm": self.comm_stream}
+        for op in stream_program(tags, comm=self.comm_stream is not None):
             if op[0] == "wait":
                 streams[op[1]].wait_stream(streams[op[2]])
                 continue
@@ -1494,23 +1443,16 @@ class BatchPlan:
 
     def _body(self, with_optim: bool):
         self._run_seq()
-        if (self.training and with_optim and not self.early_optim and not self.optim_fused
-                and not self.optim_on_comm):
+        if self.training and with_optim and not self.optim_fused and not self.optim_on_comm:
             self._launch_optim()
 
     def _dp_segments(self):
         """[(launch_lo, launch_hi, bucket)]: segment k ends with the slab reduction that
-        completes bucket k (with the early optimizer: at bucket k's optimizer launch, which is
-        left out of the segments); a trailing (lo, hi, None) segment holds any later launches."""
+        completes bucket k; a trailing (lo, hi, None) segment holds any later launches."""
         segs, lo = [], 0
-        if self.early_optim:
-            for at, k in sorted((at, k) for k, at in enumerate(self.opt_at)):
-                segs.append((lo, at, k))
-                lo = at + 1
-        else:
-            for k, ready in enumerate(self.bucket_ready):
-                segs.append((lo, ready, k))
-                lo = ready
+        for k, ready in enumerate(self.bucket_ready):
+            segs.append((lo, ready, k))
+            lo = ready
         if lo < len(self.launches):
             segs.append((lo, len(self.launches), None))
         return segs
@@ -1557,9 +1499,6 @@ class BatchPlan:
         # dense bucket over xGMI while the conv backward runs; the fused optimizer (with the
         # 1/size average folded in) runs after the last wait.
         segs = self._dp_segments()
-        if self.early_optim:
-            self._run_dp_early(segs)
-            return
         if ex.use_graphs and self.dp_graphs is None:
             self.dp_graphs = [self._capture(lambda a=lo, b=hi, k=k: self._run_segment(a, b, k))
                               for lo, hi, k in segs]
@@ -1576,34 +1515,6 @@ class BatchPlan:
             self.dp_graphs[-1].replay()
         else:
             self._launch_optim()
-
-    def _run_dp_early(self, segs):
-        """DP with per-bucket optimizers: after segment k, bucket k's all-reduce is issued
-        (RCCL orders it after the segment) and the optimizer stream waits for exactly that
-        all-reduce, then updates + re-packs the bucket while the main stream replays the
-        remaining backward."""
-        ex = self.ex
-        main = torch.cuda.current_stream()
-        if ex.use_graphs and self.dp_graphs is None:
-            self.dp_graphs = [self._capture(lambda a=lo, b=hi, k=k: self._run_segment(a, b, k))
-                              for lo, hi, k in segs]
-            self.opt_graphs = [self._capture(lambda k=k: self._launch_optim_bucket(
-                k, torch.cuda.current_stream().cuda_stream)) for k in range(len(self.opt_at))]
-        for j, (lo, hi, k) in enumerate(segs):
-            if ex.use_graphs:
-                self.dp_graphs[j].replay()
-            else:
-                self._run_segment(lo, hi, k)
-            if k is None:
-                continue
-            ex.reducer.start(k, ex.store.grad)
-            with torch.cuda.stream(self.opt_stream):
-                ex.reducer.wait(k)
-                if ex.use_graphs:
-                    self.opt_graphs[k].replay()
-                else:
-                    self._launch_optim_bucket(k, self.opt_stream.cuda_stream)
-        main.wait_stream(self.opt_stream)
 
     def _capture(self, fn):
         g = torch.cuda.CUDAGraph()

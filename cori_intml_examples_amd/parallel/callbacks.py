@@ -119,6 +119,10 @@ class LearningRateWarmupCallback(Callback):
     def __init__(self, warmup_epochs=5, momentum_correction=True, steps_per_epoch=None, verbose=0):
         super().__init__()
         self.warmup_epochs = warmup_epochs
+        # Horovod scales the momentum by new_lr / old_lr while the LR ramps (momentum
+        # correction); that matters only for a momentum optimizer, and the device-side ramp
+        # has no per-step hook for it -- refuse loudly instead of silently dropping it
+        self.momentum_correction = momentum_correction
         self.steps_per_epoch = steps_per_epoch
         self.verbose = verbose
         self.initial_lr = None
@@ -139,8 +143,15 @@ class LearningRateWarmupCallback(Callback):
         self._n = self._spe()
         ex = self.model._executor
         base = getattr(self.model.optimizer, "_base_optimizer", self.model.optimizer)
-        # steps of this fit() run count from its first batch
-        ex.set_lr_warmup(int(base.iterations), int(round(self.warmup_epochs * self._n)), self._n, dist.size(),
+        if self.momentum_correction and float(getattr(base, "momentum", 0.0) or 0.0) > 0.0:
+            raise NotImplementedError("LearningRateWarmupCallback(momentum_correction=True) with a momentum "
+                                      "optimizer: pass momentum_correction=False")
+        # the ramp is anchored at epoch 0 (as Horovod's, which uses the absolute epoch): a
+        # fit() resumed at initial_epoch > 0 continues the ramp where it stands, and one
+        # resumed past the warmup window does no warmup at all
+        e0 = int(self.params.get("initial_epoch", 0) or 0)
+        t0 = int(base.iterations) - e0 * self._n
+        ex.set_lr_warmup(t0, int(round(self.warmup_epochs * self._n)), self._n, dist.size(),
                          float(self.warmup_epochs), self.initial_lr)
 
     def on_epoch_end(self, epoch, logs=None):

@@ -356,6 +356,21 @@ def adaptive_bucket_bytes(groups: Sequence[Tuple[int, int]]) -> int:
     return max(16 << 20, total // 4)
 
 
+def data_plane() -> str:
+    """The gradient data plane of the native (captured) reducer, from ``INTML_XGMI``:
+    "rccl" (default, also "auto" / "0"): RCCL all-reduces;  "xgmi" ("1"): the whole gradient
+    as one fused xGMI all-reduce + optimizer kernel;  "hybrid": RCCL for the early (dense)
+    buckets, overlapped with the conv backward, and the fused xGMI kernel for the last (conv)
+    bucket.  Nothing but a measurement picks xGMI: ``bench.py``'s probe times every plane on
+    the job itself and pins the fastest (``probe_data_planes``)."""
+    mode = os.environ.get("INTML_XGMI", "auto").lower()
+    if mode in ("1", "on", "true", "xgmi"):
+        return "xgmi"
+    if mode == "hybrid":
+        return "hybrid"
+    return "rccl"
+
+
 class NativeGradReducer:
     """Bucketed gradient all-reduce on the native RCCL engine, CAPTURABLE: the executor
     inserts ``launch(k, ..)`` into the step's launch sequence on a comm stream forked after
@@ -376,6 +391,8 @@ class NativeGradReducer:
         self._stage = {}
         self._configured = False
         self.xgmi = None               # parallel.xgmi.XgmiAllreduce when the fused path is on
+        self.xgmi_bucket = None        # index of the bucket it reduces
+        self.plane = "rccl"
         self._xgmi_err_host = None
 
     @property
@@ -383,7 +400,13 @@ class NativeGradReducer:
         return True
 
     def configure(self, groups: Sequence[Tuple[int, int]]) -> List[List[int]]:
-        bg, spans = merge_buckets(groups, self.bucket_bytes or adaptive_bucket_bytes(groups))
+        self.plane = data_plane()
+        bb = self.bucket_bytes
+        if self.plane == "xgmi":
+            bb = 1 << 62                    # the whole gradient is ONE fused xGMI bucket
+        elif self.plane == "hybrid" and not bb:
+            bb = 1 << 20                    # dense bucket(s) over RCCL, the conv tail over xGMI
+        bg, spans = merge_buckets(groups, bb or adaptive_bucket_bytes(groups))
         if self._configured and spans == self.buckets and bg == self.bucket_groups:
             return self.bucket_groups       # same layout (another batch size): keep the staging
         self.bucket_groups, self.buckets = bg, spans   # buffers earlier graphs reference
@@ -392,29 +415,38 @@ class NativeGradReducer:
         self._setup_xgmi()
         if self.compression == "bf16":
             for k, (lo, hi) in enumerate(self.buckets):
-                self._stage[k] = torch.empty(hi - lo, dtype=torch.bfloat16, device=self.comm.device)
+                if k != self.xgmi_bucket:
+                    self._stage[k] = torch.empty(hi - lo, dtype=torch.bfloat16, device=self.comm.device)
         return self.bucket_groups
 
     def _setup_xgmi(self):
-        """ONE fused bucket, fp32 wire, N > 1 (``INTML_XGMI=1`` also at N = 1; ``=0`` off):
-        the fused xGMI all-reduce + optimizer kernel replaces RCCL + the optimizer launch,
-        if every rank's setup and self-test pass (collective; same decision on all ranks)."""
-        mode = os.environ.get("INTML_XGMI", "auto").lower()
-        want = (mode in ("1", "on", "true") or (mode == "auto" and self.size > 1))
-        ok = want and len(self.buckets) == 1 and self.buckets[0][0] == 0 and self.compression is None
-        n = self.buckets[0][1] if ok else 0
-        if self.xgmi is not None and (not ok or self.xgmi.n != n):
+        """The bucket that goes over the fused xGMI all-reduce + optimizer kernel instead of
+        RCCL + an optimizer launch: plane "xgmi" -> the single whole-gradient bucket; plane
+        "hybrid" -> the LAST bucket (the small conv tail of the backward, latency-bound on
+        RCCL) while the earlier ones stay on RCCL, forked onto the comm stream so they overlap
+        the conv backward.  fp32 wire only; collective setup + self-test, same decision on
+        every rank (else every bucket stays on RCCL)."""
+        want = self.plane in ("xgmi", "hybrid") and self.compression is None
+        k = len(self.buckets) - 1 if want else None
+        n = (self.buckets[k][1] - self.buckets[k][0]) if want else 0
+        if self.xgmi is not None and (not want or self.xgmi.n != n):
             self.xgmi.close()
             self.xgmi = None
-        if ok and self.xgmi is None:
+        self.xgmi_bucket = None
+        if want and self.xgmi is None:
             from . import xgmi as X
             self.xgmi = X.create(self.comm.rank, self.size, n, self.comm.device, allgather)
             if self.xgmi is not None:
                 self._xgmi_err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        if self.xgmi is not None:
+            self.xgmi_bucket = k
 
     def launch_fused(self, grad: torch.Tensor, opt_args, stream: int) -> None:
-        """The fused all-reduce + optimizer of the single bucket (capturable)."""
-        self.xgmi.launch(grad.data_ptr(), stream, opt=opt_args)
+        """The fused all-reduce + optimizer of the xGMI bucket (capturable); ``opt_args``
+        cover the whole flat buffer and are offset to the bucket here."""
+        from . import xgmi as X
+        lo, _ = self.buckets[self.xgmi_bucket]
+        self.xgmi.launch(grad.data_ptr() + 4 * lo, stream, opt=X.offset_optim(opt_args, lo))
 
     def launch(self, bucket: int, grad: torch.Tensor, stream: torch.cuda.Stream) -> None:
         """Enqueue bucket ``bucket``'s all-reduce on ``stream`` (capturable)."""
@@ -446,7 +478,8 @@ class NativeGradReducer:
         self.comm.mark()
         if self.xgmi is not None:
             if int(self._xgmi_err_host[0]):
-                raise RuntimeError("xgmi all-reduce: a wait timed out (peer rank dead or hung)")
+                from . import xgmi as X
+                raise RuntimeError(X.describe_error(int(self._xgmi_err_host[0])))
             self._xgmi_err_host.copy_(self.xgmi.err, non_blocking=True)
 
     def reduce_all(self, grad: torch.Tensor, average: bool = True) -> None:

@@ -15,7 +15,13 @@ Reference call site it replaces: Horovod's fused gradient all-reduce behind
 Safety: setup (uncached allocation, IPC handle exchange over the gloo control plane,
 mapping) and a numeric self-test against closed-form sums run at construction; every rank
 votes and the path is used only if ALL ranks pass (else the caller keeps RCCL).  Every
-in-kernel wait is bounded and reports through an error word (``check()``), never a hang.
+in-kernel wait is bounded in time (``timeout_s``: min(INTML_DP_TIMEOUT, 120) s by default)
+and reports through an error word (``check()``), never a hang; a rank that gives up raises
+a sticky abort word on every rank, so no later launch anywhere can pair this step's flags
+with another step's data (every later launch exits at once and the host raises).
+
+A bucket is any flat range [lo, hi) of the gradient: ``launch(grad_ptr, ..)`` takes the
+bucket's first element and the optimizer arguments are offset to it (``offset_optim``).
 """
 from __future__ import annotations
 
@@ -25,8 +31,24 @@ from typing import Callable, List, Optional
 import torch
 
 from ..ops.hip import kernels
+from ..utils.env import tune
 
 _FLAG_WORDS = 256 * 8          # XGMI_MAX_WG x XGMI_MAX_RANKS
+_TICKS_PER_S = 100_000_000     # wall_clock64 (s_memrealtime) runs at 100 MHz on gfx950
+
+
+def default_timeout_s() -> float:
+    return min(float(os.environ.get("INTML_DP_TIMEOUT", 600)), 120.0)
+
+
+def offset_optim(opt, lo: int):
+    """OptimArgs whose parameter / slot pointers start at flat element ``lo`` (a bucket)."""
+    if lo:
+        for f in ("p", "s0", "s1"):
+            v = getattr(opt, f)
+            if v:
+                setattr(opt, f, v + 4 * lo)
+    return opt
 
 
 def _align(x: int, a: int) -> int:
@@ -49,16 +71,17 @@ class XgmiAllreduce:
     every rank must construct it, in the same order."""
 
     def __init__(self, rank: int, size: int, n: int, device: torch.device,
-                 allgather: Callable[[object], List[object]], spin_limit: Optional[int] = None):
+                 allgather: Callable[[object], List[object]], timeout_s: Optional[float] = None):
         K = kernels()
         self.K, self.rank, self.size, self.n, self.device = K, rank, size, n, device
         if size > K.XGMI_MAX_RANKS:
             raise ValueError("xgmi all-reduce supports at most %d ranks" % K.XGMI_MAX_RANKS)
         self.chunk, self.sub, self.grid = geometry(n, size, K.XGMI_MAX_WG)
         words = self.chunk * size
-        # layout (bytes): flag1 | flag2 | inbox [P][chunk] fp32 | outbox [P*chunk] fp32
+        # layout (bytes): flag1 | flag2 | abort word | inbox [P][chunk] fp32 | outbox [P*chunk] fp32
         self.off_f1, self.off_f2 = 0, 4 * _FLAG_WORDS
-        self.off_in = _align(self.off_f2 + 4 * _FLAG_WORDS, 256)
+        self.off_ab = self.off_f2 + 4 * _FLAG_WORDS
+        self.off_in = _align(self.off_ab + 256, 256)
         self.off_out = _align(self.off_in + 4 * words, 256)
         self.nbytes = _align(self.off_out + 4 * words, 4096)
         self.buf = 0
@@ -66,7 +89,7 @@ class XgmiAllreduce:
         err = None
         torch.cuda.set_device(device)
         try:
-            self.buf = K.xgmi_alloc_uncached(self.nbytes, os.environ.get("INTML_XGMI_MEM", "uncached") == "finegrained")
+            self.buf = K.xgmi_alloc_uncached(self.nbytes, tune("xgmi_mem", "uncached") == "finegrained")
             handle = K.xgmi_ipc_handle(self.buf)
         except Exception as e:        # noqa: BLE001 -- reported through the vote below
             err, handle = "setup: %s" % e, b""
@@ -89,12 +112,13 @@ class XgmiAllreduce:
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
         a = K.XgmiArgs()
         a.rank, a.size, a.n, a.chunk, a.sub = rank, size, n, self.chunk, self.sub
-        a.spin_limit = int(spin_limit or os.environ.get("INTML_XGMI_SPIN_LIMIT", 1 << 22))
+        self.timeout_s = float(timeout_s or default_timeout_s())
+        a.timeout_ticks = int(self.timeout_s * _TICKS_PER_S)
         a.ctr, a.err = self.ctr.data_ptr(), self.err.data_ptr()
-        a.fence = int(os.environ.get("INTML_XGMI_FENCE", "1"))
+        a.fence = int(tune("xgmi_fence", 1))
         if err is None:
             for j, b in enumerate(bases):
-                a.set_peer(j, b + self.off_in, b + self.off_out, b + self.off_f1, b + self.off_f2)
+                a.set_peer(j, b + self.off_in, b + self.off_out, b + self.off_f1, b + self.off_f2, b + self.off_ab)
         self.args = a
         self.setup_error = err
 
@@ -114,7 +138,7 @@ class XgmiAllreduce:
         """Raise if a wait in an earlier launch timed out (a peer died or hung)."""
         e = int(self.err.item())
         if e:
-            raise RuntimeError("xgmi all-reduce: phase-%d wait timed out (peer rank dead or hung)" % e)
+            raise RuntimeError(describe_error(e))
 
     def selftest(self) -> Optional[str]:
         """Two launches on closed-form data (exact in fp32); None if correct on this rank."""
@@ -149,6 +173,12 @@ class XgmiAllreduce:
             self.buf = 0
 
 
+def describe_error(e: int) -> str:
+    if e == 3:
+        return "xgmi all-reduce: aborted (a peer rank timed out waiting; peer dead or hung)"
+    return "xgmi all-reduce: phase-%d wait timed out (peer rank dead or hung)" % e
+
+
 def create(rank: int, size: int, n: int, device: torch.device, allgather) -> Optional[XgmiAllreduce]:
     """Build + self-test collectively; returns the object only if EVERY rank passed both
     the setup and the self-test (same decision on every rank: the votes are gathered)."""
@@ -160,13 +190,13 @@ def create(rank: int, size: int, n: int, device: torch.device, allgather) -> Opt
         why = "error: %s" % e
     bad = [(i, v) for i, v in enumerate(allgather(why)) if v]
     if not bad:
-        limit = x.args.spin_limit
-        x.args.spin_limit = min(limit, 1 << 18)    # a broken path fails the test fast
+        limit = x.args.timeout_ticks
+        x.args.timeout_ticks = min(limit, 5 * _TICKS_PER_S)    # a broken path fails the test fast
         try:
             why = x.selftest()
         except Exception as e:        # noqa: BLE001
             why = "selftest error: %s" % e
-        x.args.spin_limit = limit
+        x.args.timeout_ticks = limit
         bad = [(i, v) for i, v in enumerate(allgather(why)) if v]
     if bad:
         if x is not None:

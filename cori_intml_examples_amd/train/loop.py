@@ -84,7 +84,7 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
     cb.set_model(model)
     cb.set_params({"batch_size": batch_size, "epochs": epochs, "steps": None,
                    "samples": n_local, "verbose": verbose, "do_validation": do_val,
-                   "metrics": metrics})
+                   "metrics": metrics, "initial_epoch": initial_epoch})
     for c in cb:
         c.validation_data = (vx, vy) if do_val else None
     model.stop_training = False

@@ -21,6 +21,35 @@ def env_flag(name: str, default: bool) -> bool:
     return v.strip().lower() not in ("0", "false", "no", "off", "")
 
 
+_TUNE = None
+
+
+def tune(key: str, default):
+    """Kernel-path / geometry tuning value ``key`` (executor switches and launch geometry):
+    ``default`` unless ``INTML_TUNE="key=value,key=value"`` overrides it (measurement sweeps
+    and A/B tests).  One knob for all of them instead of one environment variable each; the
+    value is parsed as the default's type (bool: 0/1/true/false)."""
+    global _TUNE
+    if _TUNE is None or _TUNE[0] != os.environ.get("INTML_TUNE", ""):
+        raw = os.environ.get("INTML_TUNE", "")
+        d = {}
+        for item in raw.split(","):
+            if "=" in item:
+                k, v = item.split("=", 1)
+                d[k.strip()] = v.strip()
+        _TUNE = (raw, d)
+    v = _TUNE[1].get(key)
+    if v is None:
+        return default
+    if isinstance(default, bool):
+        return v.lower() not in ("0", "false", "no", "off", "")
+    if isinstance(default, int):
+        return int(v)
+    if isinstance(default, float):
+        return float(v)
+    return v
+
+
 def default_device() -> torch.device:
     """``INTML_DEVICE`` overrides; otherwise the GPU of this process (local rank) if
     one is visible, else the CPU reference backend."""

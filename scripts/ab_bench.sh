@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of one env knob on the 1-GPU bench: interleaved runs, one JSON value per line.
-#   KNOB=INTML_EARLY_REDUCE A=0 B=1 bash scripts/ab_bench.sh
+#   KNOB=INTML_TUNE A=early_reduce=0 B=early_reduce=1 bash scripts/ab_bench.sh
 cd $GRAFT_REPO_ROOT
 for i in 1 2 3; do
   for v in $A $B; do

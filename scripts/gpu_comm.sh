@@ -10,5 +10,5 @@ timeout -k 10 200 python bench.py --steps 200 --warmup 30 > gpurun_out/comm_benc
 tail -n 1 gpurun_out/comm_bench_plain.log | cut -c1-160
 INTML_DP_FORCE=1 timeout -k 10 200 python bench.py --steps 200 --warmup 30 > gpurun_out/comm_bench_dp1.log 2>&1 || { tail -n 30 gpurun_out/comm_bench_dp1.log; exit 1; }
 tail -n 1 gpurun_out/comm_bench_dp1.log | cut -c1-160
-INTML_DP_FORCE=1 INTML_COMM_CAPTURE=0 timeout -k 10 200 python bench.py --steps 200 --warmup 30 > gpurun_out/comm_bench_dp1_seg.log 2>&1 || { tail -n 30 gpurun_out/comm_bench_dp1_seg.log; exit 1; }
+INTML_DP_FORCE=1 INTML_TUNE=comm_capture=0 timeout -k 10 200 python bench.py --steps 200 --warmup 30 > gpurun_out/comm_bench_dp1_seg.log 2>&1 || { tail -n 30 gpurun_out/comm_bench_dp1_seg.log; exit 1; }
 tail -n 1 gpurun_out/comm_bench_dp1_seg.log | cut -c1-160

@@ -65,7 +65,7 @@ def main(out):
 
     wb = train(base)
     results = {}
-    for name, env in (("captured", {"INTML_COMM_CAPTURE": "1"}), ("segmented", {"INTML_COMM_CAPTURE": "0"})):
+    for name, env in (("captured", {"INTML_TUNE": "comm_capture=1"}), ("segmented", {"INTML_TUNE": "comm_capture=0"})):
         os.environ.update(env)
         m = zoo.rpv_cnn((64, 64, 3), use_horovod=True, **kw)
         m.set_weights(w0)
@@ -79,7 +79,7 @@ def main(out):
         results[name]["p999_abs_diff"] = float(np.quantile(np.abs(w - wb), 0.999))
         results[name]["w"] = w
     results["captured_vs_segmented"] = float(np.abs(results["captured"].pop("w") - results["segmented"].pop("w")).max())
-    os.environ["INTML_COMM_CAPTURE"] = "1"
+    os.environ["INTML_TUNE"] = "comm_capture=1"
     # the fused xGMI all-reduce + optimizer kernel (forced on at size 1)
     os.environ["INTML_XGMI"] = "1"
     m = zoo.rpv_cnn((64, 64, 3), use_horovod=True, **kw)
@@ -90,6 +90,20 @@ def main(out):
                        "launches": [it[0] for it in plan.launches if "xgmi" in it[0] or "allreduce" in it[0]],
                        "max_abs_diff": float(np.abs(w - wb).max()),
                        "p999_abs_diff": float(np.quantile(np.abs(w - wb), 0.999))}
+    # hybrid plane: bucket 0 (head + dense) over RCCL on the comm stream with its optimizer,
+    # bucket 1 (convs) through the fused xGMI kernel on the main stream
+    os.environ["INTML_XGMI"] = "hybrid"
+    m = zoo.rpv_cnn((64, 64, 3), use_horovod=True, **kw)
+    m.set_weights(w0)
+    w = train(m)
+    plan = next(iter(m._executor._plans.values()))
+    red = m._executor.reducer
+    results["hybrid"] = {"xgmi_bucket": red.xgmi_bucket, "buckets": [list(b) for b in red.buckets],
+                         "launches": [(it[0], it[2] if len(it) > 2 else "main") for it in plan.launches
+                                      if "xgmi" in it[0] or "allreduce" in it[0] or it[0].startswith("optim")],
+                         "comm_fork": bool(plan.comm_fork),
+                         "max_abs_diff": float(np.abs(w - wb).max()),
+                         "p999_abs_diff": float(np.quantile(np.abs(w - wb), 0.999))}
     os.environ["INTML_XGMI"] = "0"
     opt = hvd.DistributedOptimizer("Adam", compression=hvd.Compression.fp16)
     m = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw)

@@ -20,16 +20,17 @@ def probe_env(monkeypatch):
         # writes these variables
         monkeypatch.setenv(k, "")
         monkeypatch.delenv(k)
-    cost = {"xgmi": 10.0, "rccl": 11.0, "rccl_forked": 12.0}
+    cost = {"xgmi": 10.0, "rccl": 11.0, "rccl_forked": 12.0, "hybrid": 13.0}
     sums = {"bad": set()}
 
     def plane():
-        if os.environ.get("INTML_XGMI") == "1":
-            return "xgmi"
+        if os.environ.get("INTML_XGMI") in ("xgmi", "hybrid"):
+            return os.environ["INTML_XGMI"]
         return "rccl_forked" if os.environ.get("INTML_BUCKET_BYTES") else "rccl"
 
     def build(args, size, dp, dev):
-        x = types.SimpleNamespace(err=types.SimpleNamespace(item=lambda: 0)) if plane() == "xgmi" else None
+        x = (types.SimpleNamespace(err=types.SimpleNamespace(item=lambda: 0)) if plane() in ("xgmi", "hybrid")
+             else None)
         m = types.SimpleNamespace(_executor=types.SimpleNamespace(reducer=types.SimpleNamespace(xgmi=x)),
                                   plane=plane())
         return m, (64, 64, 3), 1, "cfg", "metric", None
@@ -55,8 +56,27 @@ def test_probe_picks_fastest_and_sets_env(probe_env):
     cost, _, args = probe_env
     cost.update(xgmi=12.0, rccl=11.0, rccl_forked=10.0)
     r = bench.probe_data_planes(args, 2, None, None, 128, 8)
-    assert r["chosen"] == "rccl_forked"
-    assert os.environ["INTML_XGMI"] == "0" and os.environ["INTML_BUCKET_BYTES"] == str(1 << 20)
+    assert r["chosen"] == "rccl_forked" and set(r) >= {"xgmi", "rccl", "rccl_forked", "hybrid"}
+    assert os.environ["INTML_XGMI"] == "rccl" and os.environ["INTML_BUCKET_BYTES"] == str(1 << 20)
+
+
+def test_probe_can_pick_hybrid(probe_env):
+    cost, _, args = probe_env
+    cost.update(xgmi=12.0, rccl=11.0, rccl_forked=10.5, hybrid=9.0)
+    r = bench.probe_data_planes(args, 2, None, None, 128, 8)
+    assert r["chosen"] == "hybrid"
+    assert os.environ["INTML_XGMI"] == "hybrid" and os.environ["INTML_BUCKET_BYTES"] == str(1 << 20)
+
+
+def test_default_plane_is_rccl(monkeypatch):
+    """Without a probe (fit(), train_rpv) the data plane is RCCL: nothing but a measurement
+    admits xGMI."""
+    from cori_intml_examples_amd.parallel.dist import data_plane
+    monkeypatch.delenv("INTML_XGMI", raising=False)
+    assert data_plane() == "rccl"
+    for v, want in (("auto", "rccl"), ("0", "rccl"), ("1", "xgmi"), ("xgmi", "xgmi"), ("hybrid", "hybrid")):
+        monkeypatch.setenv("INTML_XGMI", v)
+        assert data_plane() == want
 
 
 def test_probe_rejects_divergent_plane(probe_env):
@@ -64,7 +84,7 @@ def test_probe_rejects_divergent_plane(probe_env):
     sums["bad"].add("xgmi")                    # fastest, but its ranks ended with different weights
     r = bench.probe_data_planes(args, 2, None, None, 128, 8)
     assert r["xgmi"] is None and "xgmi_rejected" in r and r["chosen"] == "rccl"
-    assert os.environ["INTML_XGMI"] == "0" and "INTML_BUCKET_BYTES" not in os.environ
+    assert os.environ["INTML_XGMI"] == "rccl" and "INTML_BUCKET_BYTES" not in os.environ
 
 
 def test_probe_respects_pinned_plane(probe_env, monkeypatch):
@@ -72,3 +92,22 @@ def test_probe_respects_pinned_plane(probe_env, monkeypatch):
     monkeypatch.setenv("INTML_XGMI", "1")
     assert bench.probe_data_planes(args, 2, None, None, 128, 8) is None
     assert bench.probe_data_planes(args, 1, None, None, 128, 8) is None
+
+
+def test_inline_hpo_record_on_cpu(monkeypatch):
+    """bench.py's inline HPO (the 'hpo' record of the JSON line): the farm starts before the
+    training bench, runs the DistHPO_mnist trials after it and reports trials/hour.  CPU
+    engines and a shrunken search here; the GPU run uses 64 trials x 16 epochs x 60k."""
+    from cori_intml_examples_amd import farm
+    monkeypatch.setattr(farm, "detect_gpus", lambda: 0)
+    monkeypatch.setattr(bench.InlineHpo, "TRIALS", 3)
+    monkeypatch.setattr(bench.InlineHpo, "EPOCHS", 1)
+    monkeypatch.setattr(bench.InlineHpo, "SAMPLES", 600)
+    h = bench.InlineHpo(engines_per_gpu=2, budget_s=120.0)
+    try:
+        rec = h.run()
+    finally:
+        h.stop()
+    assert rec["trials_done"] == 3 and not rec["capped"], rec
+    assert rec["trials_per_hour"] > 0 and rec["wall_s"] >= rec["startup_s"] > 0
+    assert rec["epochs"] == 1 and rec["samples"] == 600 and rec["engines_per_gpu"] == 2

@@ -74,6 +74,11 @@ def test_native_comm_engine_gpu(tmp_path):
     xg = rep["train"]["xgmi"]
     assert xg["active"] and xg["launches"] == ["xgmi_allreduce_optim_b0"], xg
     assert xg["p999_abs_diff"] < 1e-5 and xg["max_abs_diff"] < 2e-3, xg
+    hy = rep["train"]["hybrid"]
+    assert hy["xgmi_bucket"] == 1 and len(hy["buckets"]) == 2 and hy["comm_fork"], hy
+    assert [list(x) for x in hy["launches"]] == [["allreduce_b0", "comm"], ["optim_b0", "comm"],
+                                                 ["xgmi_allreduce_optim_b1", "main"]], hy
+    assert hy["p999_abs_diff"] < 1e-5 and hy["max_abs_diff"] < 2e-3, hy
     assert rep["abort_raises"] and rep["healthy"], rep
 
 
@@ -104,11 +109,8 @@ def test_xgmi_geometry():
             assert 1 <= grid <= 256 and (grid - 1) * sub < chunk <= grid * sub
 
 
-@pytest.mark.gpu
-def test_xgmi_two_processes_one_gpu(tmp_path):
-    """Two ranks on one GPU through IPC-mapped peer memory: collective self-test, the fused
-    Adam update matches the closed form, and both ranks end with identical weights."""
-    env = dict(os.environ, PYTHONPATH=ROOT, INTML_XGMI_SPIN_LIMIT=str(1 << 20))
+def _run_xgmi_workers(tmp_path, P, mode, timeout=240):
+    env = dict(os.environ, PYTHONPATH=ROOT, INTML_DP_TIMEOUT="30")
     for k in ("WORLD_SIZE", "RANK", "INTML_DP_BACKEND", "INTML_COMM"):
         env.pop(k, None)
     import socket
@@ -116,14 +118,45 @@ def test_xgmi_two_processes_one_gpu(tmp_path):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(P),
            "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(ROOT, "tests", "xgmi_worker_gpu.py"), str(tmp_path)]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+           os.path.join(ROOT, "tests", "xgmi_worker_gpu.py"), str(tmp_path), mode]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    reps = [json.load(open(tmp_path / ("xgmi%d.json" % i))) for i in range(2)]
+    return [json.load(open(tmp_path / ("xgmi%d.json" % i))) for i in range(P)], r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_xgmi_processes_one_gpu(tmp_path, P):
+    """P ranks on one GPU through IPC-mapped peer memory (the P > 2 flag slots w*P+r, the
+    XGMI_MAX_RANKS unrolls and the chunk geometry with a ragged n): collective self-test,
+    the fused Adam update matches the closed form, repeated launches stay in sequence, a
+    sub-range bucket [lo, hi) reduces and updates only its range, and every rank ends with
+    bit-identical weights."""
+    reps, r = _run_xgmi_workers(tmp_path, P, "full")
     for rep in reps:
-        assert rep["created"], r.stderr[-3000:]
-        assert rep["err"] == 0 and rep["grad_sum_ok"], rep
+        assert rep["created"] and rep["range_created"], r.stderr[-3000:]
+        assert rep["err"] == 0 and rep["grad_sum_ok"] and rep["repeat_ok"], rep
         assert rep["adam_maxdiff"] < 1e-6, rep
-    assert reps[0]["p_digest"] == reps[1]["p_digest"]
+        assert rep["range_err"] == 0 and rep["range_sum_ok"] and rep["range_outside_untouched"], rep
+        assert rep["range_adam_maxdiff"] < 1e-6, rep
+    assert all(rep["p_digest"] == reps[0]["p_digest"] for rep in reps)
+    # outside the bucket each rank keeps its own (untouched) values: compare the bucket only
+    assert len({tuple(rep["geometry"]) for rep in reps}) == 1
+
+
+@pytest.mark.gpu
+def test_xgmi_late_rank_aborts_cleanly(tmp_path):
+    """One rank launches after the other's bounded wait (2 s) has expired: the waiting rank
+    reports its timeout, the late rank sees the sticky abort and exits at once, both hosts
+    raise on check(), and every later launch on both ranks exits without touching the
+    gradient -- no rank ever pairs one step's flags with another step's data."""
+    reps, r = _run_xgmi_workers(tmp_path, 2, "delay")
+    r0, r1 = reps
+    assert r0["created"] and r1["created"], r.stderr[-3000:]
+    assert r0["err1"] == 1 and r1["err1"] == 3, reps
+    assert r0["first_launch_s"] < 10 and r1["first_launch_s"] < 1.0, reps
+    for rep in reps:
+        assert rep["err2"] != 0 and rep["second_untouched"] and rep["second_launch_s"] < 1.0, rep
+        assert rep["check_raised"], rep

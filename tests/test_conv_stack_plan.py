@@ -51,41 +51,3 @@ def test_rpv_two_bands_recompute_is_bounded():
     rows = BatchPlan._stack_rows(RPV, 2)
     conv1 = [r[1] - r[0] for r in rows[0]]
     assert sum(conv1) <= 1.5 * 64                           # < 50% extra conv1 rows for 2 bands
-
-
-@pytest.mark.parametrize("convs", [RPV, MNIST, ODD], ids=["rpv", "mnist", "odd"])
-@pytest.mark.parametrize("splits", [1, 2, 3, 4])
-def test_stack_input_row_partition(convs, splits):
-    """In-place dataset reads (BatchPlan._stack_xrows): when accepted, the bands' input-row
-    shares tile [0, H) exactly and each lies in the band's staged halo rows."""
-    rows = BatchPlan._stack_rows(convs, splits)
-    if rows is None:
-        return
-    g0 = SimpleNamespace(H=convs[0].H, KH=convs[0].KH, pad_t=convs[0].pad_t, pool=convs[0].pool)
-    got = []
-
-    class _A:
-        def __init__(self):
-            self.splits = splits
-
-        def set_xrows(self, sp, lo, hi):
-            got.append((sp, lo, hi))
-
-    plan = SimpleNamespace(ex=SimpleNamespace(convs=convs), _stack_rows=BatchPlan._stack_rows)
-    ok = BatchPlan._stack_xrows(plan, _A())
-    if not ok:
-        return
-    assert [sp for sp, _, _ in got] == list(range(splits))
-    assert got[0][1] == 0 and got[-1][2] == g0.H
-    for (_, lo, hi), (_, lo2, _) in zip(got, got[1:]):
-        assert hi == lo2
-    for sp, lo, hi in got:
-        ib, ih = rows[0][sp][4], rows[0][sp][5]
-        assert ib <= lo <= hi <= ib + ih
-
-
-def test_stack_input_row_partition_accepts_benchmarked_stacks():
-    for convs in (RPV, MNIST):
-        plan = SimpleNamespace(ex=SimpleNamespace(convs=convs), _stack_rows=BatchPlan._stack_rows)
-        a = SimpleNamespace(splits=2, set_xrows=lambda *x: None)
-        assert BatchPlan._stack_xrows(plan, a)

@@ -1,6 +1,6 @@
 """dense_bwd.hip: the per-wave pipelined dense weight-gradient kernel against a plain torch
 fp32 reference (every split / tile-width variant the executor picks, odd batch tails and
-N not a multiple of 16), and the opt-in fused optimizer path (INTML_DENSE_OPT) against the
+N not a multiple of 16), and the opt-in fused optimizer path (INTML_TUNE=dense_opt=1) against the
 default end-of-step reduction."""
 import os
 
@@ -58,7 +58,7 @@ def test_dense_wgrad_matches_fp32(M, width, N, S):
 
 @gpu
 def test_dense_fused_optimizer_matches_reduction(monkeypatch):
-    """INTML_DENSE_OPT=1 (optimizer applied inside the one-split dense wgrad) ends a few Adam
+    """INTML_TUNE=dense_opt=1 (optimizer applied inside the one-split dense wgrad) ends a few Adam
     steps where the default path (update in the end-of-step reduction) does: same gradient,
     same per-element update; only fp contraction may differ (Adam turns a last-ulp
     difference of a near-zero gradient into up to a full lr step, hence the distribution
@@ -72,7 +72,7 @@ def test_dense_fused_optimizer_matches_reduction(monkeypatch):
     w0 = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw).get_weights()
     out = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("INTML_DENSE_OPT", flag)
+        monkeypatch.setenv("INTML_TUNE", "dense_opt=" + flag)
         m = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw)
         m.set_weights(w0)
         for i in range(2):

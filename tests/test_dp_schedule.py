@@ -11,7 +11,7 @@ from cori_intml_examples_amd.parallel.dist import merge_buckets
 GROUPS = [(547712, 547841), (23584, 547712), (5088, 23584), (448, 5088), (0, 448)]
 
 
-def _fake_step(side=False, comm=True, optim_on_comm=True, bucket_bytes=1 << 20):
+def _fake_step(comm=True, optim_on_comm=True, bucket_bytes=1 << 20):
     base = [("prologue", None, "main"), ("conv_stack_fwd", None, "main"), ("dense_fwd0", None, "main"),
             ("dense_epi0", None, "main"), ("head", None, "main")]
     red_ready = [len(base)]                       # head slabs final after the head launch
@@ -24,21 +24,22 @@ def _fake_step(side=False, comm=True, optim_on_comm=True, bucket_bytes=1 << 20):
     red_ready.append(len(base))
     bucket_groups, spans = merge_buckets(GROUPS, bucket_bytes)
     inserts = [(max(red_ready[i] for i in bg), k) for k, bg in enumerate(bucket_groups)]
-    per = [("reduce_b%d", lambda k: None, "side")]
+    fake = lambda k: (lambda s: None)      # noqa: E731
+    per = [("reduce_b%d", fake, "side")]
     if comm:
-        per.append(("allreduce_b%d", lambda k: None, "comm"))
+        per.append(("allreduce_b%d", fake, "comm"))
         if optim_on_comm:
-            per.append(("optim_b%d", lambda k: None, "comm"))
+            per.append(("optim_b%d", fake, "comm"))
     launches, ready = splice_bucket_launches(base, inserts, per)
     return launches, ready, spans
 
 
-def _run(launches, side=False, opt=False):
+def _run(launches):
     """Execute the stream program on fake streams: each stream is a list of launch names;
     a wait records (dst waits for src's last launch so far)."""
     tags = [l[2] for l in launches]
-    ops = stream_program(tags, side=side, opt=opt)
-    streams = {"main": [], "side": [], "opt": [], "comm": []}
+    ops = stream_program(tags)
+    streams = {"main": [], "comm": []}
     deps = []        # (stream, position in that stream, (src stream, number of src launches seen))
     for op in ops:
         if op[0] == "wait":
@@ -72,12 +73,11 @@ def _happens_before(streams, deps, a, b):
     return False
 
 
-@pytest.mark.parametrize("side", [False, True])
-def test_dp_step_schedule_orders_reduce_allreduce_optim(side):
-    launches, ready, spans = _fake_step(side=side)
+def test_dp_step_schedule_orders_reduce_allreduce_optim():
+    launches, ready, spans = _fake_step()
     names = [l[0] for l in launches]
     assert len(spans) == 2 and ready == [names.index("optim_b0") + 1, names.index("optim_b1") + 1]
-    ops, streams, deps = _run(launches, side=side)
+    ops, streams, deps = _run(launches)
     # comm stream carries exactly the all-reduces and the per-bucket updates, in bucket order
     assert streams["comm"] == ["allreduce_b0", "optim_b0", "allreduce_b1", "optim_b1"]
     for k in range(2):
@@ -129,6 +129,24 @@ def test_bucket_cover():
 def test_linear_schedule_keeps_comm_on_main():
     launches, _, _ = _fake_step()
     tags = [l[2] for l in launches]
-    ops = stream_program(tags, side=False, opt=False, comm=False)
+    ops = stream_program(tags, comm=False)
     assert all(op[0] == "run" and op[1] == "main" for op in ops)
     assert [launches[op[2]][0] for op in ops] == [l[0] for l in launches]
+
+
+def test_splice_skips_buckets_a_factory_declines():
+    """Hybrid plane: the xGMI bucket gets the fused kernel on main, the others RCCL + optimizer
+    on the comm stream (a factory returning None skips that bucket)."""
+    base = [("a", None, "main"), ("b", None, "main"), ("c", None, "main")]
+    xk = 1
+    per = [("reduce_b%d", lambda k: (lambda s: None), "side"),
+           ("allreduce_b%d", lambda k: None if k == xk else (lambda s: None), "comm"),
+           ("optim_b%d", lambda k: None if k == xk else (lambda s: None), "comm"),
+           ("xgmi_b%d", lambda k: (lambda s: None) if k == xk else None, "main")]
+    out, ready = splice_bucket_launches(base, [(1, 0), (3, 1)], per)
+    names = [o[0] for o in out]
+    assert names == ["a", "reduce_b0", "allreduce_b0", "optim_b0", "b", "c", "reduce_b1", "xgmi_b1"]
+    assert ready == [4, 8]
+    ops = stream_program([o[2] for o in out])
+    comm = [out[op[2]][0] for op in ops if op[0] == "run" and op[1] == "comm"]
+    assert comm == ["allreduce_b0", "optim_b0"] and ops[-1] == ("wait", "main", "comm")

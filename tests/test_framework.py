@@ -163,6 +163,41 @@ def test_lr_warmup_callback_matches_per_batch_schedule():
     assert optim.get_value(m.optimizer.lr) == pytest.approx(0.004)
 
 
+def test_lr_warmup_resume_continues_absolute_ramp():
+    """A fit() resumed at initial_epoch continues the warmup ramp where it stands (the ramp is
+    anchored at epoch 0, as Horovod's callback uses the absolute epoch): epochs 0-2 in one
+    run end on the weights of epoch 0, then a resumed fit(initial_epoch=1) -- not a restart
+    of the ramp from lr/size.  Momentum correction with a momentum optimizer is refused."""
+    from cori_intml_examples_amd.parallel import callbacks as hcb
+    from cori_intml_examples_amd.parallel import dist
+
+    x, y, _ = synthetic_rpv(64, size=16, seed=1)
+    orig = dist.size
+    dist.size = lambda: 4
+    try:
+        m = zoo.rpv_cnn((16, 16, 1), [4, 4, 4], [8], dropout=0.0, optimizer="SGD", lr=0.004, device="cpu")
+        w0 = m.get_weights()
+        m.fit(x, y, batch_size=16, epochs=3, verbose=0, shuffle=False, callbacks=[hcb.LearningRateWarmupCallback(2)])
+        wa = m.get_weights()
+        m2 = zoo.rpv_cnn((16, 16, 1), [4, 4, 4], [8], dropout=0.0, optimizer="SGD", lr=0.004, device="cpu")
+        m2.set_weights(w0)
+        m2.fit(x, y, batch_size=16, epochs=1, verbose=0, shuffle=False, callbacks=[hcb.LearningRateWarmupCallback(2)])
+        optim.set_value(m2.optimizer.lr, 0.004)        # what a checkpoint of the run would hold
+        m2.fit(x, y, batch_size=16, epochs=3, initial_epoch=1, verbose=0, shuffle=False,
+               callbacks=[hcb.LearningRateWarmupCallback(2)])
+        wb = m2.get_weights()
+        m3 = zoo.rpv_cnn((16, 16, 1), [4, 4, 4], [8], dropout=0.0, optimizer=optim.SGD(lr=0.004, momentum=0.9),
+                         device="cpu")
+        with pytest.raises(NotImplementedError):
+            m3.fit(x, y, batch_size=16, epochs=1, verbose=0, callbacks=[hcb.LearningRateWarmupCallback(2)])
+        m3.fit(x, y, batch_size=16, epochs=1, verbose=0,
+               callbacks=[hcb.LearningRateWarmupCallback(2, momentum_correction=False)])
+    finally:
+        dist.size = orig
+    for a, b in zip(wa, wb):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+
+
 def test_optimizer_closed_form_single_step():
     torch.manual_seed(0)
     p0, g = torch.randn(50), torch.randn(50)

@@ -280,7 +280,7 @@ def test_conv_stack_forward_matches_per_layer(kind, drop, cin, hw, monkeypatch):
     rounding points and dropout counters), and hence the same training step."""
     outs = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("INTML_CONV_STACK", flag)
+        monkeypatch.setenv("INTML_TUNE", "conv_stack=" + flag)
         set_random_seed(33)
         m = _build(kind, "cuda", opt="Adam", drop=drop, cin=cin, hw=hw)
         x, y = _data(m, 96, seed=8)
@@ -338,3 +338,27 @@ def test_device_lr_warmup_matches_host_schedule():
     assert a._executor._plans[(32, "train")].multi_graphs, "warmup must not force one step per replay"
     for wa, wb in zip(a.get_weights(), b.get_weights()):
         np.testing.assert_allclose(wa, wb, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["rpv", "mnist"])
+def test_nonfinite_loss_reads_nan(kind):
+    """A diverged model (a NaN weight) reports loss / val_loss NaN, never a finite value: the
+    head kernel's int64 fixed-point metric sum cannot carry a NaN, so it counts non-finite
+    workgroups in a flag word and the host returns NaN.  The FoM of such a
+    history is NaN (ranked worst), and finite epochs before the divergence still win."""
+    from cori_intml_examples_amd.hpo.evaluator import figure_of_merit
+    set_random_seed(5)
+    m = _build(kind, "cuda", opt="Adam", cin=1, hw=16 if kind == "rpv" else 28)
+    x, y = _data(m, 64, seed=2)
+    h = m.fit(x, y, batch_size=32, epochs=1, validation_data=(x, y), verbose=0)
+    assert np.isfinite(h.history["loss"][0]) and np.isfinite(h.history["val_loss"][0])
+    w = m.get_weights()
+    w[-2] = w[-2].copy()
+    w[-2].flat[0] = np.nan                        # head kernel weight
+    m.set_weights(w)
+    ev = m.evaluate(x, y, verbose=0)
+    assert np.isnan(ev[0]), ev
+    h2 = m.fit(x, y, batch_size=32, epochs=1, validation_data=(x, y), verbose=0)
+    assert np.isnan(h2.history["loss"][0]) and np.isnan(h2.history["val_loss"][0]), h2.history
+    assert np.isnan(figure_of_merit(h2.history["val_loss"]))
+    assert figure_of_merit(h.history["val_loss"] + h2.history["val_loss"]) == h.history["val_loss"][0]

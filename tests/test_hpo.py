@@ -210,3 +210,21 @@ def test_cray_bench_cpu():
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["unit"] == "evaluations/hour" and rec["evaluations"] == 2 and rec["failed"] == 0
     assert rec["gpus_per_eval"] == 2 and rec["value"] > 0
+
+
+def test_figure_of_merit_nan_safe():
+    """FoM ("best" = min val_loss, "last") never lets a NaN epoch win and scores an all-NaN
+    (diverged) trial NaN, which the genetic optimizer ranks worst; min() with a NaN in the
+    list would be order-dependent."""
+    import math
+    from cori_intml_examples_amd.hpo.evaluator import figure_of_merit, parse_fom
+    nan = float("nan")
+    assert figure_of_merit([0.5, 0.3, 0.4]) == 0.3
+    assert figure_of_merit([nan, 0.3]) == 0.3 and figure_of_merit([0.3, nan]) == 0.3
+    assert math.isnan(figure_of_merit([nan, nan])) and math.isnan(figure_of_merit([]))
+    assert figure_of_merit([0.2, 0.4], "last") == 0.4
+    assert math.isnan(figure_of_merit([0.2, float("inf")], "last"))
+    assert math.isnan(parse_fom("FoM: nan"))
+    from cori_intml_examples_amd.hpo.genetic import _fitness
+    f = _fitness([0.5, nan, 0.2])
+    assert f[1] == min(f) and f[2] == max(f)
