@@ -74,6 +74,10 @@ struct ConvMMArgs {
   int dbg = 0;   // ablation (timing only, wrong results): 1 skip staging, 2 skip MFMA, 4 skip stores,
                  // 8 skip the weight staging only; 16 = per-pixel unpool staging (A/B, exact)
   unsigned long long* ts = nullptr;   // diagnostics: [grid block][8] phase stamps, wave 0 lane 0 (null = off)
+  // conv_halo LDS layout: input-halo pixel stride in elements (0 = Cs_in; padded strides
+  // break the fragment reads' bank conflicts, models/lds_layout.py)
+  int xpix = 0;
+  int kpipe = 0;                 // software-pipelined k loop with scalar tap offsets (Cs % 32 == 0)
 };
 
 // Layer-fused forward of a conv stack (conv_stack.hip): one workgroup per image, all
@@ -95,6 +99,10 @@ struct StackLayer {
   bf16* out = nullptr;                // stage output [B][Hp][Wp][Cs_out]
   uint8_t* code = nullptr;            // pool argmax codes, same shape (or null)
   int w_lds = 0;                      // bf16 element offset of the pack inside the LDS weights
+  // LDS layout of this layer's INPUT halo image (written by the previous layer's epilogue or
+  // staged from the input): pixel stride in elements and row stride in pixels, padded by the
+  // host's bank-conflict model (models/lds_layout.py) so the fragment reads are conflict-free
+  int xpix = 0, xrow = 0;
 };
 
 struct ConvStackArgs {
@@ -112,12 +120,6 @@ struct ConvStackArgs {
   int rows[MAX_STACK][MAX_STACK_SPLIT][6] = {};
   StackLayer L[MAX_STACK];
   unsigned long long* ts = nullptr;   // diagnostics: per-wave phase stamps [blocks*8][32]: 16 wall, 16 shader clock (null = off)
-  // src_mode 1 / 2: image b is dataset row perm[pos + b] (st->pos / st->eval_pos, the
-  // prologue's gather rule) read straight from StepState::data_x instead of A.x; each band
-  // then copies its owned input rows to xout (the batch buffer the backward reads)
-  int src_mode = 0;
-  bf16* xout = nullptr;
-  int xrows[MAX_STACK_SPLIT][2] = {};   // input rows [lo, hi) band sp copies to xout (host-checked)
 };
 
 // Weight gradient: dW[k][n] = sum_pixels im2col(x)[p][k] * dY[p][n]  (split over pixels)
@@ -151,6 +153,9 @@ struct WgradArgs {
   // bias, opt_b + n) as soon as their gradient is final -- no slab reduction for the layer
   OptimArgs opt;
   int opt_w = -1, opt_b = -1;
+  // wgrad_halo LDS layout (models/lds_layout.py picks it with a bank-conflict model; 0 =
+  // dense): X-halo pixel stride in elements, X-halo row stride in pixels, dY row stride
+  int xpix = 0, xrow = 0, dyld = 0;
 };
 
 // Dense forward, split-K partial products: part[s][m][n]
@@ -271,13 +276,6 @@ struct DualExtra {
   OptimArgs ro;
   float* grad = nullptr;
   int n_r = 0, rfirst = 0;
-  // Chained wgrad (ntt2 > 0): each dgrad workgroup, right after writing its block of dP
-  // (the gradient wrt the previous stage's output), runs the PREVIOUS layer's weight
-  // gradient over exactly the conv rows that block feeds (w2.blocks_per_split wgrad blocks
-  // starting at block bx * bps, one slab per dgrad block) -- the first conv layer's wgrad
-  // needs no launch of its own, and dP is re-read from this CU's own stores.
-  WgradArgs w2;
-  int MT2 = 0, ntt2 = 0;
 };
 
 // Fused data-parallel all-reduce + optimizer over xGMI peer memory (xgmi.hip).  Every rank

@@ -85,7 +85,7 @@ PYBIND11_MODULE(_kernels, m) {
       RW(ConvMMArgs, Cs_out) RW(ConvMMArgs, Hp) RW(ConvMMArgs, Wp) PTR(ConvMMArgs, code)
       RW(ConvMMArgs, drop_thr) RW(ConvMMArgs, drop_scale) RW(ConvMMArgs, seed) RW(ConvMMArgs, stream_id)
       PTR(ConvMMArgs, st) RW(ConvMMArgs, bt) RW(ConvMMArgs, R) PTR(ConvMMArgs, in_code) PTR(ConvMMArgs, zero)
-      RW(ConvMMArgs, in_pH) RW(ConvMMArgs, in_pW) RW(ConvMMArgs, dbg) PTR(ConvMMArgs, ts);
+      RW(ConvMMArgs, in_pH) RW(ConvMMArgs, in_pW) RW(ConvMMArgs, dbg) PTR(ConvMMArgs, ts) RW(ConvMMArgs, xpix) RW(ConvMMArgs, kpipe);
 
   py::class_<WgradArgs>(m, "WgradArgs")
       .def(py::init<>())
@@ -96,7 +96,7 @@ PYBIND11_MODULE(_kernels, m) {
       RW(WgradArgs, KT) PTR(WgradArgs, slab) PTR(WgradArgs, bslab) RW(WgradArgs, R)
       RW(WgradArgs, blocks_per_split) PTR(WgradArgs, dy_code) PTR(WgradArgs, zero) RW(WgradArgs, dHp) RW(WgradArgs, dWp)
       RW(WgradArgs, dbg) PTR(WgradArgs, ts) PTR(WgradArgs, ts2) RW(WgradArgs, opt) RW(WgradArgs, opt_w)
-      RW(WgradArgs, opt_b);
+      RW(WgradArgs, opt_b) RW(WgradArgs, xpix) RW(WgradArgs, xrow) RW(WgradArgs, dyld);
 
   py::class_<DenseFwdArgs>(m, "DenseFwdArgs")
       .def(py::init<>())
@@ -137,7 +137,7 @@ PYBIND11_MODULE(_kernels, m) {
       RW(StackLayer, pad_l) RW(StackLayer, KS) RW(StackLayer, NT) RW(StackLayer, pool) RW(StackLayer, relu)
       RW(StackLayer, Hp) RW(StackLayer, Wp) RW(StackLayer, drop_thr) RW(StackLayer, drop_scale)
       RW(StackLayer, stream_id) PTR(StackLayer, wpk) PTR(StackLayer, bias) PTR(StackLayer, out)
-      PTR(StackLayer, code) RW(StackLayer, w_lds);
+      PTR(StackLayer, code) RW(StackLayer, w_lds) RW(StackLayer, xpix) RW(StackLayer, xrow);
 
   py::class_<ConvStackArgs>(m, "ConvStackArgs")
       .def(py::init<>())
@@ -145,12 +145,6 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(ConvStackArgs, st) RW(ConvStackArgs, dbg) RW(ConvStackArgs, off_w) RW(ConvStackArgs, off_codes) RW(ConvStackArgs, lds_bytes)
       .def("set_buf_offsets", [](ConvStackArgs& a, int b0, int b1) { a.off_buf[0] = b0; a.off_buf[1] = b1; })
       RW(ConvStackArgs, splits) PTR(ConvStackArgs, ts) RW(ConvStackArgs, off_bias)
-      RW(ConvStackArgs, src_mode) PTR(ConvStackArgs, xout)
-      .def("set_xrows", [](ConvStackArgs& a, int sp, int lo, int hi) {
-        if (sp < 0 || sp >= MAX_STACK_SPLIT) throw std::out_of_range("conv stack band");
-        a.xrows[sp][0] = lo;
-        a.xrows[sp][1] = hi;
-      })
       .def("set_rows", [](ConvStackArgs& a, int l, int sp, int c0, int c1, int o0, int o1, int ib, int ih) {
         if (l < 0 || l >= MAX_STACK || sp < 0 || sp >= MAX_STACK_SPLIT) throw std::out_of_range("conv stack rows");
         const int v[6] = {c0, c1, o0, o1, ib, ih};
@@ -298,20 +292,11 @@ PYBIND11_MODULE(_kernels, m) {
   m.def(
       "dual_halo",
       [](const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits, uintptr_t s,
-         const RedTable* rt, const OptimArgs* ro, uintptr_t rgrad, int rfirst, const WgradArgs* w2, int MT2,
-         int ntt2) {
+         const RedTable* rt, const OptimArgs* ro, uintptr_t rgrad, int rfirst) {
         DualExtra x;
         if (rt && ro && rt->nblocks > 0) {
           x.rt = *rt, x.ro = *ro, x.grad = reinterpret_cast<float*>(rgrad);
           x.n_r = rt->nblocks, x.rfirst = rfirst;
-        }
-        if (w2 && ntt2 > 0) {
-          const int R_d = ca.R, P = w2->Ho / ca.Ho;
-          // the chained wgrad's blocks must tile exactly the rows of the dgrad blocks
-          if (P * ca.Ho != w2->Ho || ca.Ho % R_d || (P * R_d) % w2->R || w2->blocks_per_split != P * R_d / w2->R ||
-              w2->stride != 1 || w2->B != ca.B)
-            throw std::invalid_argument("dual_halo: chained wgrad geometry does not tile the dgrad blocks");
-          x.w2 = *w2, x.MT2 = MT2, x.ntt2 = ntt2;
         }
         const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, x, S(s));
         check_last("dual_halo");
@@ -319,9 +304,7 @@ PYBIND11_MODULE(_kernels, m) {
       },
       py::arg("ca"), py::arg("ntc"), py::arg("wa"), py::arg("MT"), py::arg("NTT"), py::arg("splits"), py::arg("s"),
       py::arg("rt") = nullptr, py::arg("ro") = nullptr, py::arg("rgrad") = 0, py::arg("rfirst") = 0,
-      py::arg("w2") = nullptr, py::arg("MT2") = 0, py::arg("ntt2") = 0,
-      "dual wgrad + dgrad launch; with (rt, ro, rgrad) it also runs that table's reduction + optimizer; "
-      "with (w2, MT2, ntt2) each dgrad workgroup then runs the previous layer's wgrad over its rows");
+      "dual wgrad + dgrad launch; with (rt, ro, rgrad) it also runs that table's reduction + optimizer");
   m.attr("MAX_STACK") = MAX_STACK;
   m.attr("MAX_STACK_SPLIT") = MAX_STACK_SPLIT;
   m.attr("STACK_THREADS") = conv_stack_threads();

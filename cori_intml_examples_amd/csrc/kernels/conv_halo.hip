@@ -27,8 +27,9 @@ size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc) {
   const int R_in = (a.R - 1) * a.stride + a.KH;
   const int TM = ntc >= 8 ? 2 : 4;
   const size_t ep_wave = (size_t)TM * 16 * 2 * ntc * 16;   // bytes
+  const int XP = (cs4 || !a.xpix) ? a.Cs_in : a.xpix;
   return (size_t)((ntab * 4 + 15) & ~15) + 32 + (size_t)a.KS * ntc * 64 * 16 +
-         (((size_t)R_in * W_in * a.Cs_in + 7) & ~(size_t)7) * 2 + 4 * ep_wave;
+         (((size_t)R_in * W_in * XP + 7) & ~(size_t)7) * 2 + 4 * ep_wave;
 }
 
 template <int NTC, int KCH, bool CS4>

@@ -12,6 +12,8 @@
 template <int NTC, int TM, int KCH, bool CS4>
 __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx, const int by, char* smem) {
   const int KS = a.KS, R = a.R, s = a.stride, dil = a.in_dil, Cs = a.Cs_in;
+  // halo pixel stride (elements): padded by the host's bank-conflict model (lds_layout.py)
+  const int XP = (CS4 || !a.xpix) ? Cs : a.xpix;
   const int ntab = CS4 ? KS * 8 : KS * 4;
   int* tab = reinterpret_cast<int*>(smem);
   const int tab_bytes = (ntab * 4 + 15) & ~15;
@@ -80,7 +82,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
       int e = -1;
       if (tap < KHW) {
         const int ky = tap / a.KW;
-        e = (ky * W_in + (tap - ky * a.KW)) * Cs + (k0 - tap * Cs);
+        e = (ky * W_in + (tap - ky * a.KW)) * XP + (k0 - tap * Cs);
       }
       tab[c] = e;
     }
@@ -106,7 +108,8 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
         const int pix = fcpp.div(i);
         const int r = fwin.div(pix);
         const int y = yb + r, x = xb0 + (pix - r * W_in);
-        if (y < 0 || x < 0 || y >= Ha || x >= Wa) *reinterpret_cast<bf16x8*>(xl + (size_t)i * 8) = zero_bf16x8();
+        if (y < 0 || x < 0 || y >= Ha || x >= Wa)
+          *reinterpret_cast<bf16x8*>(xl + (size_t)pix * XP + (i - pix * hcpp) * 8) = zero_bf16x8();
       }
       const int y_lo = max(yb, 0), y_hi = min(yb + R_in, Ha);
       const int x_lo = max(xb0, 0), x_hi = min(xb0 + W_in, Wa);
@@ -149,14 +152,20 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
                                ((((w >> 24) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
               }
               const uint4 v = {raw[u].x & m[0], raw[u].y & m[1], raw[u].z & m[2], raw[u].w & m[3]};
-              *reinterpret_cast<uint4*>(xl + ((size_t)((y - yb) * W_in + (x - xb0)) * Cs + qc[u])) = v;
+              *reinterpret_cast<uint4*>(xl + ((size_t)((y - yb) * W_in + (x - xb0)) * XP + qc[u])) = v;
             }
           }
         }
       }
     } else {
-      staged_copy<8, bf16x8>(
-          nch, tid, 256, halo8, [&](int i, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + (size_t)i * 8) = v; });
+      staged_copy<8, bf16x8>(nch, tid, 256, halo8, [&](int i, const bf16x8& v) {
+        int o = i * 8;
+        if (XP != Cs) {
+          const int pix = fcpp.div(i);
+          o = pix * XP + (i - pix * hcpp) * 8;
+        }
+        *reinterpret_cast<bf16x8*>(xl + o) = v;
+      });
     }
   }
   HALO_STAMP(2);
@@ -173,7 +182,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
   const FastDiv fwp(a.Wp > 0 ? a.Wp : 1), fwo(a.Wo);
   // per-wave epilogue scratch [16 rows][NTC*16] fp32, after the 16-B aligned halo image
   constexpr int EPW = TM * 16 * 2 * NTC * 16 / 4;   // floats per wave: TM*16 rows x LDC bf16
-  float* ep = reinterpret_cast<float*>(xl + (((size_t)R_in * W_in * Cs + 7) & ~(size_t)7)) + wave * EPW;
+  float* ep = reinterpret_cast<float*>(xl + (((size_t)R_in * W_in * XP + 7) & ~(size_t)7)) + wave * EPW;
   const size_t qbase = ((size_t)b * a.Hp + (oy0 >> 1)) * a.Wp;
   for (int tb = wave * TM; tb < ntiles; tb += 4 * TM) {
     bool rv[TM];
@@ -196,14 +205,58 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
         ry = fwo.div(pi);
         rx = pi - ry * a.Wo;
       }
-      xrow[t] = xl + ((size_t)(ry * s) * W_in + rx * s) * Cs;
+      xrow[t] = xl + ((size_t)(ry * s) * W_in + rx * s) * XP;
     }
     f32x4 acc[TM][NTC];
 #pragma unroll
     for (int t = 0; t < TM; ++t)
 #pragma unroll
       for (int nt = 0; nt < NTC; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < (dbg_mfma ? KS : 0); kc += KCH) {
+    // Fast k loop (kpipe; 8-channel-aligned input with Cs % 32 == 0, the co-scheduled dgrad
+    // of the RPV / MNIST stacks): a k-step's tap is wave-uniform (k = 32 ks + 8 g lies in
+    // one tap), so its halo offset is scalar arithmetic -- no per-step table lookup, whose
+    // LDS round trip the A-fragment reads depended on -- and the loop is software-pipelined:
+    // step ks + 1's A / B fragments are requested before step ks's MFMAs issue.  Rows past
+    // the block read pixel 0 (finite data, never stored); same k order as the table loop.
+    const bool kfast = !CS4 && a.kpipe && (Cs & 31) == 0 && dbg_mfma;
+    if (kfast) {
+      const int cpk = Cs >> 5;                      // k-steps per tap
+      const int g8 = 8 * g;
+      auto kbase = [&](int ks) -> int {
+        const int tap = ks / cpk;
+        const int ky = tap / a.KW;
+        return __builtin_amdgcn_readfirstlane((ky * W_in + (tap - ky * a.KW)) * XP + (ks - tap * cpk) * 32);
+      };
+      bf16x8 af[2][TM], bw[2][NTC];
+      auto load_k = [&](int ks, bf16x8* av, bf16x8* bv) {
+        const int kb = kbase(ks) + g8;
+#pragma unroll
+        for (int t = 0; t < TM; ++t) av[t] = *reinterpret_cast<const bf16x8*>(xrow[t] + kb);
+#pragma unroll
+        for (int nt = 0; nt < NTC; ++nt)
+          bv[nt] = *reinterpret_cast<const bf16x8*>(wl + ((size_t)(ks * NTC + nt) * 64 + lane) * 8);
+      };
+      auto mma_k = [&](const bf16x8* av, const bf16x8* bv) {
+#pragma unroll
+        for (int nt = 0; nt < NTC; ++nt)
+#pragma unroll
+          for (int t = 0; t < TM; ++t) acc[t][nt] = mfma16(av[t], bv[nt], acc[t][nt]);
+      };
+      load_k(0, af[0], bw[0]);
+      int ks = 0;
+      for (; ks + 2 <= KS; ks += 2) {
+        load_k(ks + 1, af[1], bw[1]);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_k(af[0], bw[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + 2 < KS) load_k(ks + 2, af[0], bw[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_k(af[1], bw[1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (ks < KS) mma_k(af[0], bw[0]);
+    }
+    for (int kc = 0; kc < ((dbg_mfma && !kfast) ? KS : 0); kc += KCH) {
       int e0[KCH], e1[KCH];
 #pragma unroll
       for (int u = 0; u < KCH; ++u) {

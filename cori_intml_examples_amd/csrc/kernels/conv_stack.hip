@@ -55,10 +55,11 @@ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
 template <int NT, int TM, bool CS4>
 __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                             int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
-                                            int OW, LDS uint8_t* codes, const lbf16* wl, const LDS int* tab,
+                                            int OW, int XPo, LDS uint8_t* codes, const lbf16* wl, const LDS int* tab,
                                             const lbf16* zl, uint32_t step, const LDS float* lb) {
+  // OW / XPo: row stride (pixels) / pixel stride (elements) of the output image
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
-  const int Wi = L.Wo + L.KW - 1;
+  const int XR = L.xrow, XP = L.xpix;           // input image layout
   const int Cs = L.Cs_in, Cso = L.Cs_out, Cout = L.Cout, Wp = L.Wp, Wo = L.Wo, KS = L.KS;
   const int Hc = c1 - c0;                       // local conv rows (even when pooled)
   const int p0 = L.pool ? c0 >> 1 : c0;         // first local stage row (global index)
@@ -99,7 +100,7 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
         ry = fwo.div(pi);
         rx = pi - ry * Wo;
       }
-      xo[t] = ((ry + roff) * Wi + rx) * Cs;
+      xo[t] = ((ry + roff) * XR + rx) * XP;
     }
     f32x4 acc[TM][NT];
 #pragma unroll
@@ -148,7 +149,7 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
         const int pyl = fwp.div(w), pxl = w - pyl * Wp;
         const int orow = p0 + pyl - obase;
         const bool keep = orow >= 0 && orow < OH;
-        const int oo = (orow * OW + pxl + ol) * Cso, co = (pyl * Wp + pxl) * Cso;
+        const int oo = (orow * OW + pxl + ol) * XPo, co = (pyl * Wp + pxl) * Cso;
         const uint32_t qi = (qb + (uint32_t)w) * (uint32_t)Cout;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
@@ -180,7 +181,7 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
           const int yl = fwo.div(p), x = p - yl * Wo;
           const int orow = c0 + yl - obase;
           if (orow < 0 || orow >= OH) continue;
-          const int oo = (orow * OW + x + ol) * Cso;
+          const int oo = (orow * OW + x + ol) * XPo;
           const uint32_t mi = (mb + (uint32_t)p) * (uint32_t)Cout;
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) {
@@ -209,12 +210,13 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
 template <int NT, int TM, bool CS4, int KS, bool FULL>
 __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                                  int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
-                                                 int OW, LDS uint8_t* codes, const lbf16* wl, uint32_t step,
+                                                 int OW, int XPo, LDS uint8_t* codes, const lbf16* wl, uint32_t step,
                                                  const LDS float* lb, bool stamp) {
+  // OW / XPo: row stride (pixels) / pixel stride (elements) of the output image
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int Wi = L.Wo + L.KW - 1;
-  const int Cs = L.Cs_in, Cso = L.Cs_out, Cout = L.Cout, Wp = L.Wp;
+  const int Wi = L.xrow, Cs = L.xpix;           // input image row / pixel strides
+  const int Cso = L.Cs_out, Cout = L.Cout, Wp = L.Wp;
   const int p0 = c0 >> 1;
   const int tpr = Wp >> 2;                      // tiles per pooled row
   const int ntiles = ((c1 - c0) >> 1) * tpr;
@@ -233,7 +235,7 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
       e0[ks] = t0 < 9 ? ((t0 / 3) * Wi + (t0 % 3)) * 4 : 0;
       e1[ks] = t1 < 9 ? ((t1 / 3) * Wi + (t1 % 3)) * 4 : 0;
     } else {
-      const int tap = k0 / Cs, c = k0 - tap * Cs;
+      const int tap = k0 / L.Cs_in, c = k0 - tap * L.Cs_in;
       e0[ks] = tap < 9 ? ((tap / 3) * Wi + (tap % 3)) * Cs + c : 0;
     }
   }
@@ -247,8 +249,8 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
   const bool tpow2 = (tpr & (tpr - 1)) == 0;
   const int tsh = __builtin_ctz(tpr);
   auto trow = [&](int tile) { return tpow2 ? tile >> tsh : tile / tpr; };
-  // epilogue lane constants: window g of the tile, channel r of n-tile 0
-  const int lo_g = g * Cso + r;
+  // epilogue lane constants: window g of the tile, channel r of n-tile 0 (output image / codes)
+  const int lo_g = g * XPo + r, lc_g = g * Cso + r;
   const uint32_t qlane = (uint32_t)g * (uint32_t)Cout + (uint32_t)r;
   // FULL: Cso == Cout == NT * 16 (no padded channels): no per-lane channel guards
   for (int tb = wave * TM; tb < ntiles; tb += STACK_WAVES * TM) {
@@ -305,7 +307,7 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
       const int orow = p0 + pyl - obase;
       const bool keep = orow >= 0 && orow < OH;
       if (FULL) {   // scalar tile bases + lane constants: one add per address
-        const int ob = (orow * OW + wx0 + ol) * Cso + lo_g, cb = (pyl * Wp + wx0) * Cso + lo_g;
+        const int ob = (orow * OW + wx0 + ol) * XPo + lo_g, cb = (pyl * Wp + wx0) * Cso + lc_g;
         const uint32_t qt = (qb + (uint32_t)(pyl * Wp + wx0)) * (uint32_t)Cout + qlane;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
@@ -324,7 +326,7 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
         continue;
       }
       const int pxl = wx0 + g;
-      const int oo = (orow * OW + pxl + ol) * Cso, co = (pyl * Wp + pxl) * Cso;
+      const int oo = (orow * OW + pxl + ol) * XPo, co = (pyl * Wp + pxl) * Cso;
       const uint32_t qi = (qb + (uint32_t)(pyl * Wp + pxl)) * (uint32_t)Cout;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
@@ -353,10 +355,10 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
 template <int NT, bool CS4>
 __device__ __forceinline__ void stack_layer_tm(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                                int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
-                                               int OW, LDS uint8_t* codes, const lbf16* wl, const LDS int* tab,
+                                               int OW, int XPo, LDS uint8_t* codes, const lbf16* wl, const LDS int* tab,
                                                const lbf16* zl, uint32_t step, const LDS float* lb) {
   constexpr int TM = NT >= 2 ? 2 : 4;
-  stack_layer<NT, TM, CS4>(A, L, b, c0, c1, roff, in, outimg, obase, OH, ol, OW, codes, wl, tab, zl, step, lb);
+  stack_layer<NT, TM, CS4>(A, L, b, c0, c1, roff, in, outimg, obase, OH, ol, OW, XPo, codes, wl, tab, zl, step, lb);
 }
 
 __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const ConvStackArgs A) {
@@ -403,16 +405,9 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     const StackLayer& L = A.L[0];
     lbf16* img = (lbf16*)(smem + A.off_buf[0]);
     const int Hi = A.rows[0][sp][5], Wi = L.Wo + L.KW - 1, Cs = L.Cs_in;
+    const int XR = L.xrow, XP = L.xpix;
     const int y0 = A.rows[0][sp][4];
     const bf16* x = A.x + (size_t)b * L.H * L.W * Cs;
-    if (A.src_mode) {   // the prologue's gather rule, read in place (no batch copy)
-      const StepState* st = A.st;
-      const int* perm = reinterpret_cast<const int*>(st->perm);
-      const int row = (A.src_mode == 1 ? st->pos : st->eval_pos) + b;
-      int src = (st->use_perm && perm) ? perm[row] : row;
-      src = min(max(src, 0), st->data_n - 1);
-      x = reinterpret_cast<const bf16*>(st->data_x) + (size_t)src * st->data_R;
-    }
     if (Cs == 4) {
       const FastDiv fwi(Wi);
       staged_copy<8, bf16x4>(
@@ -423,7 +418,10 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
             const bool ok = iy >= 0 && ix >= 0 && iy < L.H && ix < L.W;
             return load_bf16x4_if(ok, x + (iy * L.W + ix) * 4, x);
           },
-          [&](int i, const bf16x4& v) { *reinterpret_cast<LDS bf16x4*>(img + i * 4) = v; });
+          [&](int i, const bf16x4& v) {
+            const int hy = fwi.div(i);
+            *reinterpret_cast<LDS bf16x4*>(img + (hy * XR + (i - hy * Wi)) * XP) = v;
+          });
     } else {
       const int cpp = Cs >> 3;
       const FastDiv fcpp(cpp), fwi(Wi);
@@ -436,7 +434,11 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
             const bool ok = iy >= 0 && ix >= 0 && iy < L.H && ix < L.W;
             return load_bf16x8_if(ok, x + (iy * L.W + ix) * Cs + c, x);
           },
-          [&](int i, const bf16x8& v) { *reinterpret_cast<LDS bf16x8*>(img + i * 8) = v; });
+          [&](int i, const bf16x8& v) {
+            const int pix = fcpp.div(i), c = (i - pix * cpp) * 8;
+            const int hy = fwi.div(pix);
+            *reinterpret_cast<LDS bf16x8*>(img + (hy * XR + (pix - hy * Wi)) * XP + c) = v;
+          });
     }
   }
 
@@ -464,12 +466,16 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     lbf16* out = (lbf16*)(smem + ((l & 1) ? A.off_buf[0] : A.off_buf[1]));
     // where this layer's stage output lands: the next layer's halo image (rows from its
     // first input row), or a compact image of the local stage rows for the last layer
-    int obase, OH, ol, OW;
+    // (OW: logical width; ORS / OPS: row stride in pixels / pixel stride in elements of the
+    // output image -- the next layer's input layout, dense for the last layer's compact image)
+    int obase, OH, ol, OW, ORS, OPS;
     if (last) {
       obase = p0, OH = L.pool ? (c1 - c0) >> 1 : c1 - c0, ol = 0, OW = L.Wp;
+      ORS = OW, OPS = L.Cs_out;
     } else {
       const StackLayer& N = A.L[l + 1];
       obase = A.rows[l + 1][sp][4], OH = A.rows[l + 1][sp][5], ol = N.pad_l, OW = N.Wo + N.KW - 1;
+      ORS = N.xrow, OPS = N.xpix;
     }
     if (l == 1 && prefetch) {
       const int w1 = A.L[1].w_lds, w2 = A.n > 2 ? A.L[2].w_lds : 0, w3 = A.n > 3 ? A.L[3].w_lds : 0;
@@ -487,64 +493,42 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       // (all channels when Cs_out == Cout); only the rest of the image needs zeros.
       const int nr = L.pool ? (c1 - c0) >> 1 : c1 - c0;
       const int wr0 = max(0, p0 - obase), wr1 = min(OH, p0 - obase + nr);
+      // (in 8-channel vectors of the output layout; pixel padding is zeroed with its pixel,
+      // row padding past OW is never read)
+      const int vpp = OPS >> 3;                             // vectors per pixel (Cs_out % 8 == 0)
+      const int nrow = ORS * vpp;                           // vectors per image row
       if (L.Cs_out == L.Cout && wr0 < wr1 && !(A.dbg & 3)) {
-        const int cpp = L.Cs_out >> 3;
-        const int nrow = OW * cpp;                          // vectors per image row
         const int ntop = wr0 * nrow, nbot = (OH - wr1) * nrow;
-        const int nside = (OW - L.Wp) * cpp;                // border vectors per written row
+        const int nside = (OW - L.Wp) * vpp;                // border vectors per written row
         for (int i = tid; i < ntop + nbot; i += STACK_THREADS) z[i < ntop ? i : wr1 * nrow + (i - ntop)] = zero8;
         if (nside > 0) {
-          const int lcols = ol * cpp;
+          const int lcols = ol * vpp;
           for (int i = tid; i < (wr1 - wr0) * nside; i += STACK_THREADS) {
             const int rr = i / nside, c = i - rr * nside;
-            z[(wr0 + rr) * nrow + (c < lcols ? c : c + L.Wp * cpp)] = zero8;
+            z[(wr0 + rr) * nrow + (c < lcols ? c : c + L.Wp * vpp)] = zero8;
           }
         }
       } else {
-        const int nz = (OH * OW * L.Cs_out) >> 3;   // Cs_out % 8 == 0
+        const int nz = OH * nrow;
         for (int i = tid; i < nz; i += STACK_THREADS) z[i] = zero8;
       }
-      const int Wi = L.Wo + L.KW - 1, KHW = L.KH * L.KW, cw = L.Cs_in == 4 ? 4 : 8;
+      const int Wi = L.xrow, KHW = L.KH * L.KW, cw = L.Cs_in == 4 ? 4 : 8;
       const int ntab = L.Cs_in == 4 ? L.KS * 8 : L.KS * 4;
       for (int c = tid; c < ntab; c += STACK_THREADS) {
         const int k0 = c * cw, tap = k0 / L.Cs_in;
         int e = -1;
         if (tap < KHW) {
           const int ky = tap / L.KW;
-          e = (ky * Wi + (tap - ky * L.KW)) * L.Cs_in + (k0 - tap * L.Cs_in);
+          e = (ky * Wi + (tap - ky * L.KW)) * L.xpix + (k0 - tap * L.Cs_in);
         }
         tab[c] = e;
       }
     }
     __syncthreads();
     STACK_STAMP(2 + 4 * l);
-    if (l == 0 && A.xout && !(A.dbg & 8)) {
-      // this band's share of the input rows (host-computed partition, inside its staged
-      // halo image) -> the batch buffer the backward pass reads
-      const int r0 = A.xrows[sp][0], r1 = A.xrows[sp][1];
-      const int y0 = A.rows[0][sp][4], Wi = L.Wo + L.KW - 1;
-      const lbf16* img = (const lbf16*)(smem + A.off_buf[0]);
-      bf16* xo = A.xout + ((size_t)b * L.H + r0) * L.W * L.Cs_in;
-      if (L.Cs_in == 4) {
-        const int n = (r1 - r0) * L.W;
-        for (int i = tid; i < n; i += STACK_THREADS) {
-          const int ry = i / L.W, rx = i - ry * L.W;
-          *reinterpret_cast<bf16x4*>(xo + (size_t)i * 4) =
-              *reinterpret_cast<const LDS bf16x4*>(img + ((r0 + ry - y0) * Wi + rx + L.pad_l) * 4);
-        }
-      } else {
-        const int cpp = L.Cs_in >> 3, n = (r1 - r0) * L.W * cpp;
-        for (int i = tid; i < n; i += STACK_THREADS) {
-          const int pix = i / cpp, c = (i - pix * cpp) * 8;
-          const int ry = pix / L.W, rx = pix - ry * L.W;
-          *reinterpret_cast<bf16x8*>(xo + (size_t)pix * L.Cs_in + c) =
-              *reinterpret_cast<const LDS bf16x8*>(img + ((r0 + ry - y0) * Wi + rx + L.pad_l) * L.Cs_in + c);
-        }
-      }
-    }
     const lbf16* wl = wlds + L.w_lds;
-#define STACK_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, OW, codes, wl, tab, zl, step, lbias + l * 64
-#define ROWS_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, OW, codes, wl, step, lbias + l * 64, l == A.n - 1
+#define STACK_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, tab, zl, step, lbias + l * 64
+#define ROWS_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, step, lbias + l * 64, l == A.n - 1
     // row-aligned fast path (pooled, pooled width % 4 == 0, 3x3, instantiated KS), else generic
     const bool rows_ok = !(A.dbg & 16) && L.pool && (L.Wp & 3) == 0 && L.KH == 3 && L.KW == 3 && !(A.dbg & 3);
     // TM = 1 when it evens out the waves' tile counts (few tiles per workgroup)
@@ -594,7 +578,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
         const int pix = fc.div(i), c = (i - pix * cch) * 8;
         const int pyo = fw.div(pix), px = pix - pyo * L.Wp;
         *reinterpret_cast<bf16x8*>(gout + pix * L.Cs_out + c) =
-            *reinterpret_cast<const LDS bf16x8*>(out + ((own0 + pyo - obase) * OW + px + ol) * L.Cs_out + c);
+            *reinterpret_cast<const LDS bf16x8*>(out + ((own0 + pyo - obase) * ORS + px + ol) * OPS + c);
       }
       if (L.pool && L.code) {
         const int nb = ((own1 - own0) * L.Wp * L.Cs_out) >> 3;

@@ -25,12 +25,7 @@ bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT
   const int cgx = ca.B * ((ca.Ho + ca.R - 1) / ca.R);
   const dim3 wg(splits, (wa.NT + NTT - 1) / NTT, (wa.Ktiles + MT - 1) / MT);
   const int mtw = (MT + (wa.bslab ? 1 : 0) + 3) / 4;
-  size_t lds = std::max(conv_halo_lds_bytes(ca, ntc), wgrad_halo_lds_bytes(wa, MT, NTT));
-  if (x.ntt2) {
-    // chained wgrad: every dgrad block feeds whole wgrad blocks of one slab, one n-group
-    if (ntc != 1 || cgy != 1 || x.w2.Cs_in != 4 || (x.w2.NT + x.ntt2 - 1) / x.ntt2 != 1) return false;
-    lds = std::max(lds, wgrad_halo_lds_bytes(x.w2, x.MT2, x.ntt2));
-  }
+  const size_t lds = std::max(conv_halo_lds_bytes(ca, ntc), wgrad_halo_lds_bytes(wa, MT, NTT));
   if (lds > 160 * 1024 || (x.n_r && lds < 1024)) return false;
   // dgrad m-tiles per wave per pass: the TM in {4, 2} that minimises the busiest wave's
   // tile count over the block (ties -> larger TM: more fragment reuse); TM = 1 only when
@@ -45,7 +40,6 @@ bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT
     const int load = t * ((ntiles + 4 * t - 1) / (4 * t));   // tiles of the busiest wave
     if (load < best) { best = load; tm = t; }
   }
-  if (x.ntt2) return dual_launch_chain(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, x, s);
   switch (ntc) {
     case 1: return dual_launch_n1(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, x, s);
     case 2: return dual_launch_n2(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, x, s);

@@ -5,7 +5,7 @@
 #include "wgrad_halo_body.h"
 #include "reduce_body.h"
 
-template <int NTC, int MTW, int NTT, int TM, int C2 = 0>
+template <int NTC, int MTW, int NTT, int TM>
 __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, const WgradArgs wa, const int MT,
                                                         const int n_w, const int wgx, const int wgy, const int cgx,
                                                         const DualExtra x) {
@@ -27,13 +27,6 @@ __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, con
   } else {
     id -= n_w;
     conv_halo_body<NTC, TM, 8, false>(ca, id % cgx, id / cgx, smem);
-    if constexpr (C2 > 0) {
-      // chained wgrad of the previous (first, 4-channel) layer over this block's rows: the
-      // barrier retires the dgrad body's LDS use and makes its dP stores visible to the
-      // workgroup's own loads (same CU, workgroup-scope fence)
-      __syncthreads();
-      wgrad_halo_body<1, C2, true, true>(x.w2, x.MT2, id % cgx, 0, 0, smem);
-    }
   }
   if (wa.ts) {
     __syncthreads();
@@ -41,10 +34,10 @@ __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, con
   }
 }
 
-template <int NTC, int MTW, int NTT, int TM, int C2 = 0>
+template <int NTC, int MTW, int NTT, int TM>
 static void dual_t(const ConvMMArgs& ca, const WgradArgs& wa, int MT, dim3 wg, int cgx, int cgy, size_t lds,
                    const DualExtra& x, hipStream_t s) {
-  auto k = dual_halo_kernel<NTC, MTW, NTT, TM, C2>;
+  auto k = dual_halo_kernel<NTC, MTW, NTT, TM>;
   if (lds > 65536) hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int n_w = wg.x * wg.y * wg.z;
   hipLaunchKernelGGL(k, dim3(n_w + cgx * cgy + x.n_r), dim3(256), lds, s, ca, wa, MT, n_w, (int)wg.x, (int)wg.y, cgx,
@@ -79,7 +72,3 @@ DUAL_N_DECL(2);
 DUAL_N_DECL(4);
 DUAL_N_DECL(8);
 
-// chained-wgrad instantiations (dual_halo_chain.hip): NTC = 1 dgrad, first-layer wgrad of
-// ntt2 in {1, 2} n-tiles; false if the combination is not instantiated
-bool dual_launch_chain(const ConvMMArgs& ca, const WgradArgs& wa, int MT, int NTT, int mtw, int tm, dim3 wg,
-                       int cgx, int cgy, size_t lds, const DualExtra& x, hipStream_t s);

@@ -11,6 +11,12 @@
 // K split across the 64 lanes, cross-lane shuffle reductions.
 #include "bwd_through.h"
 
+// Keras' probability clip (tf.clip_by_value) propagates a NaN; fminf/fmaxf would replace it
+// by a bound and turn a diverged model's loss into a finite value
+__device__ __forceinline__ float clip_nan(float q, float lo, float hi) {
+  return q != q ? q : fminf(fmaxf(q, lo), hi);
+}
+
 #define HEAD_RB 4
 #define HEAD_EPI_MAX 1024   // widest previous dense whose epilogue the head absorbs
 #define HEAD_W_LDS 2048     // head weights staged in LDS up to this many floats
@@ -112,7 +118,7 @@ __device__ __forceinline__ void softmax_cce_lanes(const HeadArgs& a, const float
     const float yn = cls ? ysh_row[n] : 0.f;
     const float q = p / ps;
     const bool inr = (q >= eps) && (q <= 1.f - eps);
-    const float qc = fminf(fmaxf(q, eps), 1.f - eps);
+    const float qc = clip_nan(q, eps, 1.f - eps);
     const float ln = cls ? -yn * logf(qc) : 0.f;
     float gn = (cls && inr) ? -yn / qc : 0.f;
     const float gq = grp16_sum(gn * (cls ? q : 0.f));
@@ -259,7 +265,7 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
         if (yr) {
           const float yv = yr[0];
           const bool inr = (p >= eps) && (p <= 1.f - eps);
-          const float pc = fminf(fmaxf(p, eps), 1.f - eps);
+          const float pc = clip_nan(p, eps, 1.f - eps);
           const float lg = logf(pc / (1.f - pc));
           loss = fmaxf(lg, 0.f) - lg * yv + log1pf(expf(-fabsf(lg)));
           dz[0] = inr ? (pc - yv) : 0.f;
@@ -284,7 +290,7 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
           for (int n = 0; n < N; ++n) {
             const float q = p[n] / ps;
             const bool inr = (q >= eps) && (q <= 1.f - eps);
-            const float qc = fminf(fmaxf(q, eps), 1.f - eps);
+            const float qc = clip_nan(q, eps, 1.f - eps);
             loss -= yr[n] * logf(qc);
             gn[n] = inr ? -yr[n] / qc : 0.f;
             gq += gn[n] * q;

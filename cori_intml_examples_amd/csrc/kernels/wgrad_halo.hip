@@ -30,9 +30,11 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(const WgradArgs a, cons
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT) {
   const int W_in = (a.Wo - 1) * a.stride + a.KW;
   const int R_in = (a.R - 1) * a.stride + a.KH;
-  const size_t x_elems = (size_t)(((R_in * W_in * a.Cs_in) + 7) & ~7);
+  const int XP = a.xpix ? a.xpix : a.Cs_in, XR = a.xrow ? a.xrow : W_in;
+  const int ldb = a.dyld ? a.dyld : NTT * 16 + 8;
+  const size_t x_elems = (size_t)(((R_in * XR * XP) + 7) & ~7);
   const size_t npb32 = (size_t)((a.R * a.Wo + 31) & ~31);
-  return x_elems * 2 + npb32 * (NTT * 16 + 8) * 2 + 64 + (size_t)(MT * 4 + 4) * 4;
+  return x_elems * 2 + npb32 * ldb * 2 + 64 + (size_t)(MT * 4 + 4) * 4;
 }
 
 template <int MTW, int NTT, bool CS4>

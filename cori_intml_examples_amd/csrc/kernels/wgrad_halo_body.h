@@ -22,9 +22,12 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   const int R_in = (R - 1) * s + a.KH;
   const int npb = R * a.Wo;                         // pixels per full block
   const int npb32 = (npb + 31) & ~31;
-  const int ldb = NTT * 16 + 8;                     // dY LDS row stride (elements)
+  // LDS layout (bank-conflict model, models/lds_layout.py): X-halo pixel stride XP and row
+  // stride XR (pixels), dY row stride ldb; 0 = dense
+  const int XP = a.xpix ? a.xpix : Cs, XR = a.xrow ? a.xrow : W_in;
+  const int ldb = a.dyld ? a.dyld : NTT * 16 + 8;   // dY LDS row stride (elements)
   bf16* xl = reinterpret_cast<bf16*>(smem);
-  const int x_elems = ((R_in * W_in * Cs) + 7) & ~7;
+  const int x_elems = ((R_in * XR * XP) + 7) & ~7;
   bf16* dyl = xl + x_elems;
   bf16* zl = dyl + (size_t)npb32 * ldb;             // 64 B of zeros
   int* ktab = reinterpret_cast<int*>(zl + 32);      // [MT*4] halo offsets of k column blocks
@@ -44,7 +47,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
     int e = -1;
     if (tap < KHW && mt0 + c / 4 < a.Ktiles) {
       const int ky = tap / a.KW;
-      e = (ky * W_in + (tap - ky * a.KW)) * Cs + (k - tap * Cs);
+      e = (ky * XR + (tap - ky * a.KW)) * XP + (k - tap * Cs);
     }
     ktab[c] = e;
   }
@@ -80,6 +83,14 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   const int nch_x = R_in * W_in * cpp;              // X-halo chunks per block
   const int nch_y = npb32 * cpr;                    // dY chunks per block
   const FastDiv fcpp(cpp), fwin(W_in), fcpr(cpr), fwo(a.Wo);
+  // LDS element offset of X-halo chunk idx (pixel-major chunks of cw channels)
+  const bool xdense = XP == Cs && XR == W_in;
+  auto xaddr = [&](int idx) -> int {
+    if (xdense) return idx * cw;
+    const int pix = fcpp.div(idx), c = (idx - pix * cpp) * cw;
+    const int r = fwin.div(pix);
+    return (r * XR + (pix - r * W_in)) * XP + c;
+  };
   const bool dbg_stage = !(a.dbg & 1);
   // Pooled dY (dP + argmax codes) over whole even blocks: stage each pooled chunk ONCE and
   // expand it into its 2x2 window's pixel rows in LDS (a quarter of the global loads of a
@@ -124,18 +135,21 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   auto mma_block = [&](const int npix) {
       const int nks = (a.dbg & 2) ? 0 : (npix + 31) >> 5;
       for (int ks = 0; ks < nks; ++ks) {
-        // per-lane pixel rows of the two transposed reads (h = 0, 1)
-        const int P0 = ks * 32 + 8 * g + (i >> 2);
-        const int q0 = min(P0, npix - 1), q1 = min(P0 + 4, npix - 1);
+        // per-lane pixel rows of the two transposed reads (h = 0, 1).  MFMA k index 8g + j
+        // stands for pixel 4g + j (j < 4) / 16 + 4g + j - 4 (j >= 4) of the k-step -- the same
+        // bijection for both operands, so a 32-lane half reads 8 CONSECUTIVE pixels (the
+        // layout's bank-conflict-free pattern) instead of two runs 8 pixels apart
+        const int P0 = ks * 32 + 4 * g + (i >> 2);
+        const int q0 = min(P0, npix - 1), q1 = min(P0 + 16, npix - 1);
         const int y0 = fwo.div(q0), y1 = fwo.div(q1);
-        const int off0 = ((y0 * s) * W_in + (q0 - y0 * a.Wo) * s) * Cs;
-        const int off1 = ((y1 * s) * W_in + (q1 - y1 * a.Wo) * s) * Cs;
+        const int off0 = ((y0 * s) * XR + (q0 - y0 * a.Wo) * s) * XP;
+        const int off1 = ((y1 * s) * XR + (q1 - y1 * a.Wo) * s) * XP;
         const bf16* pbrow = dyl + (size_t)P0 * ldb + 4 * (i & 3);
         bf16x8 bfr[NTT], afr[MTW];
   #pragma unroll
         for (int v = 0; v < NTT; ++v) {
           const bf16* pb = pbrow + v * 16;
-          bfr[v] = __builtin_shufflevector(tr_read_h(pb), tr_read_h(pb + 4 * ldb), 0, 1, 2, 3, 4, 5, 6, 7);
+          bfr[v] = __builtin_shufflevector(tr_read_h(pb), tr_read_h(pb + 16 * ldb), 0, 1, 2, 3, 4, 5, 6, 7);
         }
   #pragma unroll
         for (int u = 0; u < MTW; ++u) {
@@ -159,6 +173,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   constexpr int WH_PX = 4, WH_PY = 4;
   if (PIPE && dbg_stage && nch_x <= WH_PX * 256 && (pexp ? nq : nch_y) <= WH_PY * 256) {
     uint4 xr[WH_PX], yr[WH_PY];
+    int xa[WH_PX];
     uint2 yc[WH_PY];
     uint32_t yp[WH_PY];
     auto fetch = [&](const int blk) {
@@ -172,6 +187,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
         const int pix = fcpp.div(idx), c = (idx - pix * cpp) * cw;
         const int r = fwin.div(pix);
         const int iy = yb + r, ix = xb0 + (pix - r * W_in);
+        xa[u] = (r * XR + (pix - r * W_in)) * XP + c;
         const bool ok = iy >= 0 && ix >= 0 && iy < a.H && ix < a.W;
         const bf16* src = ok ? xbase + ((size_t)iy * a.W + ix) * Cs + c : xbase;
         if (CS4) {
@@ -221,8 +237,8 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       for (int u = 0; u < WH_PX; ++u) {
         const int idx = tid + u * 256;
         if (idx >= nch_x) continue;
-        if (CS4) reinterpret_cast<uint2*>(xl)[idx] = uint2{xr[u].x, xr[u].y};
-        else reinterpret_cast<uint4*>(xl)[idx] = xr[u];
+        if (CS4) *reinterpret_cast<uint2*>(xl + xa[u]) = uint2{xr[u].x, xr[u].y};
+        else *reinterpret_cast<uint4*>(xl + xa[u]) = xr[u];
       }
       if (pexp) {
 #pragma unroll
@@ -293,7 +309,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
                 const bool ok = coords(idx, c, iy, ix);
                 return load_bf16x4_if(ok, xbase + ((size_t)iy * a.W + ix) * 4, xbase);
               },
-              [&](int idx, const bf16x4& v) { *reinterpret_cast<bf16x4*>(xl + (size_t)idx * 4) = v; });
+              [&](int idx, const bf16x4& v) { *reinterpret_cast<bf16x4*>(xl + xaddr(idx)) = v; });
         } else {
           staged_copy<8, bf16x8>(
               nch_x, tid, 256,
@@ -302,7 +318,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
                 const bool ok = coords(idx, c, iy, ix);
                 return load_bf16x8_if(ok, xbase + ((size_t)iy * a.W + ix) * Cs + c, xbase);
               },
-              [&](int idx, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + (size_t)idx * 8) = v; });
+              [&](int idx, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + xaddr(idx)) = v; });
         }
       }
       if (dbg_stage && pexp) {   // dY rows from pooled chunks, each loaded once

@@ -25,6 +25,7 @@ import torch
 from ..ops.hip import kernels
 from ..ops.rng import keep_threshold
 from ..utils.env import env_flag, tune
+from . import lds_layout
 from .executor_base import DeviceData, Executor, prepare_targets
 from .plan import Plan
 
@@ -796,24 +797,9 @@ class BatchPlan:
                     self.launches.append((dname, lambda s, a=a: K.dense_fwd(a, s)))
                 self.pack_readers.append((dname, sp.offset, sp.offset + sp.numel))
 
-        self.chain = {}            # dual launch name -> (WgradArgs, MT, NTT) of a chained wgrad
-        dual_args = {}             # conv index -> (dual launch name, its dgrad ConvMMArgs, ntc)
         for g, cs in reversed(list(zip(ex.convs, ex.plan.convs))):
             xin = self.xb if g.i == 0 else self.conv_out[g.i - 1]
-            chain = None
-            if g.i == 0 and 1 in dual_args and g.Cs_in == 4 and g.stride == 1 and tune("chain_wgrad", True):
-                dname1, da1, ntc1 = dual_args[1]
-                rows = self._chain_rows(g, da1)
-                if (rows is not None and ntc1 == 1 and cdiv(da1.NT, ntc1) == 1 and g.NT <= 1
-                        and cdiv(g.KH * g.KW * g.Cs_in, 16) + (1 if cs.conv.use_bias else 0) <= 4):
-                    chain = (rows[0], rows[1], bs * (da1.Ho // da1.R))
-            if chain is not None:
-                # the first layer's wgrad runs inside the layer-2 dual launch (DualExtra::w2):
-                # its slabs are final after that launch
-                wa, cfg, slab, bslab = self._wgrad_halo_args(xin, g, bs, cs.conv.use_bias, chain=chain)
-                self.chain[dname1] = (wa, cfg[0], cfg[1])
-                assert self.launches[-1][0] == dname1     # ready with the dual launch
-            elif self._wide(g.Cs_in, g.KS, g.NT):
+            if self._wide(g.Cs_in, g.KS, g.NT):
                 wa, cfg, slab, bslab = self._wgrad_tile_args(xin, g, bs, cs.conv.use_bias)
                 self.launches.append(("wgrad_conv%d" % g.i, lambda s, a=wa, c=cfg: K.wgrad_tile(a, c[0], s),
                                       "side"))
@@ -858,7 +844,6 @@ class BatchPlan:
                     # replaces the wgrad launch in place (its slabs are final after it)
                     ntc = self._halo_cfg(a, g.NTd, False, dual=True)
                     dname = "wgrad_dgrad_conv%d" % g.i
-                    dual_args[g.i] = (dname, a, ntc)
                     self.launches[w_at] = (dname, lambda s, a=a, n=ntc, w=wa, c=cfg, nm=dname: self._dual(a, n, w, c, s, nm),
                                            "main")
                 else:
@@ -905,6 +890,7 @@ class BatchPlan:
             for sp in range(splits):
                 a.set_rows(l, sp, *rows[l][sp])
         store = ex.store
+        lay = self._stack_img_layouts(convs)
         for i, (g, cs) in enumerate(zip(convs, ex.plan.convs)):
             L = K.StackLayer()
             L.H, L.W, L.Cs_in = g.H, g.W, g.Cs_in
@@ -923,6 +909,7 @@ class BatchPlan:
             if g.pool:
                 L.code = self.conv_code[i].data_ptr()
             L.w_lds = w_off[i]
+            L.xpix, L.xrow = lay[i]
             a.set_layer(i, L)
         self.stack_splits = splits
         return a
@@ -966,6 +953,7 @@ class BatchPlan:
             return (v + 15) & ~15
 
         n = len(convs)
+        lay = self._stack_img_layouts(convs)
         ntab = max((g.KS * 8 if g.Cs_in == 4 else g.KS * 4) for g in convs)
         off_bias = 32 + a16(4 * ntab)
         off_w = off_bias + 4 * 64 * self.ex.K.MAX_STACK      # biases [layer][64] fp32
@@ -978,7 +966,7 @@ class BatchPlan:
             P = 2 if g.pool else 1
             for sp in range(splits):
                 c0, c1, _, _, _, ih = rows[l][sp]
-                bufs[l & 1] = max(bufs[l & 1], ih * (g.Wo + g.KW - 1) * g.Cs_in)
+                bufs[l & 1] = max(bufs[l & 1], ih * lay[l][1] * lay[l][0])
                 if g.pool:
                     codes = max(codes, (c1 - c0) // 2 * g.Wp * g.Cs_out)
                 if l == n - 1:
@@ -990,6 +978,20 @@ class BatchPlan:
         if lds > self.LDS_LIMIT:
             return None
         return off_w, w_off, off_b0, off_b1, off_codes, lds, off_bias
+
+    @staticmethod
+    def _stack_img_layouts(convs):
+        """(xpix, xrow) of each stack layer's input halo image (lds_layout.stack_layout; dense
+        when the tune switch lds_layout is off)."""
+        out = []
+        for g in convs:
+            Wi = g.Wo + g.KW - 1
+            rows_path = g.pool and g.Wp % 4 == 0 and g.KH == 3 and g.KW == 3
+            if tune("lds_layout", True):
+                out.append(lds_layout.stack_layout(g.Cs_in, Wi, g.Wo, bool(rows_path), g.KS))
+            else:
+                out.append((g.Cs_in, Wi))
+        return out
 
     @staticmethod
     def _wide(Cs_in: int, KS: int, NT: int) -> bool:
@@ -1024,18 +1026,10 @@ class BatchPlan:
     def _dual(self, a, ntc, wa, cfg, s, name=None):
         K, ex = self.ex.K, self.ex
         early = (self.early_red or {}).get(name)
+        kw = {}
         if early is not None:   # this launch also carries an early bucket's reduction + optimizer
-            opt, grad = ex._optim_args(False, defer_pack=True), ex.store.grad.data_ptr()
-            ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, early[0], opt, grad,
-                             0)
-        else:
-            ch = self.chain.get(name)
-            if ch is not None:
-                ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, w2=ch[0], MT2=ch[1], ntt2=ch[2])
-                if not ok:
-                    raise RuntimeError("dual_halo: chained wgrad combination not instantiated (%s)" % name)
-            else:
-                ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s)
+            kw.update(rt=early[0], ro=ex._optim_args(False, defer_pack=True), rgrad=ex.store.grad.data_ptr())
+        ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, **kw)
         if not ok:   # unsupported combination
             K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
             K.conv_halo(a, ntc, s)
@@ -1059,6 +1053,10 @@ class BatchPlan:
         Wo, Ho = a.Wo, a.Ho
         W_in = (Wo - 1) * a.stride + a.KW
         step = 2 if pool else 1
+        if tune("lds_layout", True) and a.Cs_in % 8 == 0:
+            a.xpix = lds_layout.conv_layout(a.Cs_in, W_in, Wo, bool(pool), a.KH, a.KW)
+        a.kpipe = int(tune("conv_kpipe", True))
+        XP = a.xpix or a.Cs_in
         gy = cdiv(NT, ntc)
         # Balanced blocks: the fewest row blocks per image (c) that satisfy the limits, each
         # cdiv(Ho, c) rows -- not the largest R with a short remainder block.  Measured on
@@ -1069,7 +1067,7 @@ class BatchPlan:
             R = cdiv(cdiv(Ho, c), step) * step
             if R * Wo > 512:
                 continue
-            halo = ((R - 1) * a.stride + a.KH) * W_in * a.Cs_in * 2
+            halo = ((R - 1) * a.stride + a.KH) * W_in * XP * 2
             if halo + KS * ntc * 1024 > 80 * 1024:
                 continue
             if a.B * cdiv(Ho, R) * gy < want:
@@ -1114,29 +1112,7 @@ class BatchPlan:
         self.wgrad_slabs.append((slab, bslab))
         return a, (ntc, None, S), slab, bslab
 
-    def _chain_rows(self, g, da):
-        """Rows per block of a first-layer wgrad chained onto the dgrad blocks of ``da`` (the
-        layer-2 dual launch): the largest divisor of the conv rows one dgrad block feeds whose
-        block stays within ~512 pixels and the kernel's register staging pipeline; None if
-        the dgrad blocks cannot be tiled (see DualExtra in args.h)."""
-        if da.Ho <= 0 or g.Ho % da.Ho or da.Ho % da.R:
-            return None
-        P = g.Ho // da.Ho
-        rows = P * da.R
-        W_in = (g.Wo - 1) * g.stride + g.KW
-        cpp = g.Cs_in // 4
-        for r in range(rows, 0, -1):
-            if rows % r or r * g.Wo > 512:
-                continue
-            nch_x = ((r - 1) * g.stride + g.KH) * W_in * cpp
-            nch_y = cdiv(r * g.Wo, 32) * 32 * 2
-            if nch_x <= 1024 and nch_y <= 1024:
-                return r, rows // r
-        return None
-
-    def _wgrad_halo_args(self, xin, g, bs, bias, chain=None):
-        """``chain`` = (R, blocks_per_split, splits): the geometry of a wgrad chained onto a
-        dual launch's dgrad blocks (one slab per dgrad block) instead of the standalone one."""
+    def _wgrad_halo_args(self, xin, g, bs, bias):
         K, dev = self.ex.K, self.ex.device
         a = K.WgradArgs()
         a.x = xin.data_ptr()
@@ -1174,21 +1150,22 @@ class BatchPlan:
             if fits(r):
                 R = r
                 break
-        while R > 1 and (((R - 1) * g.stride + g.KH) * W_in * g.Cs_in * 2 > 64 * 1024):
+        # LDS layout from the bank-conflict model (pixel / row strides of the X halo, dY rows)
+        if tune("lds_layout", True):
+            a.xpix, a.xrow, a.dyld = lds_layout.wgrad_layout(g.Cs_in, W_in, g.Wo, NTT, g.KH, g.KW, g.stride,
+                                                             a.Ktiles)
+        XP, XR = (a.xpix or g.Cs_in), (a.xrow or W_in)
+        while R > 1 and (((R - 1) * g.stride + g.KH) * XR * XP * 2 > 64 * 1024):
             R -= 1
-        if chain is not None:
-            R, bps, S = chain
-            a.R = R
-        else:
-            a.R = R
-            nblocks = bs * cdiv(g.Ho, R)
-            groups = cdiv(NT, NTT) * cdiv(a.Ktiles, MT)
-            per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
-            s_budget = max(1, (8 << 20) // per_split_bytes)
-            cap = tune("wgrad_splits", 1024)
-            S = max(1, min(nblocks, s_budget, max(1, cap // groups)))
-            bps = cdiv(nblocks, S)
-            S = cdiv(nblocks, bps)
+        a.R = R
+        nblocks = bs * cdiv(g.Ho, R)
+        groups = cdiv(NT, NTT) * cdiv(a.Ktiles, MT)
+        per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
+        s_budget = max(1, (8 << 20) // per_split_bytes)
+        cap = tune("wgrad_splits", 1024)
+        S = max(1, min(nblocks, s_budget, max(1, cap // groups)))
+        bps = cdiv(nblocks, S)
+        S = cdiv(nblocks, bps)
         a.blocks_per_split = bps
         lds = K.wgrad_halo_lds_bytes(a, MT, NTT)
         if lds > 150 * 1024:

@@ -179,12 +179,13 @@ def describe_error(e: int) -> str:
     return "xgmi all-reduce: phase-%d wait timed out (peer rank dead or hung)" % e
 
 
-def create(rank: int, size: int, n: int, device: torch.device, allgather) -> Optional[XgmiAllreduce]:
+def create(rank: int, size: int, n: int, device: torch.device, allgather,
+           timeout_s: Optional[float] = None) -> Optional[XgmiAllreduce]:
     """Build + self-test collectively; returns the object only if EVERY rank passed both
     the setup and the self-test (same decision on every rank: the votes are gathered)."""
     x, why = None, None
     try:
-        x = XgmiAllreduce(rank, size, n, device, allgather)
+        x = XgmiAllreduce(rank, size, n, device, allgather, timeout_s=timeout_s)
         why = x.setup_error
     except Exception as e:            # noqa: BLE001
         why = "error: %s" % e

@@ -38,7 +38,7 @@ for name, fn, *_ in bp.launches:
         continue
     dfl = fn.__defaults__
     if name.startswith("wgrad_dgrad"):
-        ca, ntc, wa, cfg = dfl
+        ca, ntc, wa, cfg = dfl[:4]
     else:
         ca, ntc, (wa, cfg) = None, None, dfl
     MT, NTT, S = cfg
