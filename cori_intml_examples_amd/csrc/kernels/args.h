@@ -111,6 +111,7 @@ struct ConvStackArgs {
   uint32_t seed = 0;
   const StepState* st = nullptr;
   int off_w = 0, off_buf[2] = {0, 0}, off_codes = 0, lds_bytes = 0;   // LDS layout (bytes)
+  int off_codes2 = 0;                 // second argmax-code plane (odd layers)
   int off_bias = 0;                   // LDS bytes: biases [MAX_STACK][64] fp32
   int dbg = 0;   // ablation (timing only, wrong results): 1 no MFMA loop, 2 no epilogue, 4 no global stores, 8 no staging;
                  // 16 = generic layer path only (A/B of the row-aligned path; results exact)
@@ -156,6 +157,7 @@ struct WgradArgs {
   // wgrad_halo LDS layout (models/lds_layout.py picks it with a bank-conflict model; 0 =
   // dense): X-halo pixel stride in elements, X-halo row stride in pixels, dY row stride
   int xpix = 0, xrow = 0, dyld = 0;
+  int kperm = 0;                 // bit0: k index 8g+j <-> pixel 4g+j / 16+4g+j-4; bit1: no row-aligned fast path
 };
 
 // Dense forward, split-K partial products: part[s][m][n]

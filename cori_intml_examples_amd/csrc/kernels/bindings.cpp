@@ -38,6 +38,7 @@ void launch_dense_bwd_pair(const WgradArgs& wa, int kg, int ntt, int splits, con
                            hipStream_t s);
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s);
 int conv_stack_threads();
+int conv_stack_tabn();
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
 int gather_gx(int R);
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s);
@@ -96,7 +97,7 @@ PYBIND11_MODULE(_kernels, m) {
       RW(WgradArgs, KT) PTR(WgradArgs, slab) PTR(WgradArgs, bslab) RW(WgradArgs, R)
       RW(WgradArgs, blocks_per_split) PTR(WgradArgs, dy_code) PTR(WgradArgs, zero) RW(WgradArgs, dHp) RW(WgradArgs, dWp)
       RW(WgradArgs, dbg) PTR(WgradArgs, ts) PTR(WgradArgs, ts2) RW(WgradArgs, opt) RW(WgradArgs, opt_w)
-      RW(WgradArgs, opt_b) RW(WgradArgs, xpix) RW(WgradArgs, xrow) RW(WgradArgs, dyld);
+      RW(WgradArgs, opt_b) RW(WgradArgs, xpix) RW(WgradArgs, xrow) RW(WgradArgs, dyld) RW(WgradArgs, kperm);
 
   py::class_<DenseFwdArgs>(m, "DenseFwdArgs")
       .def(py::init<>())
@@ -142,7 +143,7 @@ PYBIND11_MODULE(_kernels, m) {
   py::class_<ConvStackArgs>(m, "ConvStackArgs")
       .def(py::init<>())
       PTR(ConvStackArgs, x) RW(ConvStackArgs, B) RW(ConvStackArgs, n) RW(ConvStackArgs, seed)
-      PTR(ConvStackArgs, st) RW(ConvStackArgs, dbg) RW(ConvStackArgs, off_w) RW(ConvStackArgs, off_codes) RW(ConvStackArgs, lds_bytes)
+      PTR(ConvStackArgs, st) RW(ConvStackArgs, dbg) RW(ConvStackArgs, off_w) RW(ConvStackArgs, off_codes) RW(ConvStackArgs, off_codes2) RW(ConvStackArgs, lds_bytes)
       .def("set_buf_offsets", [](ConvStackArgs& a, int b0, int b1) { a.off_buf[0] = b0; a.off_buf[1] = b1; })
       RW(ConvStackArgs, splits) PTR(ConvStackArgs, ts) RW(ConvStackArgs, off_bias)
       .def("set_rows", [](ConvStackArgs& a, int l, int sp, int c0, int c1, int o0, int o1, int ib, int ih) {
@@ -308,6 +309,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("MAX_STACK") = MAX_STACK;
   m.attr("MAX_STACK_SPLIT") = MAX_STACK_SPLIT;
   m.attr("STACK_THREADS") = conv_stack_threads();
+  m.attr("STACK_TABN") = conv_stack_tabn();
   m.def("conv_stack_fwd", [](const ConvStackArgs& a, uintptr_t s) {
     launch_conv_stack_fwd(a, S(s)); check_last("conv_stack_fwd"); });
   m.def("slab_reduce", [](uintptr_t grad, int lo, int hi, const RedTable& t, uintptr_t s) {

@@ -34,6 +34,7 @@
 // 16 waves would cap the kernel at 128 VGPRs and spill
 #define STACK_THREADS 768
 #define STACK_WAVES (STACK_THREADS / 64)
+#define STACK_TABN 80            // ints per layer's k-offset table (KS <= 18: <= 72 entries)
 #define LDS __attribute__((address_space(3)))
 
 typedef LDS bf16 lbf16;
@@ -361,15 +362,22 @@ __device__ __forceinline__ void stack_layer_tm(const ConvStackArgs& A, const Sta
   stack_layer<NT, TM, CS4>(A, L, b, c0, c1, roff, in, outimg, obase, OH, ol, OW, XPo, codes, wl, tab, zl, step, lb);
 }
 
+// the row-aligned fast path applies (pooled, pooled width % 4 == 0, 3x3; ablations off)
+__device__ __forceinline__ bool stack_rows_ok(const ConvStackArgs& A, const StackLayer& L) {
+  return !(A.dbg & 16) && L.pool && (L.Wp & 3) == 0 && L.KH == 3 && L.KW == 3 && !(A.dbg & 3);
+}
+
 __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const ConvStackArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem_[];
   LDS char* smem = (LDS char*)smem_;
   const int tid = threadIdx.x;
   const int b = blockIdx.x / A.splits, sp = blockIdx.x - b * A.splits;
   lbf16* zl = (lbf16*)smem;                                      // 32 B of zeros
-  LDS int* tab = (LDS int*)(smem + 32);                          // k-chunk -> halo offset
+  LDS int* tab = (LDS int*)(smem + 32);                          // [layer][STACK_TABN] k-chunk -> halo offset
   lbf16* wlds = (lbf16*)(smem + A.off_w);
-  LDS uint8_t* codes = (LDS uint8_t*)(smem + A.off_codes);
+  // two argmax-code planes (layer parity): a layer's epilogue writes its plane while slower
+  // waves may still copy the previous layer's codes out (no barrier between those phases)
+  LDS uint8_t* codes_pl[2] = {(LDS uint8_t*)(smem + A.off_codes), (LDS uint8_t*)(smem + A.off_codes2)};
   const uint32_t step = A.st ? (uint32_t)A.st->t : 0u;
   STACK_STAMP(0);
   if (tid < 8) ((LDS uint32_t*)zl)[tid] = 0u;
@@ -442,6 +450,25 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     }
   }
 
+  // k-chunk -> halo offset tables of every layer (the generic path reads them; the
+  // row-aligned path keeps its tap offsets in registers, but a rows_ok layer without an
+  // instantiated (KS, NT) falls back to the generic path), all computed once here: the
+  // per-layer table phase and its barrier are gone
+  for (int l = 0; l < A.n; ++l) {
+    const StackLayer& L = A.L[l];
+    const int Wi = L.xrow, KHW = L.KH * L.KW, cw = L.Cs_in == 4 ? 4 : 8;
+    const int ntab = L.Cs_in == 4 ? L.KS * 8 : L.KS * 4;
+    for (int c = tid; c < ntab; c += STACK_THREADS) {
+      const int k0 = c * cw, tap = k0 / L.Cs_in;
+      int e = -1;
+      if (tap < KHW) {
+        const int ky = tap / L.KW;
+        e = (ky * Wi + (tap - ky * L.KW)) * L.xpix + (k0 - tap * L.Cs_in);
+      }
+      tab[l * STACK_TABN + c] = e;
+    }
+  }
+
   bf16x8 pf[PF];
   if (prefetch) {
 #pragma unroll
@@ -455,6 +482,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   }
 
   STACK_STAMP(1);
+  __syncthreads();                  // image, layer-0 weights, biases and tables staged
   for (int l = 0; l < A.n; ++l) {
     const StackLayer L = A.L[l];      // by value: one batch of scalar loads per layer instead of
     const bool last = l + 1 == A.n;   // a kernarg reload of every field after each barrier
@@ -477,20 +505,14 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       obase = A.rows[l + 1][sp][4], OH = A.rows[l + 1][sp][5], ol = N.pad_l, OW = N.Wo + N.KW - 1;
       ORS = N.xrow, OPS = N.xpix;
     }
-    if (l == 1 && prefetch) {
-      const int w1 = A.L[1].w_lds, w2 = A.n > 2 ? A.L[2].w_lds : 0, w3 = A.n > 3 ? A.L[3].w_lds : 0;
-#pragma unroll
-      for (int j = 0; j < PF; ++j) {
-        const int v = tid + j * STACK_THREADS;
-        const int e = v < nv1 ? w1 + v * 8 : v < nv1 + nv2 ? w2 + (v - nv1) * 8 : w3 + (v - nv1 - nv2) * 8;
-        if (v < nv1 + nv2 + nv3) *reinterpret_cast<LDS bf16x8*>(wlds + e) = pf[j];
-      }
-    }
+    LDS uint8_t* codes = codes_pl[l & 1];
     {
       LDS bf16x8* z = (LDS bf16x8*)out;
       const bf16x8 zero8 = zero_bf16x8();
       // The epilogue writes every channel of output rows [wr0, wr1) x columns [ol, ol + Wp)
-      // (all channels when Cs_out == Cout); only the rest of the image needs zeros.
+      // (all channels when Cs_out == Cout); only the rest of the image needs zeros -- at
+      // addresses no epilogue store touches, so the zeroing runs beside this layer's tiles
+      // (the barrier after them publishes both).  Otherwise the whole image is zeroed first.
       const int nr = L.pool ? (c1 - c0) >> 1 : c1 - c0;
       const int wr0 = max(0, p0 - obase), wr1 = min(OH, p0 - obase + nr);
       // (in 8-channel vectors of the output layout; pixel padding is zeroed with its pixel,
@@ -511,26 +533,15 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       } else {
         const int nz = OH * nrow;
         for (int i = tid; i < nz; i += STACK_THREADS) z[i] = zero8;
-      }
-      const int Wi = L.xrow, KHW = L.KH * L.KW, cw = L.Cs_in == 4 ? 4 : 8;
-      const int ntab = L.Cs_in == 4 ? L.KS * 8 : L.KS * 4;
-      for (int c = tid; c < ntab; c += STACK_THREADS) {
-        const int k0 = c * cw, tap = k0 / L.Cs_in;
-        int e = -1;
-        if (tap < KHW) {
-          const int ky = tap / L.KW;
-          e = (ky * Wi + (tap - ky * L.KW)) * L.xpix + (k0 - tap * L.Cs_in);
-        }
-        tab[c] = e;
+        __syncthreads();                                    // before any epilogue store
       }
     }
-    __syncthreads();
     STACK_STAMP(2 + 4 * l);
     const lbf16* wl = wlds + L.w_lds;
-#define STACK_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, tab, zl, step, lbias + l * 64
+#define STACK_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, tab + l * STACK_TABN, zl, step, lbias + l * 64
 #define ROWS_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, step, lbias + l * 64, l == A.n - 1
     // row-aligned fast path (pooled, pooled width % 4 == 0, 3x3, instantiated KS), else generic
-    const bool rows_ok = !(A.dbg & 16) && L.pool && (L.Wp & 3) == 0 && L.KH == 3 && L.KW == 3 && !(A.dbg & 3);
+    const bool rows_ok = stack_rows_ok(A, L);
     // TM = 1 when it evens out the waves' tile counts (few tiles per workgroup)
     const int ntl = ((c1 - c0) >> 1) * (L.Wp >> 2);
     const bool tm1 = ntl <= STACK_WAVES || cdiv(ntl, STACK_WAVES) < 2 * cdiv(ntl, 2 * STACK_WAVES);
@@ -565,6 +576,18 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     }
 #undef STACK_ARGS
 #undef ROWS_ARGS
+    if (l == 0 && prefetch) {
+      // the later layers' packs (in registers since the kernel start, their loads hidden
+      // behind layer 0) -> their LDS slots, which layer 0 does not read; the barrier below
+      // publishes them to layer 1
+      const int w1 = A.L[1].w_lds, w2 = A.n > 2 ? A.L[2].w_lds : 0, w3 = A.n > 3 ? A.L[3].w_lds : 0;
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int v = tid + j * STACK_THREADS;
+        const int e = v < nv1 ? w1 + v * 8 : v < nv1 + nv2 ? w2 + (v - nv1) * 8 : w3 + (v - nv1 - nv2) * 8;
+        if (v < nv1 + nv2 + nv3) *reinterpret_cast<LDS bf16x8*>(wlds + e) = pf[j];
+      }
+    }
     STACK_STAMP(3 + 4 * l);
     __syncthreads();
     STACK_STAMP(4 + 4 * l);
@@ -594,6 +617,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
 }
 
 int conv_stack_threads() { return STACK_THREADS; }
+int conv_stack_tabn() { return STACK_TABN; }
 
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s) {
   auto k = conv_stack_fwd_kernel;

@@ -64,7 +64,10 @@ __device__ __forceinline__ void gather_block(const GatherArgs& a, const StepStat
   const float* ys = reinterpret_cast<const float*>(st->data_y);
   const int* perm = reinterpret_cast<const int*>(st->perm);
   const int R = st->data_R, C = st->data_C;
-  const int pos = pos0 + row;
+  // the cursor is clamped BEFORE it indexes the permutation (perm holds data_n entries): a
+  // cursor run past the data set -- a launch replayed on its own, a caller's bad pos --
+  // must not read past the permutation buffer
+  const int pos = min(max(pos0 + row, 0), max(st->data_n - 1, 0));
   int src = (st->use_perm && perm) ? perm[pos] : pos;
   src = min(max(src, 0), st->data_n - 1);
   const int nvec = R / 8;   // 16-byte vectors per row

@@ -3,6 +3,10 @@
 #pragma once
 #include "bwd_through.h"
 
+// a staged X-halo chunk and its LDS element offset
+struct XChunk4 { bf16x4 v; int o; };
+struct XChunk8 { bf16x8 v; int o; };
+
 __device__ __forceinline__ bf16x4 tr_read_h(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, p));
 }
@@ -83,14 +87,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   const int nch_x = R_in * W_in * cpp;              // X-halo chunks per block
   const int nch_y = npb32 * cpr;                    // dY chunks per block
   const FastDiv fcpp(cpp), fwin(W_in), fcpr(cpr), fwo(a.Wo);
-  // LDS element offset of X-halo chunk idx (pixel-major chunks of cw channels)
-  const bool xdense = XP == Cs && XR == W_in;
-  auto xaddr = [&](int idx) -> int {
-    if (xdense) return idx * cw;
-    const int pix = fcpp.div(idx), c = (idx - pix * cpp) * cw;
-    const int r = fwin.div(pix);
-    return (r * XR + (pix - r * W_in)) * XP + c;
-  };
+
   const bool dbg_stage = !(a.dbg & 1);
   // Pooled dY (dP + argmax codes) over whole even blocks: stage each pooled chunk ONCE and
   // expand it into its 2x2 window's pixel rows in LDS (a quarter of the global loads of a
@@ -132,24 +129,42 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   };
 
   // MFMA reduction over the staged block's npix pixels
+  // per-lane pixel offsets within a 32-pixel k-step (the kperm bijection, see below)
+  const int dP0 = ((a.kperm & 1) ? 4 * g : 8 * g) + (i >> 2), dP1 = dP0 + ((a.kperm & 1) ? 16 : 4);
   auto mma_block = [&](const int npix) {
       const int nks = (a.dbg & 2) ? 0 : (npix + 31) >> 5;
+      // Row-aligned fast path (output width % 32 == 0, whole k-steps): a k-step's 32 pixels
+      // lie in ONE output row, so the halo offset is a scalar per k-step plus a per-lane
+      // constant -- no per-step division or clamping (same pixels, same k order).  One MFMA
+      // body for both paths (a second copy doubled the accumulators' AGPRs and halved the
+      // occupancy of the dual kernels).
+      const bool rowal = (a.Wo & 31) == 0 && (npix & 31) == 0 && !(a.kperm & 2);
+      const int la0 = dP0 * s * XP, la1 = dP1 * s * XP;
+      int y = 0, x0 = 0;
       for (int ks = 0; ks < nks; ++ks) {
         // per-lane pixel rows of the two transposed reads (h = 0, 1).  MFMA k index 8g + j
         // stands for pixel 4g + j (j < 4) / 16 + 4g + j - 4 (j >= 4) of the k-step -- the same
         // bijection for both operands, so a 32-lane half reads 8 CONSECUTIVE pixels (the
         // layout's bank-conflict-free pattern) instead of two runs 8 pixels apart
-        const int P0 = ks * 32 + 4 * g + (i >> 2);
-        const int q0 = min(P0, npix - 1), q1 = min(P0 + 16, npix - 1);
-        const int y0 = fwo.div(q0), y1 = fwo.div(q1);
-        const int off0 = ((y0 * s) * XR + (q0 - y0 * a.Wo) * s) * XP;
-        const int off1 = ((y1 * s) * XR + (q1 - y1 * a.Wo) * s) * XP;
+        const int P0 = ks * 32 + dP0;
+        const int P1 = ks * 32 + dP1;
+        int off0, off1;
+        if (rowal) {
+          const int base = __builtin_amdgcn_readfirstlane(((y * s) * XR + x0 * s) * XP);
+          if ((x0 += 32) == a.Wo) { x0 = 0; ++y; }
+          off0 = base + la0, off1 = base + la1;
+        } else {
+          const int q0 = min(P0, npix - 1), q1 = min(P1, npix - 1);
+          const int y0 = fwo.div(q0), y1 = fwo.div(q1);
+          off0 = ((y0 * s) * XR + (q0 - y0 * a.Wo) * s) * XP;
+          off1 = ((y1 * s) * XR + (q1 - y1 * a.Wo) * s) * XP;
+        }
         const bf16* pbrow = dyl + (size_t)P0 * ldb + 4 * (i & 3);
         bf16x8 bfr[NTT], afr[MTW];
   #pragma unroll
         for (int v = 0; v < NTT; ++v) {
           const bf16* pb = pbrow + v * 16;
-          bfr[v] = __builtin_shufflevector(tr_read_h(pb), tr_read_h(pb + 16 * ldb), 0, 1, 2, 3, 4, 5, 6, 7);
+          bfr[v] = __builtin_shufflevector(tr_read_h(pb), tr_read_h(pb + (P1 - P0) * ldb), 0, 1, 2, 3, 4, 5, 6, 7);
         }
   #pragma unroll
         for (int u = 0; u < MTW; ++u) {
@@ -301,24 +316,28 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
           ix = xb0 + (pix - r * W_in);
           return iy >= 0 && ix >= 0 && iy < a.H && ix < a.W;
         };
+        // (the LDS offset rides along with the loaded value: the coordinates are computed
+        // once, in the load, instead of again in the store)
         if (CS4) {
-          staged_copy<8, bf16x4>(
+          staged_copy<8, XChunk4>(
               nch_x, tid, 256,
               [&](int idx) {
                 int c, iy, ix;
                 const bool ok = coords(idx, c, iy, ix);
-                return load_bf16x4_if(ok, xbase + ((size_t)iy * a.W + ix) * 4, xbase);
+                return XChunk4{load_bf16x4_if(ok, xbase + ((size_t)iy * a.W + ix) * 4, xbase),
+                               ((iy - yb) * XR + (ix - xb0)) * XP + c};
               },
-              [&](int idx, const bf16x4& v) { *reinterpret_cast<bf16x4*>(xl + xaddr(idx)) = v; });
+              [&](int, const XChunk4& v) { *reinterpret_cast<bf16x4*>(xl + v.o) = v.v; });
         } else {
-          staged_copy<8, bf16x8>(
+          staged_copy<8, XChunk8>(
               nch_x, tid, 256,
               [&](int idx) {
                 int c, iy, ix;
                 const bool ok = coords(idx, c, iy, ix);
-                return load_bf16x8_if(ok, xbase + ((size_t)iy * a.W + ix) * Cs + c, xbase);
+                return XChunk8{load_bf16x8_if(ok, xbase + ((size_t)iy * a.W + ix) * Cs + c, xbase),
+                               ((iy - yb) * XR + (ix - xb0)) * XP + c};
               },
-              [&](int idx, const bf16x8& v) { *reinterpret_cast<bf16x8*>(xl + xaddr(idx)) = v; });
+              [&](int, const XChunk8& v) { *reinterpret_cast<bf16x8*>(xl + v.o) = v.v; });
         }
       }
       if (dbg_stage && pexp) {   // dY rows from pooled chunks, each loaded once

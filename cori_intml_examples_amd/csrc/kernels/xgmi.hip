@@ -27,6 +27,12 @@ __device__ __forceinline__ unsigned sys_load(const unsigned* p) {
 __device__ __forceinline__ void sys_store(unsigned* p, unsigned v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// first cause wins: a timeout recorded by one workgroup is not overwritten by the abort the
+// rank's other workgroups then observe
+__device__ __forceinline__ void set_err(int* err, int v) {
+  int zero = 0;
+  __hip_atomic_compare_exchange_strong(err, &zero, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Lanes 0..P-1 of wave 0 each raise flag `slot` of rank `lane` to seq.
 __device__ __forceinline__ void signal_all(unsigned* const* flags, int slot, int P, unsigned seq, int fence) {
@@ -59,12 +65,12 @@ __device__ __forceinline__ bool wait_all(const XgmiArgs& a, const unsigned* flag
     while (sys_load(flags + t) < seq) {
       if (sys_load(a.abort_[a.rank])) {
         s_ok = 0;
-        __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        set_err(a.err, 3);
         break;
       }
       if ((long long)(wall_clock64() - t0) > a.timeout_ticks) {
         s_ok = 0;
-        __hip_atomic_store(a.err, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        set_err(a.err, phase);
         for (int j = 0; j < P; ++j) sys_store(a.abort_[j], 1u);
         break;
       }
@@ -136,7 +142,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
     s_seq = a.ctr[w] + 1u;
     // sticky abort (a rank timed out in an earlier launch): touch nothing, keep the counters
     s_abort = sys_load(a.abort_[a.rank]) != 0u;
-    if (s_abort) __hip_atomic_store(a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (s_abort) set_err(a.err, 3);
   }
   __syncthreads();
   if (s_abort) return;

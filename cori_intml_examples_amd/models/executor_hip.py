@@ -881,7 +881,7 @@ class BatchPlan:
         a = K.ConvStackArgs()
         a.x = self.xb.data_ptr()
         a.B, a.n, a.seed, a.st = self.bs, n, ex.seed, ex.state.data_ptr()
-        a.off_w, a.off_codes, a.lds_bytes = off_w, off_codes, lds
+        a.off_w, (a.off_codes, a.off_codes2), a.lds_bytes = off_w, off_codes, lds
         a.off_bias = off_bias
         a.dbg = tune("stack_dbg", 0)
         a.set_buf_offsets(off_b0, off_b1)
@@ -947,15 +947,18 @@ class BatchPlan:
         return [[tuple(r) for r in layer] for layer in rows]
 
     def _stack_layout(self, convs, rows, splits):
-        """LDS byte layout: zeros + k-offset table | all weight packs | two ping-pong halo
-        images | code plane.  None if it exceeds the CU's LDS."""
+        """LDS byte layout: zeros + per-layer k-offset tables | biases | all weight packs | two
+        ping-pong halo images | two code planes.  None if it exceeds the CU's LDS."""
         def a16(v):
             return (v + 15) & ~15
 
         n = len(convs)
         lay = self._stack_img_layouts(convs)
         ntab = max((g.KS * 8 if g.Cs_in == 4 else g.KS * 4) for g in convs)
-        off_bias = 32 + a16(4 * ntab)
+        tabn = self.ex.K.STACK_TABN
+        if ntab > tabn:
+            return None
+        off_bias = 32 + a16(4 * tabn * self.ex.K.MAX_STACK)         # [layer][STACK_TABN] tables
         off_w = off_bias + 4 * 64 * self.ex.K.MAX_STACK      # biases [layer][64] fp32
         w_off, welems = [], 0
         for g in convs:
@@ -974,10 +977,11 @@ class BatchPlan:
         off_b0 = off_w + a16(2 * welems)
         off_b1 = off_b0 + a16(2 * bufs[0])
         off_codes = off_b1 + a16(2 * bufs[1])
-        lds = off_codes + a16(codes)
+        off_codes2 = off_codes + a16(codes)          # two code planes (layer parity)
+        lds = off_codes2 + a16(codes)
         if lds > self.LDS_LIMIT:
             return None
-        return off_w, w_off, off_b0, off_b1, off_codes, lds, off_bias
+        return off_w, w_off, off_b0, off_b1, (off_codes, off_codes2), lds, off_bias
 
     @staticmethod
     def _stack_img_layouts(convs):
@@ -1053,29 +1057,34 @@ class BatchPlan:
         Wo, Ho = a.Wo, a.Ho
         W_in = (Wo - 1) * a.stride + a.KW
         step = 2 if pool else 1
-        if tune("lds_layout", True) and a.Cs_in % 8 == 0:
-            a.xpix = lds_layout.conv_layout(a.Cs_in, W_in, Wo, bool(pool), a.KH, a.KW)
         a.kpipe = int(tune("conv_kpipe", True))
-        XP = a.xpix or a.Cs_in
         gy = cdiv(NT, ntc)
-        # Balanced blocks: the fewest row blocks per image (c) that satisfy the limits, each
-        # cdiv(Ho, c) rows -- not the largest R with a short remainder block.  Measured on
-        # MNIST's 26-row dgrad (co-scheduled with its wgrad): 15 + 11-row blocks 156 us/step,
-        # 13 + 13 125 us; the RPV layers divide evenly and are unchanged.
-        best = step
-        for c in range(1, Ho + 1):
-            R = cdiv(cdiv(Ho, c), step) * step
-            if R * Wo > 512:
-                continue
-            halo = ((R - 1) * a.stride + a.KH) * W_in * XP * 2
-            if halo + KS * ntc * 1024 > 80 * 1024:
-                continue
-            if a.B * cdiv(Ho, R) * gy < want:
-                continue         # too few workgroups: more, smaller blocks
-            best = R
-            break
+
+        def rows(XP):
+            # Balanced blocks: the fewest row blocks per image (c) that satisfy the limits, each
+            # cdiv(Ho, c) rows -- not the largest R with a short remainder block.  Measured on
+            # MNIST's 26-row dgrad (co-scheduled with its wgrad): 15 + 11-row blocks 156 us/step,
+            # 13 + 13 125 us; the RPV layers divide evenly and are unchanged.
+            for c in range(1, Ho + 1):
+                R = cdiv(cdiv(Ho, c), step) * step
+                if R * Wo > 512:
+                    continue
+                halo = ((R - 1) * a.stride + a.KH) * W_in * XP * 2
+                if halo + KS * ntc * 1024 > 80 * 1024:
+                    continue
+                if a.B * cdiv(Ho, R) * gy < want:
+                    continue         # too few workgroups: more, smaller blocks
+                return R
+            return step
+
+        best = rows(a.Cs_in)
+        if tune("lds_layout", True) and a.Cs_in % 8 == 0:
+            # the bank-conflict-free pixel stride, unless its larger halo costs block rows
+            xp = lds_layout.conv_layout(a.Cs_in, W_in, Wo, bool(pool), a.KH, a.KW)
+            if xp != a.Cs_in and rows(xp) >= best:
+                a.xpix = xp
         a.R = best
-        lds = K_lds = self.ex.K.conv_halo_lds_bytes(a, ntc)
+        lds = self.ex.K.conv_halo_lds_bytes(a, ntc)
         if lds > 150 * 1024:
             raise NotImplementedError("conv halo stage too large (%d bytes)" % lds)
         return ntc
@@ -1151,9 +1160,10 @@ class BatchPlan:
                 R = r
                 break
         # LDS layout from the bank-conflict model (pixel / row strides of the X halo, dY rows)
+        a.kperm = int(tune("wgrad_perm", True)) | (0 if tune("wgrad_fast", True) else 2)
         if tune("lds_layout", True):
             a.xpix, a.xrow, a.dyld = lds_layout.wgrad_layout(g.Cs_in, W_in, g.Wo, NTT, g.KH, g.KW, g.stride,
-                                                             a.Ktiles)
+                                                             a.Ktiles, bool(a.kperm & 1))
         XP, XR = (a.xpix or g.Cs_in), (a.xrow or W_in)
         while R > 1 and (((R - 1) * g.stride + g.KH) * XR * XP * 2 > 64 * 1024):
             R -= 1

@@ -45,9 +45,11 @@ def cycles(addrs: Sequence[int], kind: str) -> int:
     return tot
 
 
-def wgrad_pixel(g: int, j: int) -> int:
+def wgrad_pixel(g: int, j: int, perm: bool = True) -> int:
     """Pixel (within a 32-pixel k-step) of MFMA k index 8g + j in the weight-gradient kernel
-    (wgrad_halo_body.h mma_block)."""
+    (wgrad_halo_body.h mma_block; perm=False: the identity, pixel 8g + j)."""
+    if not perm:
+        return 8 * g + j
     return 4 * g + j if j < 4 else 16 + 4 * g + (j - 4)
 
 
@@ -57,7 +59,7 @@ def _taps(KH: int, KW: int) -> List[Tuple[int, int]]:
 
 # ------------------------------------------------------------------ access patterns
 def wgrad_x_cost(Cs: int, xpix: int, xrow: int, Wo: int, KH: int = 3, KW: int = 3,
-                 stride: int = 1, ktiles: int = 3) -> float:
+                 stride: int = 1, ktiles: int = 3, perm: bool = True) -> float:
     """Average cycles of the X-halo (A operand) transposed reads: lane (i, g) reads 4
     channels (8 B) of pixel P(g, (i >> 2) + 4 * sec) shifted by the tap of its k row group."""
     res = []
@@ -67,7 +69,7 @@ def wgrad_x_cost(Cs: int, xpix: int, xrow: int, Wo: int, KH: int = 3, KW: int = 
             addrs = []
             for ln in range(64):
                 i, g = ln & 15, ln >> 4
-                P = wgrad_pixel(g, (i >> 2) + 4 * sec)
+                P = wgrad_pixel(g, (i >> 2) + 4 * sec, perm)
                 k = mt * 16 + 4 * (i & 3)
                 tap = min(k // Cs, KHW - 1)
                 ky, kx = tap // KW, tap % KW
@@ -79,14 +81,14 @@ def wgrad_x_cost(Cs: int, xpix: int, xrow: int, Wo: int, KH: int = 3, KW: int = 
     return sum(res) / len(res)
 
 
-def wgrad_dy_cost(ntt: int, dyld: int) -> float:
+def wgrad_dy_cost(ntt: int, dyld: int, perm: bool = True) -> float:
     """Average cycles of the dY-row (B operand) transposed reads of n-tile 0."""
     res = []
     for sec in (0, 1):
         addrs = []
         for ln in range(64):
             i, g = ln & 15, ln >> 4
-            P = wgrad_pixel(g, (i >> 2) + 4 * sec)
+            P = wgrad_pixel(g, (i >> 2) + 4 * sec, perm)
             addrs.append((P * dyld + 4 * (i & 3)) * 2)
         res.append(cycles(addrs, "tr_b64"))
     return sum(res) / len(res)
@@ -123,7 +125,7 @@ def _cands(base: int, pads: Iterable[int]) -> List[int]:
 
 @functools.lru_cache(maxsize=256)
 def wgrad_layout(Cs: int, W_in: int, Wo: int, ntt: int, KH: int = 3, KW: int = 3, stride: int = 1,
-                 ktiles: int = 3) -> Tuple[int, int, int]:
+                 ktiles: int = 3, perm: bool = True) -> Tuple[int, int, int]:
     """(xpix, xrow, dyld) for wgrad_halo_body: the X-halo pixel / row strides and the dY row
     stride with the fewest modelled LDS cycles (ties: the smallest footprint)."""
     best = None
@@ -131,13 +133,13 @@ def wgrad_layout(Cs: int, W_in: int, Wo: int, ntt: int, KH: int = 3, KW: int = 3
         if (xpix * 2) % 8:
             continue                   # 8-byte aligned pixels (transposed 8-byte reads)
         for xrow in range(W_in, W_in + 17):
-            c = wgrad_x_cost(Cs, xpix, xrow, Wo, KH, KW, stride, ktiles)
+            c = wgrad_x_cost(Cs, xpix, xrow, Wo, KH, KW, stride, ktiles, perm)
             key = (c, xpix * xrow)
             if best is None or key < best[0]:
                 best = (key, xpix, xrow)
     dbest = None
     for dyld in _cands(ntt * 16, (0, 8, 16, 24)):
-        c = wgrad_dy_cost(ntt, dyld)
+        c = wgrad_dy_cost(ntt, dyld, perm)
         if dbest is None or (c, dyld) < dbest[0]:
             dbest = ((c, dyld), dyld)
     return best[1], best[2], dbest[1]
