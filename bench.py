@@ -84,17 +84,13 @@ def build(args, size, dp, dev):
 
 
 def synthetic(n, shape, ncls, ex, dev, g):
+    """The bench's data set, generated on the device by the K16 synth kernel (io/synth.py):
+    RPV-like jet images (binary heads) or MNIST-like class templates (10 classes), in the
+    executor's layout, resident for the whole run."""
     import torch
-    from cori_intml_examples_amd.models.executor_base import DeviceData
-    x = torch.rand((n,) + shape, generator=g, device=dev)
-    xs = torch.zeros(n, shape[0], shape[1], ex.in_Cs, dtype=torch.bfloat16, device=dev)
-    xs[..., :shape[2]] = x.to(torch.bfloat16)
-    del x
-    if ncls == 1:
-        y = (torch.rand(n, 1, generator=g, device=dev) > 0.5).float()
-    else:
-        y = torch.nn.functional.one_hot(torch.randint(0, ncls, (n,), generator=g, device=dev), ncls).float()
-    return DeviceData(xs.reshape(n, -1), y, n)
+    from cori_intml_examples_amd.io import synth
+    seed = int(torch.randint(0, 1 << 31, (1,), generator=g, device=dev).item())
+    return synth.synth_device("rpv" if ncls == 1 else "mnist", n, shape, ncls, ex.in_Cs, seed, dev)
 
 
 def time_steps(model, data, B, steps, warmup, chunk, g, dev):
@@ -299,7 +295,7 @@ class InlineHpo:
                 "wall_s": round(wall, 2), "startup_s": round(self.startup_s, 2),
                 "mean_trial_s": round(sum(r["t1"] - r["t0"] for r in done) / max(1, len(done)), 3),
                 "best_val_loss": best, "budget_s": self.budget_s,
-                "data": "synthetic MNIST (60k), resident per engine; random-init weights"}
+                "data": "synthetic MNIST (60k) generated on each engine GPU by the K16 kernel, resident; random-init weights"}
 
     def stop(self):
         try:
@@ -456,7 +452,7 @@ def main():
                "value": round(value, 1), "unit": "images/s", "n_gpus": size, "steps": steps,
                "warmup": warmup_note, "ms_per_step": round(ms, 4), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": round(value / baseline, 2) if baseline else None,
-               "dtype": "bf16", "data": "synthetic (device-resident, random-init weights)",
+               "dtype": "bf16", "data": "synthetic (RPV-like jets / MNIST-like templates generated on the GPU by the K16 kernel, device-resident; random-init weights)",
                "config": {"model": cfg_name, "global_batch": B * size, "per_gpu_batch": B,
                           "seq_len": None, "input": list(shape),
                           "optimizer": type(getattr(model.optimizer, "_base_optimizer", model.optimizer)).__name__,

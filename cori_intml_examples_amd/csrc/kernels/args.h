@@ -311,3 +311,22 @@ struct XgmiArgs {
   int* err = nullptr;            // phase (1, 2) of a timed-out wait; 3 = a peer aborted
   OptimArgs opt;                 // p / s0 / s1 point at the bucket's first element
 };
+
+// K16 (synth.hip): parameter initialiser over one flat span -- kind 0 zeros, 1 ones,
+// 2 uniform(-scale, scale) from rng_u32(element, seed, stream, 0)
+struct InitArgs {
+  float* p = nullptr;
+  int n = 0, kind = 0;
+  float scale = 0.f;
+  uint32_t seed = 0, stream = 0;
+};
+
+// K16 (synth.hip): synthetic samples [first, first + n) of a data stream -- kind 0 uniform
+// [0, 1) pixels, 1 RPV-like jet images, 2 MNIST-like class templates + noise; x bf16
+// [n][H][W][Cs] (channels >= C zero), y fp32 [n][ncls] (one-hot, or the 0/1 label)
+struct SynthArgs {
+  bf16* x = nullptr;
+  float* y = nullptr;
+  int n = 0, first = 0, H = 0, W = 0, C = 1, Cs = 1, ncls = 1, kind = 0;
+  uint32_t seed = 0;
+};

@@ -18,6 +18,7 @@ void launch_wgrad_tile(const WgradArgs& a, int ntc, hipStream_t s);
 size_t wgrad_tile_lds_bytes(int ntc);
 void launch_wgrad_halo(const WgradArgs& a, int MT, int NTT, int splits, hipStream_t s);
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT);
+int wgrad_halo_resident(const WgradArgs& a, int MT, int NTT, bool bias);
 int head_rows_per_block(bool fused);
 int head_epi_max();
 void launch_wgrad(const WgradArgs& a, int ktw, int ntt, int splits, hipStream_t s);
@@ -37,6 +38,8 @@ void launch_dense_dx(const DenseFwdArgs& a, int ntc, hipStream_t s);
 void launch_dense_bwd_pair(const WgradArgs& wa, int kg, int ntt, int splits, const DenseFwdArgs& da, int ntc,
                            hipStream_t s);
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s);
+void launch_init_params(const InitArgs& a, hipStream_t s);
+void launch_synth(const SynthArgs& a, hipStream_t s);
 int conv_stack_threads();
 int conv_stack_tabn();
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
@@ -156,6 +159,16 @@ PYBIND11_MODULE(_kernels, m) {
         a.L[i] = l;
       });
 
+  py::class_<InitArgs>(m, "InitArgs")
+      .def(py::init<>())
+      PTR(InitArgs, p) RW(InitArgs, n) RW(InitArgs, kind) RW(InitArgs, scale) RW(InitArgs, seed) RW(InitArgs, stream);
+  py::class_<SynthArgs>(m, "SynthArgs")
+      .def(py::init<>())
+      PTR(SynthArgs, x) PTR(SynthArgs, y) RW(SynthArgs, n) RW(SynthArgs, first) RW(SynthArgs, H) RW(SynthArgs, W)
+      RW(SynthArgs, C) RW(SynthArgs, Cs) RW(SynthArgs, ncls) RW(SynthArgs, kind) RW(SynthArgs, seed);
+  m.def("init_params", [](const InitArgs& a, uintptr_t s) { launch_init_params(a, S(s)); check_last("init_params"); });
+  m.def("synth", [](const SynthArgs& a, uintptr_t s) { launch_synth(a, S(s)); check_last("synth"); });
+
   py::class_<PrologueArgs>(m, "PrologueArgs")
       .def(py::init<>())
       RW(PrologueArgs, sb) RW(PrologueArgs, ga) RW(PrologueArgs, gather_gx) RW(PrologueArgs, gather_blocks)
@@ -253,6 +266,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wgrad_lds_bytes", &wgrad_lds_bytes);
   m.def("conv_halo_lds_bytes", &conv_halo_lds_bytes);
   m.def("wgrad_halo_lds_bytes", &wgrad_halo_lds_bytes);
+  m.def("wgrad_halo_resident", &wgrad_halo_resident);
   m.def("head_rows_per_block", &head_rows_per_block, py::arg("fused") = false);
   m.def("conv_tile_lds_bytes", &conv_tile_lds_bytes);
   m.def("conv_tile", [](const ConvMMArgs& a, int ntc, uintptr_t s) {

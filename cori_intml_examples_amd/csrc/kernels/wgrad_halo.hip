@@ -63,3 +63,26 @@ void launch_wgrad_halo(const WgradArgs& a, int MT, int NTT, int splits, hipStrea
   C(1, 1) C(2, 1) C(4, 1) C(1, 2) C(2, 2) C(4, 2) C(1, 4) C(2, 4) C(4, 4) C(1, 8) C(2, 8)
 #undef C
 }
+
+// Workgroups of the (non-pipelined) launch resident at once on the whole device: its
+// occupancy (VGPRs, LDS) x the CU count.  The host sizes the split count to ONE such round
+// -- a grid past it runs a second, mostly empty round (measured on the RPV first layer:
+// 1024 workgroups 16.0 us, 683 workgroups 14.2 us).  0 if the query fails.
+int wgrad_halo_resident(const WgradArgs& a, int MT, int NTT, bool bias) {
+  const bool cs4 = a.Cs_in == 4;
+  const size_t lds = wgrad_halo_lds_bytes(a, MT, NTT);
+  const int mtw = (MT + (bias ? 1 : 0) + 3) / 4;
+  const void* k = nullptr;
+#define C(M_, N_)                                                                               \
+  if (!k && mtw <= M_ && NTT == N_)                                                             \
+    k = cs4 ? (const void*)wgrad_halo_kernel<M_, N_, true, false> : (const void*)wgrad_halo_kernel<M_, N_, false, false>;
+  C(1, 1) C(2, 1) C(4, 1) C(1, 2) C(2, 2) C(4, 2) C(1, 4) C(2, 4) C(4, 4) C(1, 8) C(2, 8)
+#undef C
+  if (!k) return 0;
+  int dev = 0, per_cu = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+  if (lds > 65536) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, lds) != hipSuccess) return 0;
+  return per_cu * prop.multiProcessorCount;
+}

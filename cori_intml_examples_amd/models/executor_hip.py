@@ -1172,7 +1172,9 @@ class BatchPlan:
         groups = cdiv(NT, NTT) * cdiv(a.Ktiles, MT)
         per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
         s_budget = max(1, (8 << 20) // per_split_bytes)
-        cap = tune("wgrad_splits", 1024)
+        # splits: one round of resident workgroups (occupancy x CUs), not more -- the
+        # latency-bound blocks then all stream concurrently instead of a second thin round
+        cap = tune("wgrad_splits", 0) or K.wgrad_halo_resident(a, MT, NTT, bool(bias)) or 768
         S = max(1, min(nblocks, s_budget, max(1, cap // groups)))
         bps = cdiv(nblocks, S)
         S = cdiv(nblocks, bps)

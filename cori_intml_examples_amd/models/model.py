@@ -21,6 +21,7 @@ import torch
 from .. import optim as optimizers
 from ..train import callbacks as cbks
 from ..utils.env import default_device, next_seed
+from .executor_base import DeviceData
 from .layers import Dense, InputLayer, KTensor, Layer
 from .params import ParamStore
 from .plan import build_plan, canonical_loss
@@ -194,7 +195,7 @@ class Model:
     def evaluate(self, x=None, y=None, batch_size=None, verbose=1, sample_weight=None, steps=None):
         self._check_compiled()
         ex = self._executor
-        data = ex.upload(x, y)
+        data = x if isinstance(x, DeviceData) else ex.upload(x, y)
         self._run_eval(data, batch_size or 32)
         loss, acc, _ = ex.read_metrics()
         if verbose:

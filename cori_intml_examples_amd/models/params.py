@@ -70,15 +70,21 @@ class ParamStore:
 
     # -- initialisation (Keras defaults: glorot_uniform kernels, zero biases) -------------
     def initialize(self, seed: int) -> None:
+        """Keras initialisers.  Uniform kinds (glorot / he uniform) and constants run on the
+        counter-based RNG -- the init kernel on a GPU (K16, csrc/kernels/synth.hip), its
+        bit-identical torch twin on the CPU (ops/rng.init_uniform) -- so the same seed gives
+        the same weights on both backends with no host round trip; the parameter index is
+        the RNG stream.  Normal kinds are drawn on the host."""
+        from ..ops import rng
+        on_gpu = self.device.type == "cuda"
+        K = None
+        if on_gpu:
+            from ..ops import hip
+            K = hip.kernels()
         g = torch.Generator().manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
-        host = torch.zeros(self.capacity, dtype=torch.float32)
-        for s in self.specs:
+        host = None
+        for idx, s in enumerate(self.specs):
             init = s.init if isinstance(s.init, str) else "glorot_uniform"
-            if init in ("zeros", "Zeros"):
-                continue
-            if init in ("ones", "Ones"):
-                host[s.offset:s.offset + s.numel] = 1.0
-                continue
             if len(s.shape) == 4:
                 rf = s.shape[0] * s.shape[1]
                 fan_in, fan_out = s.shape[2] * rf, s.shape[3] * rf
@@ -86,18 +92,35 @@ class ParamStore:
                 fan_in, fan_out = s.shape
             else:
                 fan_in = fan_out = s.numel
-            if init in ("glorot_uniform", "VarianceScaling"):
-                lim = math.sqrt(6.0 / (fan_in + fan_out))
-                host[s.offset:s.offset + s.numel] = (torch.rand(s.numel, generator=g) * 2 - 1) * lim
+            kind, scale = None, 0.0
+            if init in ("zeros", "Zeros"):
+                kind = 0
+            elif init in ("ones", "Ones"):
+                kind = 1
+            elif init in ("glorot_uniform", "VarianceScaling"):
+                kind, scale = 2, math.sqrt(6.0 / (fan_in + fan_out))
             elif init == "he_uniform":
-                lim = math.sqrt(6.0 / fan_in)
-                host[s.offset:s.offset + s.numel] = (torch.rand(s.numel, generator=g) * 2 - 1) * lim
+                kind, scale = 2, math.sqrt(6.0 / fan_in)
             elif init == "glorot_normal":
                 std = math.sqrt(2.0 / (fan_in + fan_out))
-                host[s.offset:s.offset + s.numel] = torch.randn(s.numel, generator=g) * std
+                vals = torch.randn(s.numel, generator=g) * std
+                self.master[s.offset:s.offset + s.numel].copy_(vals.to(self.device))
+                continue
             else:
                 raise NotImplementedError("initializer %s" % init)
-        self.master.copy_(host.to(self.device))
+            if on_gpu:
+                a = K.InitArgs()
+                a.p = self.master.data_ptr() + 4 * s.offset
+                a.n, a.kind, a.scale, a.seed, a.stream = s.numel, kind, float(scale), int(seed) & 0xFFFFFFFF, idx
+                K.init_params(a, hip.stream_handle())
+            else:
+                if host is None:
+                    host = self.master.detach()
+                seg = host[s.offset:s.offset + s.numel]
+                if kind == 2:
+                    seg.copy_(rng.init_uniform(s.numel, scale, int(seed), idx))
+                else:
+                    seg.fill_(float(kind))
 
     # -- host I/O --------------------------------------------------------------------------
     def get_weights(self) -> List[np.ndarray]:

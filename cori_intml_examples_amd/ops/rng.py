@@ -53,3 +53,22 @@ def uniform01(numel: int, seed: int, stream: int, step: int = 0, device="cpu") -
     idx = torch.arange(numel, dtype=torch.int64, device=device)
     u = rng_u32(idx, seed, stream, step)
     return (u >> 8).to(torch.float32) * (1.0 / 16777216.0)
+
+
+def u01_of(u: torch.Tensor) -> torch.Tensor:
+    """fp32 in [0, 1) from hash values (int64 holding uint32): (u >> 8) * 2^-24, exact."""
+    return (u >> 8).to(torch.float32) * torch.tensor(2.0 ** -24, dtype=torch.float32)
+
+
+def uint_below(u: torch.Tensor, m: int) -> torch.Tensor:
+    """floor((u >> 8) * m / 2^24): an integer in [0, m) (csrc/kernels/synth.hip uint_below)."""
+    return ((u >> 8) * m) >> 24
+
+
+def init_uniform(numel: int, scale: float, seed: int, stream: int) -> torch.Tensor:
+    """uniform(-scale, scale) of a parameter span: (u01 * 2 - 1) * scale in fp32, each op
+    rounded once -- bit-identical to init_params_kernel (csrc/kernels/synth.hip)."""
+    idx = torch.arange(numel, dtype=torch.int64)
+    u = u01_of(rng_u32(idx, seed & _M32, stream & _M32, 0))
+    return (u * torch.tensor(2.0, dtype=torch.float32) - torch.tensor(1.0, dtype=torch.float32)) * \
+        torch.tensor(scale, dtype=torch.float32)

@@ -23,6 +23,11 @@ from . import callbacks as cbks
 
 
 def _split_validation(x, y, validation_split, validation_data):
+    from ..models.executor_base import DeviceData
+    if isinstance(x, DeviceData) and validation_data is None and validation_split and 0.0 < validation_split < 1.0:
+        from ..io.synth import split
+        tr, va = split(x, validation_split)
+        return tr, None, va, None
     if validation_data is not None:
         if len(validation_data) == 3:
             vx, vy, vw = validation_data
@@ -55,6 +60,7 @@ def shard_indices(n: int, rank: int, size: int, shuffle: bool, seed: int, epoch:
 
 def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_split, validation_data,
              shuffle, initial_epoch):
+    from ..models.executor_base import DeviceData
     from ..parallel import state as dp_state
     ex = model._executor
     x, y, vx, vy = _split_validation(x, y, validation_split, validation_data)
@@ -70,9 +76,10 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
         from ..parallel import dist as _dist
         shard = (dp.rank, dp.size, int(_dist.broadcast_object(int(model._seed) & 0x7FFFFFFF, 0)))
 
-    train = ex.upload(x, y)
+    # (a DeviceData -- e.g. io.synth.for_model, generated on the device -- is used as is)
+    train = x if isinstance(x, DeviceData) else ex.upload(x, y)
     n_local = train.n // shard[1] if shard else train.n
-    val = ex.upload(vx, vy) if vx is not None else None
+    val = vx if isinstance(vx, DeviceData) else (ex.upload(vx, vy) if vx is not None else None)
     do_val = val is not None
 
     model.history = cbks.History()

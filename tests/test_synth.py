@@ -1,0 +1,129 @@
+"""K16: counter-based initialisers and synthetic data sets (csrc/kernels/synth.hip) and their
+CPU twins (ops/rng.init_uniform, io/synth.synth_cpu).
+
+CPU: the twins' statistics (Glorot bounds, label balance, learnable structure) and the
+model-level contract (same seed -> same weights on every backend; DeviceData accepted by
+fit / evaluate).  GPU: the kernels reproduce the twins BIT FOR BIT (bf16 pixels, fp32
+targets and weights).  Reference: the Keras initialisers of rpv.py:42-58 / mnist.py:40-56
+(SURVEY.md §2.7 K16); the data sets stand in for files this image does not have, so parity
+with the reference's data is unpinned.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from cori_intml_examples_amd.apps import zoo
+from cori_intml_examples_amd.io import synth
+from cori_intml_examples_amd.ops import rng
+
+
+def test_init_uniform_twin_bounds_and_determinism():
+    lim = math.sqrt(6.0 / (27 + 16))
+    a = rng.init_uniform(20000, lim, seed=7, stream=3)
+    b = rng.init_uniform(20000, lim, seed=7, stream=3)
+    c = rng.init_uniform(20000, lim, seed=7, stream=4)
+    assert torch.equal(a, b) and not torch.equal(a, c)
+    assert a.dtype == torch.float32
+    assert float(a.abs().max()) <= lim and float(a.min()) < -0.9 * lim and float(a.max()) > 0.9 * lim
+    assert abs(float(a.mean())) < 0.02 * lim
+    assert abs(float(a.var()) - lim * lim / 3) < 0.05 * lim * lim / 3
+
+
+def test_model_init_is_seeded_and_keras_shaped():
+    m1 = zoo.rpv_cnn((16, 16, 3), conv_sizes=[8, 16], fc_sizes=[32], device="cpu")
+    ws = m1.get_weights()
+    for w in ws:
+        if w.ndim == 1:
+            assert not w.any()                        # zero biases
+        else:
+            fi, fo = (w.shape[0] * w.shape[1] * w.shape[2], w.shape[3]) if w.ndim == 4 else w.shape[:2]
+            if w.ndim == 4:
+                fo *= w.shape[0] * w.shape[1]
+            assert np.abs(w).max() <= math.sqrt(6.0 / (fi + fo)) + 1e-7
+
+
+@pytest.mark.parametrize("kind,shape,ncls", [("rpv", (32, 32, 3), 1), ("mnist", (28, 28, 1), 10),
+                                             ("uniform", (8, 8, 2), 1), ("uniform", (8, 8, 1), 5)])
+def test_synth_cpu_shapes_and_determinism(kind, shape, ncls):
+    x, y = synth.synth_cpu(kind, 64, shape, ncls, seed=5)
+    x2, y2 = synth.synth_cpu(kind, 64, shape, ncls, seed=5)
+    assert x.shape == (64,) + shape and y.shape == (64, ncls)
+    assert torch.equal(x, x2) and torch.equal(y, y2)
+    # a shard is the same samples as the slice of the whole stream
+    xs, ys = synth.synth_cpu(kind, 16, shape, ncls, seed=5, first=24)
+    assert torch.equal(xs, x[24:40]) and torch.equal(ys, y[24:40])
+    assert torch.isfinite(x).all() and float(x.min()) >= 0.0
+    if ncls > 1:
+        assert torch.equal(y.sum(1), torch.ones(64))
+
+
+def test_synth_rpv_is_learnable():
+    # signal images carry more, narrower jets: the count of bright pixels separates the classes
+    x, y = synth.synth_cpu("rpv", 512, (32, 32, 1), 1, seed=9)
+    assert 0.35 < float(y.mean()) < 0.65
+    bright = (x > 0.6).float().flatten(1).sum(1)
+    sig, bkg = bright[y[:, 0] > 0.5], bright[y[:, 0] < 0.5]
+    assert float(sig.mean()) != float(bkg.mean())
+    peak = x.flatten(1).max(1).values
+    assert float(peak.min()) > 0.4                      # every image has at least one jet
+
+
+def test_synth_mnist_classes_share_templates():
+    x, y = synth.synth_cpu("mnist", 400, (28, 28, 1), 10, seed=3)
+    cls = y.argmax(1)
+    assert len(set(cls.tolist())) == 10
+    # same-class images correlate more than different-class ones (template + noise)
+    f = x.flatten(1) - x.flatten(1).mean(1, keepdim=True)
+    f = f / f.norm(dim=1, keepdim=True)
+    sim = f @ f.T
+    same = cls[:, None] == cls[None, :]
+    off = ~torch.eye(400, dtype=torch.bool)
+    assert float(sim[same & off].mean()) > float(sim[~same].mean()) + 0.1
+
+
+def test_fit_and_evaluate_accept_device_data():
+    m = zoo.mnist_cnn(4, 8, 16, 0.1, 0.1, optimizer="Adam", lr=1e-3, device="cpu")
+    data = synth.for_model(m, "mnist", 96, seed=2)
+    h = m.fit(data, None, batch_size=32, epochs=1, validation_split=0.25, verbose=0)
+    assert len(h.history["val_loss"]) == 1 and np.isfinite(h.history["loss"][0])
+    ev = m.evaluate(data, None, batch_size=32, verbose=0)
+    assert np.isfinite(ev[0])
+
+
+@pytest.mark.gpu
+def test_init_kernel_matches_cpu_twin():
+    from cori_intml_examples_amd.ops import hip
+    K = hip.kernels()
+    for stream, (n, lim, kind) in enumerate([(1000, 0.37, 2), (4097, 0.011, 2), (33, 0.0, 0), (65, 0.0, 1)]):
+        p = torch.full((n,), 7.0, device="cuda")
+        a = K.InitArgs()
+        a.p, a.n, a.kind, a.scale, a.seed, a.stream = p.data_ptr(), n, kind, lim, 12345, stream
+        K.init_params(a, hip.stream_handle())
+        want = rng.init_uniform(n, lim, 12345, stream) if kind == 2 else torch.full((n,), float(kind))
+        assert torch.equal(p.cpu(), want), (n, kind)
+    # model level: the same seed gives the same weights on the CPU and the GPU executors
+    torch.manual_seed(0)
+    mc = zoo.rpv_cnn((16, 16, 3), conv_sizes=[8, 16], fc_sizes=[32], device="cpu")
+    mg = zoo.rpv_cnn((16, 16, 3), conv_sizes=[8, 16], fc_sizes=[32], device="cuda:0")
+    mg.store.initialize(mc._seed)
+    mc.store.initialize(mc._seed)
+    for a_, b_ in zip(mc.get_weights(), mg.get_weights()):
+        assert np.array_equal(a_, b_)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,shape,ncls,Cs", [("rpv", (64, 64, 3), 1, 4), ("rpv", (64, 64, 1), 1, 4),
+                                                ("mnist", (28, 28, 1), 10, 4), ("uniform", (16, 16, 3), 1, 4),
+                                                ("uniform", (8, 8, 8), 7, 8)])
+def test_synth_kernel_matches_cpu_twin(kind, shape, ncls, Cs):
+    n, first = 96, 1000
+    d = synth.synth_device(kind, n, shape, ncls, Cs, seed=77, device="cuda:0", first=first)
+    torch.cuda.synchronize()
+    v, y = synth.synth_cpu(kind, n, shape, ncls, seed=77, first=first)
+    H, W, C = shape
+    xg = d.x.view(n, H, W, Cs).cpu()
+    assert torch.equal(xg[..., :C], v.to(torch.bfloat16)), (kind, (xg[..., :C].float() - v).abs().max())
+    assert not xg[..., C:].float().any()
+    assert torch.equal(d.y.cpu(), y)
