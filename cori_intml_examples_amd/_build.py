@@ -60,18 +60,29 @@ def build_kernels(verbose=False, jobs=8):
     headers = glob.glob(os.path.join(kdir, "*.h"))
     srcs = sorted(glob.glob(os.path.join(kdir, "*.hip"))) + [os.path.join(kdir, "bindings.cpp")]
     os.makedirs(BUILD, exist_ok=True)
+    # -amdgpu-mfma-vgpr-form: MFMA accumulators in arch VGPRs.  The default AGPR form made the
+    # register allocator rotate accumulators between AGPR sets through VGPR copies at every
+    # loop back-edge (thousands of v_accvgpr_read/write per kernel: ~90 VALU per 40 MFMAs in
+    # wgrad_gl's k loop); the VGPR form has none, and equal or higher occupancy for every
+    # kernel here (conv_gl<8> 2 -> 4 waves/SIMD, conv_halo 2 -> 4, wgrad_gl 2 -> 3).
     flags = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-I" + kdir,
-             "-Wno-unused-result", "-munsafe-fp-atomics"]
+             "-Wno-unused-result", "-munsafe-fp-atomics", "-mllvm", "-amdgpu-mfma-vgpr-form"]
     objs, jobs_list = [], []
+    # a change of the compile flags rebuilds every object (timestamps alone would miss it)
+    stamp = os.path.join(BUILD, "kernel_flags.txt")
+    flag_txt = " ".join(flags)
+    stale_flags = not os.path.exists(stamp) or open(stamp).read() != flag_txt
     for src in srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
-        if _newer(obj, [src] + headers):
+        if stale_flags or _newer(obj, [src] + headers):
             extra = _py_includes() if src.endswith(".cpp") else []
             lang = ["-x", "hip"] if src.endswith(".hip") else []
             jobs_list.append([HIPCC] + flags + extra + lang + ["-c", src, "-o", obj])
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), jobs_list))
+    with open(stamp, "w") as f:
+        f.write(flag_txt)
     out = kernels_so_path()
     if jobs_list or _newer(out, objs):
         _run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", out] + objs, verbose)

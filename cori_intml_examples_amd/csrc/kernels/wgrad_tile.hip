@@ -216,13 +216,20 @@ namespace {
 __device__ __forceinline__ int wg_swz(int R) { return ((R & 3) | (((R >> 3) & 1) << 2)) << 1; }
 }
 
+// ROWAL: 64 % Wo == 0 and Ho*Wo % 64 == 0 (every legacy / wide layer): a stage is whole
+// output rows of ONE image, so each DMA slot's pixel is a lane-constant offset (row, column)
+// from a wave-uniform stage base -- the per-stage address math is a few adds and compares
+// instead of 64-bit multiply chains (PMC: VALU:MFMA 9.6 and ~250 VALU per 40 MFMAs, mostly
+// v_mul_lo / v_mad_u64 at quarter rate, made the generic path VALU-bound).
+template <bool ROWAL>
 __global__ __launch_bounds__(256) void wgrad_gl_kernel(const WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NTC = 8, NW = 4;
   constexpr int ROWB = 256;                       // bytes per pixel row of either image
   constexpr int IMG = WT_PX * ROWB;               // 16 KB
   constexpr int STG = 2 * IMG;                    // A + B per stage
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar branches)
   const int wm = wave & 1, wn = wave >> 1;
   const int k0 = blockIdx.y * WT_MK;
   const int nt0 = blockIdx.z * NTC;
@@ -261,10 +268,48 @@ __global__ __launch_bounds__(256) void wgrad_gl_kernel(const WgradArgs a) {
     pbx[u] = rem - pby[u] * a.Wo;
   }
   const int adv_y = WT_PX / a.Wo, adv_x = WT_PX - (WT_PX / a.Wo) * a.Wo;
+  // ROWAL lane constants: slot u's source offsets from the stage's (image, first row) base
+  int offA[4], rowA[4], offB[4];
+  bool colA[4];
+  long long sp = p_begin;                         // stage's first pixel (wave-uniform)
+  int sb = 0, sy = 0;                             // its image and output row
+  if (ROWAL) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int R = 16 * wave + 4 * u + g;
+      const int dyl = R / a.Wo, xl = R - dyl * a.Wo;
+      rowA[u] = dyl * s - a.pad_t + tky[u];
+      const int ix = xl * s - a.pad_l + tkx[u];
+      colA[u] = tok[u] && ix >= 0 && ix < a.W;
+      offA[u] = (rowA[u] * a.W + ix) * Cs + tch[u];
+      offB[u] = R * a.Cs_dy + bn[u];
+    }
+    sb = (int)(p_begin / hw);
+    sy = (int)(p_begin - (long long)sb * hw) / a.Wo;
+  }
 
   auto issue = [&](int buf) {
     char* as_ = smem + buf * STG;
     char* bs_ = as_ + IMG;
+    if (ROWAL) {
+      const int left = (int)min((long long)WT_PX, p_end - sp);      // valid pixels of the stage
+      const bf16* xb = a.x + ((size_t)sb * a.H + (size_t)sy * s) * a.W * Cs;
+      const bf16* yb = a.dy + (size_t)sp * a.Cs_dy;
+      const int ys = sy * s;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int R = 16 * wave + 4 * u + g;
+        const int iy = ys + rowA[u];
+        const bool ok = R < left && colA[u] && iy >= 0 && iy < a.H;
+        __builtin_amdgcn_global_load_lds(ok ? xb + offA[u] : zero, as_ + (16 * wave + 4 * u) * ROWB, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(R < left && bok[u] ? yb + offB[u] : zero, bs_ + (16 * wave + 4 * u) * ROWB,
+                                         16, 0, 0);
+      }
+      sp += WT_PX;
+      sy += adv_y;
+      if (sy >= a.Ho) { sy -= a.Ho; ++sb; }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const bool pv = pb_[u] < p_end;
@@ -367,8 +412,11 @@ static void launch_wt(const WgradArgs& a, hipStream_t s) {
   const int S = (int)((P + a.px_per_split - 1) / a.px_per_split);
   const int gy = (a.Ktiles * 16 + WT_MK - 1) / WT_MK;
   const int gz = (a.NT + NTC - 1) / NTC;
-  if (NTC == 8 && a.zero != nullptr && a.dy_code == nullptr)
-    hipLaunchKernelGGL(wgrad_gl_kernel, dim3(S, gy, gz), dim3(256), wgrad_gl_lds_bytes(), s, a);
+  if (NTC == 8 && a.zero != nullptr && a.dy_code == nullptr) {
+    const bool rowal = a.Wo > 0 && WT_PX % a.Wo == 0 && (a.Ho * a.Wo) % WT_PX == 0 && a.px_per_split % WT_PX == 0;
+    if (rowal) hipLaunchKernelGGL(wgrad_gl_kernel<true>, dim3(S, gy, gz), dim3(256), wgrad_gl_lds_bytes(), s, a);
+    else hipLaunchKernelGGL(wgrad_gl_kernel<false>, dim3(S, gy, gz), dim3(256), wgrad_gl_lds_bytes(), s, a);
+  }
   else
     hipLaunchKernelGGL(wgrad_tile_kernel<NTC>, dim3(S, gy, gz), dim3(256), wgrad_tile_lds_bytes(NTC), s, a);
 }

@@ -8,7 +8,7 @@ import csv
 import sys
 from collections import defaultdict
 
-KEEP = ("conv_stack", "dual_halo", "wgrad_halo", "reduce_optim", "dense_", "head_kernel", "prologue",
+KEEP = ("conv_stack", "conv_gl", "wgrad_gl", "dense_lds", "dual_halo", "wgrad_halo", "reduce_optim", "dense_", "head_kernel", "prologue",
         "conv_halo", "wgrad_tile", "conv_tile", "optim_kernel", "slab_reduce", "xgmi", "dense_wgrad", "dense_dx")
 
 
