@@ -26,7 +26,9 @@ def cluster():
     cl.stop()
 
 
-def _square(x):
+def _square(x, hold=0.0):
+    import time
+    time.sleep(hold)          # long enough that one engine cannot drain the queue alone
     print("square of", x)
     return x * x
 
@@ -43,7 +45,7 @@ def test_ids_and_load_balanced(cluster):
     _, c = cluster
     assert c.ids == [0, 1]
     lv = c.load_balanced_view()
-    ars = [lv.apply(_square, i) for i in range(8)]
+    ars = [lv.apply(_square, i, 0.3) for i in range(8)]
     assert [a.get(30) for a in ars] == [i * i for i in range(8)]
     assert {a.engine_id for a in ars} == {0, 1}          # both engines got work
     a = ars[3]
