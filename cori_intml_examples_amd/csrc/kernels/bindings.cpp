@@ -12,7 +12,8 @@ namespace py = pybind11;
 
 void launch_conv_halo(const ConvMMArgs& a, int ntc, hipStream_t s);
 size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc);
-void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s);
+void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s, bool big);
+long long conv_tile_big_blocks(const ConvMMArgs& a, int ntc);
 size_t conv_tile_lds_bytes(int ntc);
 void launch_wgrad_tile(const WgradArgs& a, int ntc, hipStream_t s);
 size_t wgrad_tile_lds_bytes(int ntc);
@@ -269,8 +270,10 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wgrad_halo_resident", &wgrad_halo_resident);
   m.def("head_rows_per_block", &head_rows_per_block, py::arg("fused") = false);
   m.def("conv_tile_lds_bytes", &conv_tile_lds_bytes);
-  m.def("conv_tile", [](const ConvMMArgs& a, int ntc, uintptr_t s) {
-    launch_conv_tile(a, ntc, S(s)); check_last("conv_tile"); });
+  m.def("conv_tile", [](const ConvMMArgs& a, int ntc, uintptr_t s, bool big) {
+    launch_conv_tile(a, ntc, S(s), big); check_last("conv_tile"); }, py::arg("a"), py::arg("ntc"), py::arg("s"),
+    py::arg("big") = false);
+  m.def("conv_tile_big_blocks", &conv_tile_big_blocks);
   m.def("wgrad_tile_lds_bytes", &wgrad_tile_lds_bytes);
   m.def("wgrad_tile", [](const WgradArgs& a, int ntc, uintptr_t s) {
     launch_wgrad_tile(a, ntc, S(s)); check_last("wgrad_tile"); });

@@ -138,12 +138,13 @@ struct Walker {
 };
 
 // Shared epilogue: per wave [16 rows][NW*16] through LDS scratch, 16-byte global stores.
-template <int NTC>
+// WM: 64-row wave groups of the block (2: 128-row blocks of 4 waves, 4: 256-row blocks of 8)
+template <int NTC, int WM = 2>
 __device__ __forceinline__ void tile_epilogue(const ConvMMArgs& a, const TileRows& tr, f32x4 (&acc)[4][NTC / 2],
                                               char* smem, long long row0, int nt0, uint32_t step) {
   constexpr int NW = NTC / 2;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave % WM, wn = wave / WM;
   const long long nrows = tr.nrows;
   const int LDC = NW * 16;
   float* ep = reinterpret_cast<float*>(smem) + wave * 16 * LDC;
@@ -248,21 +249,33 @@ constexpr int GL_NBUF = 4;
 constexpr int GL_DIST = GL_NBUF - 1;
 }
 
-template <int NTC>
-__global__ __launch_bounds__(256) void conv_gl_kernel(const ConvMMArgs a) {
-  static_assert(NTC % 4 == 0, "uniform per-wave DMA count needs NTC % 4 == 0");
+// NWV waves per block: 4 (128 rows, the 2 x 2 wave grid) or 8 (256 rows, 4 x 2): the larger
+// block halves the L2 traffic of the weight operand per MFMA, and with NTC = 16 (all 256
+// output channels of a wide layer) the activation taps are fetched once instead of per
+// 128-channel half.  PMC: the 128 x 128 form moved ~1.1 GB through L2 per launch (~11 TB/s,
+// ~20 % MFMA busy); halving that traffic bought only 1-10 % per legacy launch (conv2 fwd
+// 133.8 -> 131.7 us, strided dgrad 85.5 -> 75.8 us; a 5-deep ring: equal): the per-CU
+// LDS-DMA rate of the row-gathered A operand (~7.5 B/clk/CU here), not L2 bandwidth, bounds it.
+template <int NTC, int NWV, int NBUF = GL_NBUF>
+__global__ __launch_bounds__(64 * NWV) void conv_gl_kernel(const ConvMMArgs a) {
+  constexpr int DIST = NBUF - 1;
+  static_assert(NTC % NWV == 0, "uniform per-wave DMA count needs NTC % NWV == 0");
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BMB = 32 * NWV;                        // rows per block (2 DMA slots of 16 per wave)
+  constexpr int WM = BMB / 64;                         // 64-row wave groups
   constexpr int NW = NTC / 2;
-  constexpr int A_BYTES = BM * 64;
+  static_assert(NWV / WM == 2, "two n-groups of waves");
+  constexpr int A_BYTES = BMB * 64;
   constexpr int STEP_BYTES = A_BYTES + NTC * 1024;
-  constexpr int PER_STEP = 2 + NTC / 4;               // DMA instructions per wave per k-step
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
-  const int wm = wave & 1, wn = wave >> 1;
+  constexpr int PER_STEP = 2 + NTC / NWV;              // DMA instructions per wave per k-step
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
   const int nt0 = blockIdx.y * NTC;
   TileRows tr;
   TapLattice tl;
   tile_geometry(a, tr, tl);
-  const long long row0 = (long long)blockIdx.x * BM;
+  const long long row0 = (long long)blockIdx.x * BMB;
   if (row0 >= tr.nrows) return;                       // (parity classes differ in size)
   const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
   const int KS = tl.KS;
@@ -276,7 +289,7 @@ __global__ __launch_bounds__(256) void conv_gl_kernel(const ConvMMArgs a) {
 
   // issue k-step k (the walker's current position) into ring slot k % GL_NBUF
   auto issue = [&](int k) {
-    char* sb = smem + (k % GL_NBUF) * STEP_BYTES;
+    char* sb = smem + (k % NBUF) * STEP_BYTES;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const bf16* src = wk.okr[u] ? wk.rowp[u] + wk.wcs * 32 : zero;
@@ -284,8 +297,8 @@ __global__ __launch_bounds__(256) void conv_gl_kernel(const ConvMMArgs a) {
     }
     const int kp = wk.pack_ks(a, tl);
 #pragma unroll
-    for (int j = 0; j < NTC / 4; ++j) {              // fragment n = wave + 4j
-      const int n = wave + 4 * j;
+    for (int j = 0; j < NTC / NWV; ++j) {            // fragment n = wave + NWV j
+      const int n = wave + NWV * j;
       const int nt = min(nt0 + n, a.NT - 1);         // clamped: columns past N are dropped
       __builtin_amdgcn_global_load_lds(a.wpk + ((size_t)(kp * a.NT + nt) * 64 + lane) * 8,
                                        sb + A_BYTES + n * 1024, 16, 0, 0);
@@ -302,18 +315,19 @@ __global__ __launch_bounds__(256) void conv_gl_kernel(const ConvMMArgs a) {
 
   if (KS > 0) wk.set_tap(a, tl);
 #pragma unroll
-  for (int k = 0; k < GL_DIST; ++k)
+  for (int k = 0; k < DIST; ++k)
     if (k < KS) issue(k);
   for (int st = 0; st < KS; ++st) {
     // own DMA of stage st retired: later stages issued so far = min(GL_DIST-1, KS-1-st)
-    const int later = min(GL_DIST - 1, KS - 1 - st);
-    if (later >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PER_STEP) : "memory");
+    const int later = min(DIST - 1, KS - 1 - st);
+    if (later >= 3 && DIST >= 4) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * PER_STEP) : "memory");
+    else if (later >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PER_STEP) : "memory");
     else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PER_STEP) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (st + GL_DIST < KS) issue(st + GL_DIST);        // slot of stage st-1: free after the barrier
-    const char* A = smem + (st % GL_NBUF) * STEP_BYTES;
+    if (st + DIST < KS) issue(st + DIST);        // slot of stage st-1: free after the barrier
+    const char* A = smem + (st % NBUF) * STEP_BYTES;
     const char* Bb = A + A_BYTES;
     bf16x8 af[4], bfr[NW];
 #pragma unroll
@@ -328,7 +342,7 @@ __global__ __launch_bounds__(256) void conv_gl_kernel(const ConvMMArgs a) {
       for (int n = 0; n < NW; ++n) acc[t][n] = mfma16(af[t], bfr[n], acc[t][n]);
   }
   __syncthreads();                                    // ring reads done before epilogue scratch reuse
-  tile_epilogue<NTC>(a, tr, acc, smem, row0, nt0, step);
+  tile_epilogue<NTC, WM>(a, tr, acc, smem, row0, nt0, step);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -451,9 +465,10 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(const ConvMMArgs a) {
 
 static size_t epilogue_bytes(int ntc) { return (size_t)4 * 16 * (ntc / 2) * 16 * 4; }
 
-static size_t gl_lds_bytes(int ntc) {
-  const size_t stage = (size_t)GL_NBUF * (BM * 64 + ntc * 1024);
-  return stage > epilogue_bytes(ntc) ? stage : epilogue_bytes(ntc);
+static size_t gl_lds_bytes(int ntc, int nwv = 4, int nbuf = GL_NBUF) {
+  const size_t stage = (size_t)nbuf * (32 * nwv * 64 + ntc * 1024);
+  const size_t ep = epilogue_bytes(ntc) * nwv / 4;
+  return stage > ep ? stage : ep;
 }
 
 size_t conv_tile_lds_bytes(int ntc) {
@@ -463,28 +478,54 @@ size_t conv_tile_lds_bytes(int ntc) {
   return reg > gl ? reg : gl;
 }
 
-template <int NTC>
-static void launch_t(const ConvMMArgs& a, hipStream_t s) {
+static long long tile_maxrows(const ConvMMArgs& a) {
   const bool pool = a.mode == 0 && a.pool;
   const long long nrows = pool ? (long long)a.B * a.Hp * a.Wp * 4 : (long long)a.B * a.Ho * a.Wo;
   const int d = a.in_dil > 1 ? a.in_dil : 1;
-  const long long maxrows = pool ? nrows : (long long)a.B * ((a.Ho + d - 1) / d) * ((a.Wo + d - 1) / d);
-  const int gx = (int)((maxrows + BM - 1) / BM);
+  return pool ? nrows : (long long)a.B * ((a.Ho + d - 1) / d) * ((a.Wo + d - 1) / d);
+}
+
+template <int NTC, int NWV, int NBUF = GL_NBUF>
+static void launch_gl(const ConvMMArgs& a, hipStream_t s) {
+  const int d = a.in_dil > 1 ? a.in_dil : 1;
+  const int gx = (int)((tile_maxrows(a) + 32 * NWV - 1) / (32 * NWV));
+  const int gy = (a.NT + NTC - 1) / NTC;
+  auto k = conv_gl_kernel<NTC, NWV, NBUF>;
+  const size_t lds = gl_lds_bytes(NTC, NWV, NBUF);
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k, dim3(gx, gy, d * d), dim3(64 * NWV), lds, s, a);
+}
+
+template <int NTC>
+static void launch_t(const ConvMMArgs& a, hipStream_t s) {
+  const int d = a.in_dil > 1 ? a.in_dil : 1;
+  const int gx = (int)((tile_maxrows(a) + BM - 1) / BM);
   const int gy = (a.NT + NTC - 1) / NTC;
   if constexpr (NTC % 4 == 0) {
     if (a.in_code == nullptr && a.zero != nullptr) {
-      hipLaunchKernelGGL(conv_gl_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), gl_lds_bytes(NTC), s, a);
+      launch_gl<NTC, 4>(a, s);
       return;
     }
   }
   hipLaunchKernelGGL(conv_tile_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), conv_tile_lds_bytes(NTC), s, a);
 }
 
-void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s) {
+// ntc: n-tiles per block; big: 256-row blocks of 8 waves (LDS-DMA path only; the host picks
+// it when the grid still has >= 512 blocks)
+void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s, bool big) {
+  const bool gl = a.in_code == nullptr && a.zero != nullptr;
+  if (big && gl && ntc == 16) { launch_gl<16, 8>(a, s); return; }   // (a 5-deep ring measured equal)
+  if (big && gl && ntc == 8) { launch_gl<8, 8>(a, s); return; }
   switch (ntc) {
     case 2: launch_t<2>(a, s); break;
     case 4: launch_t<4>(a, s); break;
     case 8: launch_t<8>(a, s); break;
     default: break;
   }
+}
+
+// blocks of the big-tile launch for (ntc) -- the host's grid-size rule
+long long conv_tile_big_blocks(const ConvMMArgs& a, int ntc) {
+  const int d = a.in_dil > 1 ? a.in_dil : 1;
+  return ((tile_maxrows(a) + 255) / 256) * ((a.NT + ntc - 1) / ntc) * d * d;
 }

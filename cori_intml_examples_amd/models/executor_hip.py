@@ -591,6 +591,11 @@ class BatchPlan(GeometryMixin):
         pa.gather_gx = 1 if ga.skip_x else K.gather_gx(ga.R)
         pa.gather_blocks = pa.gather_gx * bs
         pa.pack_mode = 1 if training else 2
+        pro_dbg = tune("pro_dbg", 0)          # timing ablation only: 1 no re-pack, 2 no gather
+        if pro_dbg == 1:
+            pa.pack_mode = 0
+        elif pro_dbg == 2:
+            pa.gather_blocks = 0
         pa.master = store.master.data_ptr()
         pa.arena = ex.arena.data_ptr()
         self.launches.append(("prologue", lambda s, a=pa: K.prologue(a, ex.pack_table, s)))

@@ -192,9 +192,17 @@ class GeometryMixin:
             ntc = 8 if NT > 4 else (4 if NT > 2 else 2)
             if K.conv_tile_lds_bytes(ntc) > 150 * 1024:
                 raise NotImplementedError("conv tile LDS")
+            big = False
             if tune("conv_glds", True):
                 a.zero = self._zero_buf().data_ptr()
-            return lambda s, a=a, n=ntc: K.conv_tile(a, n, s)
+                # 256-row / 8-wave blocks (all 256 channels of a wide layer per block: NTC 16)
+                # when the grid keeps >= 512 blocks: half the L2 traffic per MFMA
+                if tune("conv_big", True) and a.in_code == 0:
+                    for nb in ((16, 8) if NT >= 16 else (8,)):
+                        if NT >= nb and K.conv_tile_big_blocks(a, nb) >= tune("conv_big_min", 512):
+                            ntc, big = nb, True
+                            break
+            return lambda s, a=a, n=ntc, b=big: K.conv_tile(a, n, s, b)
         ntc = self._halo_cfg(a, NT, pool)
         return lambda s, a=a, n=ntc: K.conv_halo(a, n, s)
 

@@ -20,7 +20,12 @@ os.environ["INTML_GRAPHS"] = "0"
 
 def build(model, B, dev):
     from cori_intml_examples_amd.apps import zoo
-    if model == "mnist":
+    if model == "legacy":
+        m = zoo.rpv_legacy_cnn((64, 64, 1), device=dev)
+        shape = (64, 64, 1)
+        rs = np.random.RandomState(0)
+        y = (rs.rand(B * 4) > 0.5).astype(np.float32)
+    elif model == "mnist":
         m = zoo.mnist_cnn(32, 64, 128, 0.25, 0.5, lr=1.0, device=dev)
         shape = (28, 28, 1)
         rs = np.random.RandomState(0)

@@ -172,3 +172,13 @@ def test_dense_and_head(kind, drop, cin, hw, n):
     gw = m.store.view(hd.dense, "kernel", grad=True).cpu()
     assert _rel(gw, a.t() @ dz) < 5e-3
     assert _rel(m.store.view(hd.dense, "bias", grad=True).cpu(), dz.sum(0)) < 5e-3
+
+
+@pytest.mark.parametrize("kind,drop,cin", [("wide", 0.2, 3), ("wide_strided", 0.0, 3)])
+def test_wide_convs_on_big_tiles(kind, drop, cin, monkeypatch):
+    """The 256-row / 8-wave LDS-DMA conv blocks (conv_gl_kernel<NTC, 8>), which the legacy
+    bench shapes take on grid size alone, forced onto the small wide cases: forward, dgrad
+    (plain and input-dilated) and the pooled epilogue against the fp32 reference."""
+    monkeypatch.setenv("INTML_TUNE", "conv_big_min=1")
+    test_conv_forward(kind, drop, cin, 16, 40)
+    test_conv_dgrad_bwd_through(kind, drop, cin, 16, 40)
