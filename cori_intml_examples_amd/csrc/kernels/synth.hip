@@ -16,7 +16,7 @@
 namespace {
 
 constexpr uint32_t S_LAB = 1, S_NJ = 2, S_CY = 3, S_CX = 4, S_AMP = 5, S_CH = 6, S_NOISE = 7, S_TPL = 8,
-                   S_MCLS = 9, S_MNOISE = 10;
+                   S_MCLS = 9, S_MNOISE = 10, S_SHIFT = 11;
 constexpr int RPV_JETS = 6;
 
 __device__ __forceinline__ float u01(uint32_t u) { return (float)(u >> 8) * 5.9604644775390625e-8f; }
@@ -67,6 +67,10 @@ __global__ __launch_bounds__(256) void synth_kernel(const SynthArgs a) {
     }
   } else if (a.kind == 2) {
     cls = uint_below(rng_u32(i, a.seed, S_MCLS, 0u), a.ncls);
+    // per-sample translation of the class template by -3..3 pixels in y and x (wrapping)
+    const uint32_t us = rng_u32(i, a.seed, S_SHIFT, 0u);
+    jy[0] = uint_below(us, 7) - 3;
+    jx[0] = (int)((us & 0xFFu) % 7u) - 3;
   } else {
     cls = a.ncls == 1 ? (u01(rng_u32(i, a.seed, S_LAB, 0u)) < 0.5f ? 1 : 0)
                       : uint_below(rng_u32(i, a.seed, S_LAB, 0u), a.ncls);
@@ -92,8 +96,9 @@ __global__ __launch_bounds__(256) void synth_kernel(const SynthArgs a) {
           auto tpl = [&](int yy, int xx) -> float {
             return (rng_u32(tb + (uint32_t)(yy * a.W + xx), a.seed, S_TPL, 0u) >> 8) >= 11744051u ? 1.f : 0.f;
           };
-          const float sm = ((tpl(y, x) + tpl((y + a.H - 1) % a.H, x)) + tpl(y, (x + a.W - 1) % a.W)) * (1.f / 3.f);
-          v = sm + 0.35f * (2.f * u01(rng_u32(pix, a.seed, S_MNOISE, 0u)) - 1.f);
+          const int ty = (y - jy[0] + 2 * a.H) % a.H, tx = (x - jx[0] + 2 * a.W) % a.W;
+          const float sm = ((tpl(ty, tx) + tpl((ty + a.H - 1) % a.H, tx)) + tpl(ty, (tx + a.W - 1) % a.W)) * (1.f / 3.f);
+          v = sm + 0.5f * (2.f * u01(rng_u32(pix, a.seed, S_MNOISE, 0u)) - 1.f);
           v = fminf(fmaxf(v, 0.f), 1.f);
         } else {
           v = u01(rng_u32(pix, a.seed, S_NOISE, 0u));

@@ -13,7 +13,8 @@ Kinds (the reference trains on RPV HDF5 files / MNIST downloads this image does 
 * ``rpv`` -- calorimeter-like images: 2-3 wide "jets" (background) or 4-6 narrow ones
   (signal, label 1) as separable quadratic bumps on uniform noise (cf. io/datasets.synthetic_rpv);
 * ``mnist`` -- 10 class templates (thresholded hash, smoothed with the pixels above and to
-  the left) plus uniform noise, clipped to [0, 1] (cf. io/datasets.synthetic_mnist).
+  the left), translated by -3..3 pixels per sample, plus uniform noise of amplitude 0.5,
+  clipped to [0, 1] (cf. io/datasets.synthetic_mnist).
 """
 from __future__ import annotations
 
@@ -25,7 +26,7 @@ import torch
 from ..ops.rng import rng_u32, u01_of, uint_below
 
 KINDS = {"uniform": 0, "rpv": 1, "mnist": 2}
-S_LAB, S_NJ, S_CY, S_CX, S_AMP, S_CH, S_NOISE, S_TPL, S_MCLS, S_MNOISE = range(1, 11)
+S_LAB, S_NJ, S_CY, S_CX, S_AMP, S_CH, S_NOISE, S_TPL, S_MCLS, S_MNOISE, S_SHIFT = range(1, 12)
 _M32 = 0xFFFFFFFF
 RPV_JETS = 6
 
@@ -79,8 +80,13 @@ def synth_cpu(kind: str, n: int, shape: Tuple[int, int, int], ncls: int, seed: i
         t = torch.arange(ncls * H * W, dtype=torch.int64)
         tpl = ((rng_u32(t, seed, S_TPL, 0) >> 8) >= 11744051).to(torch.float32).view(ncls, H, W)
         sm = ((tpl + torch.roll(tpl, 1, 1)) + torch.roll(tpl, 1, 2)) * (_f(1.0) / _f(3.0))
-        noise = _f(0.35) * (_f(2.0) * u01_of(rng_u32(pix, seed, S_MNOISE, 0)) - _f(1.0))
-        v = torch.clamp(sm[cls][..., None] + noise, 0.0, 1.0)
+        us = rng_u32(i, seed, S_SHIFT, 0)
+        sy, sx = uint_below(us, 7) - 3, (us & 0xFF) % 7 - 3             # per-sample translation
+        ty = (yy[None, :] - sy[:, None]) % H                             # [n, H]
+        tx = (xx[None, :] - sx[:, None]) % W                             # [n, W]
+        img = sm[cls[:, None, None], ty[:, :, None], tx[:, None, :]]     # [n, H, W]
+        noise = _f(0.5) * (_f(2.0) * u01_of(rng_u32(pix, seed, S_MNOISE, 0)) - _f(1.0))
+        v = torch.clamp(img[..., None] + noise, 0.0, 1.0)
     else:
         ul = rng_u32(i, seed, S_LAB, 0)
         cls = (u01_of(ul) < _f(0.5)).to(torch.int64) if ncls == 1 else uint_below(ul, ncls)
