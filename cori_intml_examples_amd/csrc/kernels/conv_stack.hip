@@ -367,6 +367,15 @@ __device__ __forceinline__ bool stack_rows_ok(const ConvStackArgs& A, const Stac
   return !(A.dbg & 16) && L.pool && (L.Wp & 3) == 0 && L.KH == 3 && L.KW == 3 && !(A.dbg & 3);
 }
 
+// 16 B per lane global -> LDS (M0 + 16 * lane), outside the compiler's wait tracking: the
+// caller waits for it itself (s_waitcnt vmcnt(0)) before any LDS read of the destination.
+// `ldst` must be wave-uniform.
+__device__ __forceinline__ void dma16_untracked(const bf16* gsrc, LDS char* ldst) {
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+               :: "s"(m0v), "v"(gsrc) : "memory", "m0");
+}
+
 __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const ConvStackArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem_[];
   LDS char* smem = (LDS char*)smem_;
@@ -469,20 +478,35 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     }
   }
 
-  bf16x8 pf[PF];
-  if (prefetch) {
-#pragma unroll
-    for (int j = 0; j < PF; ++j) {
-      const int v = tid + j * STACK_THREADS;
-      const bf16* src = v < nv1 ? A.L[1].wpk + (size_t)v * 8
-                      : v < nv1 + nv2 ? A.L[2].wpk + (size_t)(v - nv1) * 8
-                      : A.L[A.n > 3 ? 3 : 1].wpk + (size_t)(v < nv1 + nv2 + nv3 ? v - nv1 - nv2 : 0) * 8;
-      pf[j] = load_bf16x8_if(v < nv1 + nv2 + nv3, src, A.L[1].wpk);
-    }
-  }
-
   STACK_STAMP(1);
   __syncthreads();                  // image, layer-0 weights, biases and tables staged
+
+  // The later layers' weight packs -> their LDS slots by LDS-DMA, issued AFTER that barrier
+  // so they land during layer 0's tiles: the slots (contiguous, layer 1 first) are not read
+  // by layer 0; an explicit vmcnt(0) before layer 0's closing barrier publishes them to
+  // layer 1.  The DMA is issued from inline asm: as a builtin the compiler's wait tracking
+  // treats it as an LDS store that every later ds_read may alias and puts a vmcnt(0) in
+  // front of layer 0's first LDS read (serialising it); register prefetch serialised too
+  // (a select on the loaded value waited at once; the live registers spilled).
+  // (the DMA source addresses stay live until that wait: overwriting the VGPRs of an
+  // outstanding load's address made the compiler wait for it right away)
+  const bf16* dma_src[PF];
+  if (prefetch) {
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int ntot = nv1 + nv2 + nv3;                 // multiples of 64 vectors per layer
+    LDS char* wdst = (LDS char*)(wlds + A.L[1].w_lds);
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {                  // wave-uniform 64-vector chunks
+      const int vb = wave * 64 + j * STACK_THREADS;
+      if (vb >= ntot) break;
+      const int v = vb + lane;
+      const bf16* src = v < nv1 ? A.L[1].wpk + (size_t)v * 8
+                      : v < nv1 + nv2 ? A.L[2].wpk + (size_t)(v - nv1) * 8
+                      : A.L[3].wpk + (size_t)(v - nv1 - nv2) * 8;
+      dma_src[j] = src;
+      dma16_untracked(src, wdst + (size_t)vb * 16);
+    }
+  }
   for (int l = 0; l < A.n; ++l) {
     const StackLayer L = A.L[l];      // by value: one batch of scalar loads per layer instead of
     const bool last = l + 1 == A.n;   // a kernarg reload of every field after each barrier
@@ -576,19 +600,12 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     }
 #undef STACK_ARGS
 #undef ROWS_ARGS
-    if (l == 0 && prefetch) {
-      // the later layers' packs (in registers since the kernel start, their loads hidden
-      // behind layer 0) -> their LDS slots, which layer 0 does not read; the barrier below
-      // publishes them to layer 1
-      const int w1 = A.L[1].w_lds, w2 = A.n > 2 ? A.L[2].w_lds : 0, w3 = A.n > 3 ? A.L[3].w_lds : 0;
-#pragma unroll
-      for (int j = 0; j < PF; ++j) {
-        const int v = tid + j * STACK_THREADS;
-        const int e = v < nv1 ? w1 + v * 8 : v < nv1 + nv2 ? w2 + (v - nv1) * 8 : w3 + (v - nv1 - nv2) * 8;
-        if (v < nv1 + nv2 + nv3) *reinterpret_cast<LDS bf16x8*>(wlds + e) = pf[j];
-      }
-    }
     STACK_STAMP(3 + 4 * l);
+    if (l == 0 && prefetch) {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) asm volatile("" :: "v"(dma_src[j]));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the untracked DMA
+    }
     __syncthreads();
     STACK_STAMP(4 + 4 * l);
     // owned stage rows (+ argmax codes) -> global, 16-byte stores

@@ -356,7 +356,7 @@ class GeometryMixin:
         nblocks = bs * cdiv(g.Ho, R)
         groups = cdiv(NT, NTT) * cdiv(a.Ktiles, MT)
         per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
-        s_budget = max(1, (8 << 20) // per_split_bytes)
+        s_budget = max(1, (tune("wgrad_slab_mb", 8) << 20) // per_split_bytes)
         # splits: one round of resident workgroups (occupancy x CUs), not more -- the
         # latency-bound blocks then all stream concurrently instead of a second thin round
         cap = tune("wgrad_splits", 0) or K.wgrad_halo_resident(a, MT, NTT, bool(bias)) or 768
