@@ -107,6 +107,23 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
     return (((size_t)b * a.dHp + wy) * a.dWp + wx) * a.Cs_dy + nt0 * 16 + ch * 8;
   };
   // write pooled chunk q (dP values v, codes cw) to the 4 pixels of its window
+  // ... the same from the chunk's precomputed LDS offset (window's top-left pixel row)
+  auto pq_store_at = [&](int dst, const uint4& v, const uint2& cw) {
+#pragma unroll
+    for (int pos = 0; pos < 4; ++pos) {
+      uint32_t m[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t w = h ? cw.y : cw.x;
+        m[2 * h] = (((w & 0xFF) == (uint32_t)pos) ? 0x0000FFFFu : 0u) |
+                   ((((w >> 8) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
+        m[2 * h + 1] = ((((w >> 16) & 0xFF) == (uint32_t)pos) ? 0x0000FFFFu : 0u) |
+                       ((((w >> 24) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
+      }
+      *reinterpret_cast<uint4*>(dyl + dst + ((pos >> 1) * a.Wo + (pos & 1)) * ldb) =
+          uint4{v.x & m[0], v.y & m[1], v.z & m[2], v.w & m[3]};
+    }
+  };
   auto pq_store = [&](int q, const uint4& v, const uint2& cw) {
     const int p2 = fcpr.div(q), ch = q - p2 * cpr;
     const int ry = fhw.div(p2);
@@ -191,20 +208,45 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
     int xa[WH_PX];
     uint2 yc[WH_PY];
     uint32_t yp[WH_PY];
+    // Per-lane staging constants, the same for every block: a chunk's halo row / column /
+    // channel, its LDS offset and its source offset from the block's first input row (the
+    // block only moves the row base), and the pooled dY chunk's source offset from the
+    // block's first pooled row and LDS offset -- the per-block fetch is adds and compares,
+    // not FastDiv chains.
+    int xrow[WH_PX], xoff[WH_PX], qoff[WH_PY], qdst[WH_PY];
+    uint32_t xcol = 0;                  // bit u: the chunk's column lies inside the image
+#pragma unroll
+    for (int u = 0; u < WH_PX; ++u) {
+      const int idx = min(tid + u * 256, nch_x - 1);
+      const int pix = fcpp.div(idx), c = (idx - pix * cpp) * cw;
+      const int r = fwin.div(pix), px = pix - r * W_in;
+      const int ix = px - a.pad_l;
+      xa[u] = (r * XR + px) * XP + c;
+      xrow[u] = r;
+      xoff[u] = (r * a.W + ix) * Cs + c;
+      if (ix >= 0 && ix < a.W) xcol |= 1u << u;
+    }
+    if (pexp) {
+#pragma unroll
+      for (int u = 0; u < WH_PY; ++u) {
+        const int q = min(tid + u * 256, nq - 1);
+        const int p2 = fcpr.div(q), ch = q - p2 * cpr;
+        const int ry = fhw.div(p2), wx = p2 - ry * hw;
+        qoff[u] = (ry * a.dWp + wx) * a.Cs_dy + nt0 * 16 + ch * 8;
+        qdst[u] = ((2 * ry) * a.Wo + 2 * wx) * ldb + ch * 8;
+      }
+    }
     auto fetch = [&](const int blk) {
       const int b = blk / nrb, oy0 = (blk - b * nrb) * R;
       const int npix = min(R, a.Ho - oy0) * a.Wo;
-      const int yb = oy0 * s - a.pad_t, xb0 = -a.pad_l;
+      const int yb = oy0 * s - a.pad_t;
       const bf16* xbase = a.x + (size_t)b * a.H * a.W * Cs;
+      const bf16* xrow0 = xbase + (ptrdiff_t)yb * a.W * Cs;         // may point before xbase
 #pragma unroll
       for (int u = 0; u < WH_PX; ++u) {
-        const int idx = min(tid + u * 256, nch_x - 1);
-        const int pix = fcpp.div(idx), c = (idx - pix * cpp) * cw;
-        const int r = fwin.div(pix);
-        const int iy = yb + r, ix = xb0 + (pix - r * W_in);
-        xa[u] = (r * XR + (pix - r * W_in)) * XP + c;
-        const bool ok = iy >= 0 && ix >= 0 && iy < a.H && ix < a.W;
-        const bf16* src = ok ? xbase + ((size_t)iy * a.W + ix) * Cs + c : xbase;
+        const int iy = yb + xrow[u];
+        const bool ok = ((xcol >> u) & 1u) && iy >= 0 && iy < a.H;
+        const bf16* src = ok ? xrow0 + xoff[u] : xbase;
         if (CS4) {
           const uint2 v = *reinterpret_cast<const uint2*>(src);
           xr[u] = uint4{ok ? v.x : 0u, ok ? v.y : 0u, 0u, 0u};
@@ -214,9 +256,10 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
         }
       }
       if (pexp) {
+        const size_t qb = (((size_t)b * a.dHp + (oy0 >> 1)) * a.dWp) * a.Cs_dy;
 #pragma unroll
         for (int u = 0; u < WH_PY; ++u) {
-          const size_t o = pq_off(min(tid + u * 256, nq - 1), b, oy0);
+          const size_t o = qb + qoff[u];
           yr[u] = *reinterpret_cast<const uint4*>(a.dy + o);
           yc[u] = *reinterpret_cast<const uint2*>(a.dy_code + o);
         }
@@ -258,7 +301,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       if (pexp) {
 #pragma unroll
         for (int u = 0; u < WH_PY; ++u)
-          if (tid + u * 256 < nq) pq_store(tid + u * 256, yr[u], yc[u]);
+          if (tid + u * 256 < nq) pq_store_at(qdst[u], yr[u], yc[u]);
         return;
       }
 #pragma unroll
