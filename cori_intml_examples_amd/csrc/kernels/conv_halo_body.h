@@ -103,16 +103,34 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
       // the (up to) four full-resolution halo pixels of its window -- a quarter of the
       // global loads of rebuilding every pixel from its window (unpool_load8 per pixel).
       const int Ha = 2 * a.in_pH, Wa = 2 * a.in_pW;
-      // halo pixels outside the pooled area (padding, odd edge) hold zeros
-      for (int i = tid; i < nch; i += 256) {
-        const int pix = fcpp.div(i);
-        const int r = fwin.div(pix);
-        const int y = yb + r, x = xb0 + (pix - r * W_in);
-        if (y < 0 || x < 0 || y >= Ha || x >= Wa)
-          *reinterpret_cast<bf16x8*>(xl + (size_t)pix * XP + (i - pix * hcpp) * 8) = zero_bf16x8();
-      }
       const int y_lo = max(yb, 0), y_hi = min(yb + R_in, Ha);
       const int x_lo = max(xb0, 0), x_hi = min(xb0 + W_in, Wa);
+      // halo pixels outside the pooled area (padding, odd edge) hold zeros: whole rows above
+      // / below it and the columns left / right of it -- enumerated directly (the border is
+      // a few hundred chunks; testing all R_in x W_in chunks cost two FastDivs each), and
+      // written while the first batch of pooled loads is in flight
+      auto zero_border = [&]() {
+        const int ntop = min(R_in, max(0, -yb));
+        const int nbot = min(R_in - ntop, max(0, yb + R_in - Ha));
+        const int lc = min(W_in, max(0, -xb0)), rc = min(W_in - lc, max(0, xb0 + W_in - Wa));
+        const int rowch = W_in * hcpp;
+        for (int rr = 0; rr < ntop + nbot; ++rr) {         // workgroup-uniform
+          const int r = rr < ntop ? rr : R_in - 1 - (rr - ntop);
+          for (int i = tid; i < rowch; i += 256) {
+            const int px = fcpp.div(i);
+            *reinterpret_cast<bf16x8*>(xl + (size_t)(r * W_in + px) * XP + (i - px * hcpp) * 8) = zero_bf16x8();
+          }
+        }
+        const int side = (lc + rc) * hcpp;
+        const int nside = (R_in - ntop - nbot) * side;
+        for (int i = tid; i < nside; i += 256) {
+          const int m = i / side, j = i - m * side;
+          const int cp = j / hcpp, ch = j - cp * hcpp;
+          const int px = cp < lc ? cp : W_in - rc + (cp - lc);
+          *reinterpret_cast<bf16x8*>(xl + (size_t)((ntop + m) * W_in + px) * XP + ch * 8) = zero_bf16x8();
+        }
+      };
+      if (!(y_lo < y_hi && x_lo < x_hi)) zero_border();
       if (y_lo < y_hi && x_lo < x_hi) {
         const int py0 = y_lo >> 1, npy = ((y_hi - 1) >> 1) - py0 + 1;
         const int px0 = x_lo >> 1, npx = ((x_hi - 1) >> 1) - px0 + 1;
@@ -135,6 +153,8 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
             raw[u] = *reinterpret_cast<const uint4*>(xbase + o);
             cw[u] = *reinterpret_cast<const uint2*>(cbase + o);
           }
+          if (q0 == tid) zero_border();               // beside the first batch's loads
+                                                      // (threads past nq: after the loop)
 #pragma unroll
           for (int u = 0; u < UQ; ++u) {
             if (q0 + u * 256 >= nq) break;
@@ -156,6 +176,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
             }
           }
         }
+        if (tid >= nq) zero_border();
       }
     } else {
       staged_copy<8, bf16x8>(nch, tid, 256, halo8, [&](int i, const bf16x8& v) {
