@@ -20,6 +20,23 @@ struct BwdThrough {
   bf16* dy = nullptr;                   // output [B, cH, cW, pCs] (or [B, pH, pW, pCs])
 };
 
+// Where an updated master element goes in the bf16 fragment packs (pack_write, optim_math.h):
+// the optimizer that produces a new weight writes its bf16 copies into the packs the MFMA
+// kernels read, so no step needs a separate re-pack pass over the master.  One route per
+// packed weight tensor, master range [lo, hi):
+//   kind 1, conv  W[tap][ci][co]: fwd pack  k = tap*Cs + ci,            n = co
+//                                 dgrad pack k = (KHW-1-tap)*Csb + co,  n = ci
+//   kind 2, dense W[k][n] (k = Keras flatten index over Cin channels, padded kp = (k / Cin)*Cs + k % Cin):
+//                                 fwd pack  k = kp, n = n;   bwd pack k = n, n = kp
+// fwd / bwd: element offsets of the packs in the arena (-1: none); NT / NTb: their n-tiles.
+struct PackRoute {
+  int lo, hi, kind;
+  int KHW, Cin, Cout, Cs, Csb;
+  int NT, NTb;
+  long long fwd, bwd;
+};
+#define MAX_ROUTES 8
+
 // Keras optimizer update of a flat fp32 range (optimizer kernels; also fused into the
 // reductions / the dense weight-gradient kernel).
 struct OptimArgs {
@@ -37,6 +54,10 @@ struct OptimArgs {
   int pack_only = 0;
   int defer_pack = 0;            // leave the re-pack to the next step's prologue (marks stale)
   bf16* arena = nullptr;
+  // routes (device array, read with workgroup-uniform indices): nroutes > 0 -> every updated
+  // weight is also written to its packs (pack_write) and nothing is marked stale
+  const PackRoute* routes = nullptr;
+  int nroutes = 0;
 };
 
 // Implicit-GEMM convolution / 1x1 "dense as conv" (fwd, dgrad, dense-dX).
@@ -121,6 +142,13 @@ struct ConvStackArgs {
   int rows[MAX_STACK][MAX_STACK_SPLIT][6] = {};
   StackLayer L[MAX_STACK];
   unsigned long long* ts = nullptr;   // diagnostics: per-wave phase stamps [blocks*8][32]: 16 wall, 16 shader clock (null = off)
+  // Prologue-free step: from_data = image b is read straight from the bound dataset through
+  // the step cursor (training ? pos : eval_pos) and the epoch permutation (step_src_row), and
+  // the band-0 workgroup records that dataset row in srcidx[b] for the later kernels of the
+  // step (the first layer's wgrad, the head's targets); step_inc = 1: the step bookkeeping
+  // runs after this launch, so the dropout counter is st->t + 1
+  int from_data = 0, training = 0, step_inc = 0;
+  int* srcidx = nullptr;
 };
 
 // Weight gradient: dW[k][n] = sum_pixels im2col(x)[p][k] * dY[p][n]  (split over pixels)
@@ -158,9 +186,20 @@ struct WgradArgs {
   // dense): X-halo pixel stride in elements, X-halo row stride in pixels, dY row stride
   int xpix = 0, xrow = 0, dyld = 0;
   int kperm = 0;                 // bit0: k index 8g+j <-> pixel 4g+j / 16+4g+j-4; bit1: no row-aligned fast path
+  // xidx != null: image b of x is dataset row xidx[b] of st->data_x (prologue-free step)
+  const int* xidx = nullptr;
+  const StepState* xst = nullptr;
 };
 
 // Dense forward, split-K partial products: part[s][m][n]
+struct StepBeginArgs {
+  StepState* st = nullptr;
+  int training = 1;
+  int bs = 0;
+  int opt_kind = 0;
+  float beta1 = 0.9f, beta2 = 0.999f, decay = 0.f, schedule_decay = 0.004f;
+};
+
 struct DenseFwdArgs {
   const bf16* x = nullptr;
   int M = 0, Ks = 0;             // x is [M][Ks]
@@ -173,6 +212,11 @@ struct DenseFwdArgs {
   int mode = 0;
   const StepState* st = nullptr;
   BwdThrough bt;
+  // book: workgroup 0 runs the step bookkeeping (step_book.h) -- the training step's first
+  // dense launch takes it over when no prologue launch runs (the conv stack before it reads
+  // the iteration count as t + 1, see ConvStackArgs::step_inc)
+  int book = 0;
+  StepBeginArgs sb;
 };
 
 // Split-K reduction + bias + activation + dropout -> bf16 [M][Ns]
@@ -211,6 +255,8 @@ struct HeadArgs {
   // layer's bf16 output and uses it as h -- one launch instead of two
   DenseEpiArgs epi;
   unsigned long long* ts = nullptr;   // diagnostics: [block][8] phase stamps (null = off)
+  // yidx != null: row m's targets are dataset row yidx[m] of st->data_y (prologue-free step)
+  const int* yidx = nullptr;
 };
 
 struct GatherArgs {
@@ -224,13 +270,6 @@ struct GatherArgs {
   int skip_x = 0;                // images read straight from the dataset by the conv stack
 };
 
-struct StepBeginArgs {
-  StepState* st = nullptr;
-  int training = 1;
-  int bs = 0;
-  int opt_kind = 0;
-  float beta1 = 0.9f, beta2 = 0.999f, decay = 0.f, schedule_decay = 0.004f;
-};
 
 // One launch opening every step: batch gather (workgroups [0, gather_blocks)), weight
 // re-pack of the previous update (the rest; pack_mode 1 always, 2 only if st->packs_stale),

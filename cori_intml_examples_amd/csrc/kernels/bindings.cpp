@@ -101,13 +101,15 @@ PYBIND11_MODULE(_kernels, m) {
       RW(WgradArgs, KT) PTR(WgradArgs, slab) PTR(WgradArgs, bslab) RW(WgradArgs, R)
       RW(WgradArgs, blocks_per_split) PTR(WgradArgs, dy_code) PTR(WgradArgs, zero) RW(WgradArgs, dHp) RW(WgradArgs, dWp)
       RW(WgradArgs, dbg) PTR(WgradArgs, ts) PTR(WgradArgs, ts2) RW(WgradArgs, opt) RW(WgradArgs, opt_w)
-      RW(WgradArgs, opt_b) RW(WgradArgs, xpix) RW(WgradArgs, xrow) RW(WgradArgs, dyld) RW(WgradArgs, kperm);
+      RW(WgradArgs, opt_b) RW(WgradArgs, xpix) RW(WgradArgs, xrow) RW(WgradArgs, dyld) RW(WgradArgs, kperm)
+      PTR(WgradArgs, xidx) PTR(WgradArgs, xst);
 
   py::class_<DenseFwdArgs>(m, "DenseFwdArgs")
       .def(py::init<>())
       PTR(DenseFwdArgs, x) RW(DenseFwdArgs, M) RW(DenseFwdArgs, Ks) PTR(DenseFwdArgs, wpk)
       RW(DenseFwdArgs, NT) RW(DenseFwdArgs, KS) RW(DenseFwdArgs, splits) RW(DenseFwdArgs, ks_per_split)
-      PTR(DenseFwdArgs, part) RW(DenseFwdArgs, mode) PTR(DenseFwdArgs, st) RW(DenseFwdArgs, bt);
+      PTR(DenseFwdArgs, part) RW(DenseFwdArgs, mode) PTR(DenseFwdArgs, st) RW(DenseFwdArgs, bt)
+      RW(DenseFwdArgs, book) RW(DenseFwdArgs, sb);
 
   py::class_<DenseEpiArgs>(m, "DenseEpiArgs")
       .def(py::init<>())
@@ -121,7 +123,8 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(HeadArgs, h) RW(HeadArgs, M) RW(HeadArgs, K) RW(HeadArgs, Ks) RW(HeadArgs, N)
       RW(HeadArgs, flat_C) RW(HeadArgs, flat_Cs) PTR(HeadArgs, w) PTR(HeadArgs, bias) PTR(HeadArgs, y)
       RW(HeadArgs, act) RW(HeadArgs, training) RW(HeadArgs, inv_bs) PTR(HeadArgs, st) PTR(HeadArgs, probs)
-      PTR(HeadArgs, wslab) PTR(HeadArgs, bslab) RW(HeadArgs, bt) RW(HeadArgs, epi) PTR(HeadArgs, ts);
+      PTR(HeadArgs, wslab) PTR(HeadArgs, bslab) RW(HeadArgs, bt) RW(HeadArgs, epi) PTR(HeadArgs, ts)
+      PTR(HeadArgs, yidx);
 
   py::class_<GatherArgs>(m, "GatherArgs")
       .def(py::init<>())
@@ -150,6 +153,7 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(ConvStackArgs, st) RW(ConvStackArgs, dbg) RW(ConvStackArgs, off_w) RW(ConvStackArgs, off_codes) RW(ConvStackArgs, off_codes2) RW(ConvStackArgs, lds_bytes)
       .def("set_buf_offsets", [](ConvStackArgs& a, int b0, int b1) { a.off_buf[0] = b0; a.off_buf[1] = b1; })
       RW(ConvStackArgs, splits) PTR(ConvStackArgs, ts) RW(ConvStackArgs, off_bias)
+      RW(ConvStackArgs, from_data) RW(ConvStackArgs, training) RW(ConvStackArgs, step_inc) PTR(ConvStackArgs, srcidx)
       .def("set_rows", [](ConvStackArgs& a, int l, int sp, int c0, int c1, int o0, int o1, int ib, int ih) {
         if (l < 0 || l >= MAX_STACK || sp < 0 || sp >= MAX_STACK_SPLIT) throw std::out_of_range("conv stack rows");
         const int v[6] = {c0, c1, o0, o1, ib, ih};
@@ -180,7 +184,8 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(OptimArgs, p) PTR(OptimArgs, g) PTR(OptimArgs, s0) PTR(OptimArgs, s1) RW(OptimArgs, n) RW(OptimArgs, lo)
       PTR(OptimArgs, st) RW(OptimArgs, kind) RW(OptimArgs, beta1) RW(OptimArgs, beta2) RW(OptimArgs, eps)
       RW(OptimArgs, rho) RW(OptimArgs, momentum) RW(OptimArgs, nesterov) RW(OptimArgs, grad_scale)
-      RW(OptimArgs, pack_only) RW(OptimArgs, defer_pack) PTR(OptimArgs, arena);
+      RW(OptimArgs, pack_only) RW(OptimArgs, defer_pack) PTR(OptimArgs, arena) PTR(OptimArgs, routes)
+      RW(OptimArgs, nroutes);
 
   py::class_<PackTable>(m, "PackTable")
       .def(py::init([]() { PackTable t; memset(&t, 0, sizeof(t)); return t; }))
@@ -256,6 +261,9 @@ PYBIND11_MODULE(_kernels, m) {
       py::arg("type"), py::arg("KH"), py::arg("KW"), py::arg("Cin"), py::arg("Cout"), py::arg("Cs"), py::arg("tpe") = -1);
 
   m.attr("STEP_STATE_BYTES") = (int)sizeof(StepState);
+  static_assert(sizeof(PackRoute) == 56 && offsetof(PackRoute, fwd) == 40, "PackRoute layout (models/plan routes)");
+  m.attr("PACK_ROUTE_BYTES") = (int)sizeof(PackRoute);
+  m.attr("MAX_ROUTES") = MAX_ROUTES;
   m.attr("STEP_STATE_METRICS_OFFSET") = (int)offsetof(StepState, metric_slots);
   m.attr("STEP_STATE_METRIC_SLOTS") = 16;
   m.attr("STEP_STATE_MSCHED_OFFSET") = (int)offsetof(StepState, m_schedule);

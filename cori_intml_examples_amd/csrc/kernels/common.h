@@ -220,6 +220,20 @@ struct PackTable {
   DensePair dp[MAX_DENSE_PAIRS];
 };
 
+// Dataset row of batch row b of this step: the cursor (training ? pos : eval_pos) + b,
+// clamped BEFORE it indexes the permutation (perm holds data_n entries: a cursor run past the
+// data set -- a launch replayed on its own, a caller's bad pos -- must not read past it).
+__device__ __forceinline__ int step_src_pos(const StepState* st, int pos) {
+  const int n = st->data_n;
+  pos = min(max(pos, 0), max(n - 1, 0));
+  const int* perm = reinterpret_cast<const int*>(st->perm);
+  const int src = (st->use_perm && perm) ? perm[pos] : pos;
+  return min(max(src, 0), n - 1);
+}
+__device__ __forceinline__ int step_src_row(const StepState* st, int training, int b) {
+  return step_src_pos(st, (training ? st->pos : st->eval_pos) + b);
+}
+
 // Dense flatten mapping: keras flat index (h,w,c) over C channels -> padded index over Cs.
 __device__ __forceinline__ int flat_keras_to_padded(int k, int C, int Cs) {
   int hw = k / C;

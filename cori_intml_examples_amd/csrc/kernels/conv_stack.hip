@@ -387,7 +387,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   // two argmax-code planes (layer parity): a layer's epilogue writes its plane while slower
   // waves may still copy the previous layer's codes out (no barrier between those phases)
   LDS uint8_t* codes_pl[2] = {(LDS uint8_t*)(smem + A.off_codes), (LDS uint8_t*)(smem + A.off_codes2)};
-  const uint32_t step = A.st ? (uint32_t)A.st->t : 0u;
+  const uint32_t step = A.st ? (uint32_t)A.st->t + (uint32_t)A.step_inc : 0u;
   STACK_STAMP(0);
   if (tid < 8) ((LDS uint32_t*)zl)[tid] = 0u;
   // biases -> LDS [layer][64] (read by the epilogues: no global load after the prefetch
@@ -425,6 +425,11 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     const int XR = L.xrow, XP = L.xpix;
     const int y0 = A.rows[0][sp][4];
     const bf16* x = A.x + (size_t)b * L.H * L.W * Cs;
+    if (A.from_data) {   // straight from the bound dataset: no gather launch
+      const int src = step_src_row(A.st, A.training, b);
+      x = reinterpret_cast<const bf16*>(A.st->data_x) + (size_t)src * A.st->data_R;
+      if (sp == 0 && tid == 0 && A.srcidx) A.srcidx[b] = src;
+    }
     if (Cs == 4) {
       const FastDiv fwi(Wi);
       staged_copy<8, bf16x4>(

@@ -11,8 +11,12 @@
 // bf16 "transposed" pack, routing every output element straight back through the previous
 // stage's dropout / ReLU masks (flattened conv dP or hidden-dense dH).
 #include "dense_body.h"
+#include "step_book.h"
 
 __global__ __launch_bounds__(256) void dense_splitk_kernel(const DenseFwdArgs a) {
+  // prologue-free step: this step's bookkeeping (no workgroup of this launch reads its
+  // scalars; every later launch of the step does)
+  if (a.book && blockIdx.x == 0 && threadIdx.x == 0) step_bookkeeping(a.sb);
   dense_splitk_body(a, blockIdx.x);
 }
 
@@ -37,6 +41,7 @@ constexpr long long DL_BIG_BYTES = 8ll << 20;   // weight bytes above which the 
 
 __global__ __launch_bounds__(512) void dense_lds_kernel(const DenseFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.book && blockIdx.x == 0 && threadIdx.x == 0) step_bookkeeping(a.sb);   // (as dense_splitk)
   bf16* const As = reinterpret_cast<bf16*>(smem);  // [2][DL_KST][DL_ROWS][DL_LDA]
   constexpr int STG = DL_KST * DL_ROWS * DL_LDA;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;

@@ -167,7 +167,12 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   if (tid < 16) bsh[tid] = (a.bias && tid < a.N) ? a.bias[tid] : 0.f;
   if (tid >= 64 && tid < 64 + RB * 16) {
     const int rl = (tid - 64) >> 4, n = (tid - 64) & 15;
-    ysh[rl][n] = (a.y && n < a.N && row0 + rl < a.M) ? a.y[(size_t)(row0 + rl) * a.N + n] : 0.f;
+    const int m = row0 + rl;
+    const bool ok = a.y && n < a.N && m < a.M;
+    // (prologue-free step: the targets' dataset row, recorded by the conv stack)
+    const float* yr = a.yidx ? reinterpret_cast<const float*>(a.st->data_y) + (size_t)a.yidx[ok ? m : 0] * a.st->data_C
+                             : a.y + (size_t)m * a.N;
+    ysh[rl][n] = ok ? yr[n] : 0.f;
   }
   bool done_epi = false;
   if constexpr (RB == 1) {

@@ -13,48 +13,7 @@
 #include "args.h"
 #include "optim_math.h"
 #include "reduce_body.h"
-
-// Step bookkeeping (one thread): iteration counter, LR decay and the optimizer's
-// bias-correction scalars for this step.  (The data cursor is advanced by the head kernel,
-// after every prologue workgroup has read it.)
-__device__ void step_bookkeeping(const StepBeginArgs& a) {
-  StepState* st = a.st;
-  if (!a.training) return;
-  st->t += 1;
-  const double t = (double)st->t;
-  double base = (double)st->lr;
-  const int g = st->t - st->warm_t0 - 1;
-  if (g >= 0 && g < st->warm_steps) {
-    const double n = (double)st->warm_size;
-    base = (double)st->warm_base / n * ((double)(g + 1) / st->warm_spe * (n - 1.0) / st->warm_epochs + 1.0);
-  }
-  const double lr = base / (1.0 + (double)a.decay * (t - 1.0));
-  st->lr_eff = (float)lr;
-  switch (a.opt_kind) {
-    case OPT_ADAM: {
-      const double b1t = pow((double)a.beta1, t), b2t = pow((double)a.beta2, t);
-      st->s[0] = (float)(lr * sqrt(1.0 - b2t) / (1.0 - b1t));
-      break;
-    }
-    case OPT_NADAM: {
-      const double b1 = a.beta1;
-      const double mc_t = b1 * (1.0 - 0.5 * pow(0.96, t * a.schedule_decay));
-      const double mc_t1 = b1 * (1.0 - 0.5 * pow(0.96, (t + 1.0) * a.schedule_decay));
-      const double ms_new = st->m_schedule * mc_t;
-      const double ms_next = ms_new * mc_t1;
-      st->m_schedule = ms_new;
-      st->s[0] = (float)mc_t;
-      st->s[1] = (float)mc_t1;
-      st->s[2] = (float)(1.0 / (1.0 - ms_new));
-      st->s[3] = (float)(1.0 / (1.0 - ms_next));
-      st->s[4] = (float)(1.0 / (1.0 - pow((double)a.beta2, t)));
-      st->s[5] = (float)lr;
-      break;
-    }
-    default:
-      st->s[0] = (float)lr;
-  }
-}
+#include "step_book.h"
 
 // Batch rows from the device-resident dataset by the epoch's permutation (16-byte copies),
 // targets alongside.  `pos0` is the step's cursor (read before the bookkeeping advances it).
@@ -62,14 +21,8 @@ __device__ __forceinline__ void gather_block(const GatherArgs& a, const StepStat
                                              int gx) {
   const bf16* xs = reinterpret_cast<const bf16*>(st->data_x);
   const float* ys = reinterpret_cast<const float*>(st->data_y);
-  const int* perm = reinterpret_cast<const int*>(st->perm);
   const int R = st->data_R, C = st->data_C;
-  // the cursor is clamped BEFORE it indexes the permutation (perm holds data_n entries): a
-  // cursor run past the data set -- a launch replayed on its own, a caller's bad pos --
-  // must not read past the permutation buffer
-  const int pos = min(max(pos0 + row, 0), max(st->data_n - 1, 0));
-  int src = (st->use_perm && perm) ? perm[pos] : pos;
-  src = min(max(src, 0), st->data_n - 1);
+  const int src = step_src_pos(st, pos0 + row);   // (cursor clamped before the permutation)
   const int nvec = R / 8;   // 16-byte vectors per row
   const uint4* s = reinterpret_cast<const uint4*>(xs + (size_t)src * R);
   uint4* d = reinterpret_cast<uint4*>(a.xb + (size_t)row * R);
@@ -292,7 +245,17 @@ __global__ __launch_bounds__(256) void optim_kernel(const OptimArgs a) {
   *reinterpret_cast<float4*>(a.p + e) = p;
   if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
   if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
-  if (a.defer_pack && blockIdx.x == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
+  if (a.nroutes) {
+    if (e >= a.lo && e + 4 <= end) {
+      pack_write4(a, e, p);
+    } else {
+      if (e >= a.lo && e < end) pack_write(a, e, p.x);
+      if (e + 1 >= a.lo && e + 1 < end) pack_write(a, e + 1, p.y);
+      if (e + 2 >= a.lo && e + 2 < end) pack_write(a, e + 2, p.z);
+      if (e + 3 >= a.lo && e + 3 < end) pack_write(a, e + 3, p.w);
+    }
+  }
+  if (a.defer_pack && !a.nroutes && blockIdx.x == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
 }
 
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s) {

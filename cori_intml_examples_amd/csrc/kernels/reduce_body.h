@@ -123,6 +123,7 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
       *reinterpret_cast<float4*>(a.p + e) = p;
       if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
       if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
+      if (a.nroutes) pack_write4(a, e, p);
     }
   } else {
     int e;
@@ -135,9 +136,10 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
       a.p[e] = p;
       if (a.s0) a.s0[e] = s0;
       if (a.s1) a.s1[e] = s1;
+      if (a.nroutes) pack_write(a, e, p);
     }
   }
-  if (a.defer_pack && blk == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
+  if (a.defer_pack && !a.nroutes && blk == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
 }
 
 // the same with the optimizer kind chosen at run time (a workgroup-uniform switch)

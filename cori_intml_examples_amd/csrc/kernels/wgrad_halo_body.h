@@ -18,6 +18,13 @@ __device__ __forceinline__ bf16x4 tr_read_h(const bf16* p) {
 #define WH_STAMP(i)                                                                     \
   if (a.ts2 && threadIdx.x == 0 && (i) < 16) a.ts2[(size_t)blockIdx.x * 16 + (i)] = wall_clock64();
 
+// image b of the wgrad input: the activation buffer, or (prologue-free step, first layer)
+// dataset row xidx[b] of the bound dataset
+__device__ __forceinline__ const bf16* wg_xbase(const WgradArgs& a, int b) {
+  if (a.xidx) return reinterpret_cast<const bf16*>(a.xst->data_x) + (size_t)a.xidx[b] * a.xst->data_R;
+  return a.x + (size_t)b * a.H * a.W * a.Cs_in;
+}
+
 template <int MTW, int NTT, bool CS4, bool PIPE>
 __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT, const int bx, const int by,
                                                 const int bz, char* smem) {
@@ -240,7 +247,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       const int b = blk / nrb, oy0 = (blk - b * nrb) * R;
       const int npix = min(R, a.Ho - oy0) * a.Wo;
       const int yb = oy0 * s - a.pad_t;
-      const bf16* xbase = a.x + (size_t)b * a.H * a.W * Cs;
+      const bf16* xbase = wg_xbase(a, b);
       const bf16* xrow0 = xbase + (ptrdiff_t)yb * a.W * Cs;         // may point before xbase
 #pragma unroll
       for (int u = 0; u < WH_PX; ++u) {
@@ -350,7 +357,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       if (blk != blk0) __syncthreads();   // previous block's readers are done
       if (dbg_stage) {   // X halo
         const int yb = oy0 * s - a.pad_t, xb0 = -a.pad_l;
-        const bf16* xbase = a.x + (size_t)b * a.H * a.W * Cs;
+        const bf16* xbase = wg_xbase(a, b);
         auto coords = [&](int idx, int& c, int& iy, int& ix) -> bool {
           const int pix = fcpp.div(idx);
           c = (idx - pix * cpp) * cw;

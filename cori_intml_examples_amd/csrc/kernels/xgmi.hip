@@ -116,6 +116,7 @@ __device__ __forceinline__ void finish4(const XgmiArgs& a, float* __restrict__ g
       *reinterpret_cast<float4*>(o.p + idx) = p4;
       if (o.s0) *reinterpret_cast<float4*>(o.s0 + idx) = m4;
       if (o.s1) *reinterpret_cast<float4*>(o.s1 + idx) = v4;
+      if (o.nroutes) pack_write4(o, o.lo + (int)idx, p4);   // o.lo: the bucket's flat start
     }
     return;
   }
@@ -129,6 +130,7 @@ __device__ __forceinline__ void finish4(const XgmiArgs& a, float* __restrict__ g
       o.p[idx + e] = pe;
       if (o.s0) o.s0[idx + e] = s0;
       if (o.s1) o.s1[idx + e] = s1;
+      if (o.nroutes) pack_write(o, o.lo + (int)(idx + e), pe);
     }
   }
 }
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
         if (q < P && q != r) finish4<KIND>(a, grad, (long long)q * C + k, n, g[q]);
     }
   }
-  if (a.mode == 1 && a.opt.defer_pack && w == 0 && t == 0) a.opt.st->packs_stale = 1;
+  if (a.mode == 1 && a.opt.defer_pack && !a.opt.nroutes && w == 0 && t == 0) a.opt.st->packs_stale = 1;
   if (t == 0) a.ctr[w] = seq;
 }
 

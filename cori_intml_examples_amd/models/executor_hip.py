@@ -275,6 +275,30 @@ class HipExecutor(Executor):
                 tab.add(sp.offset, sp.numel, PACK_DENSE_BWD, g.src.H, g.src.W, g.src.C, g.N, g.src.Cs, g.NTb, g.pack_bwd)
         self.pack_table = tab.t
         self.arena = torch.zeros(max(off, 8), dtype=BF16, device=self.device)
+        # pack routes (PackRoute, args.h): the optimizer writes every updated weight's bf16
+        # copies into these packs itself, so a training step needs no re-pack pass
+        routes = []
+        for g, cs in zip(self.convs, self.plan.convs):
+            sp = st.spec(cs.conv, "kernel")
+            bwd = g.pack_dgrad if g.i > 0 and g.Cs_out % 4 == 0 else -1
+            routes.append((sp.offset, sp.offset + sp.numel, 1, g.KH * g.KW, g.Cin, g.Cout, g.Cs_in,
+                           g.Cs_out if g.i > 0 else 0, g.NT, g.NTd if g.i > 0 else 0, g.pack_fwd, bwd))
+        for g, ds in zip(self.denses, self.plan.denses):
+            sp = st.spec(ds.dense, "kernel")
+            routes.append((sp.offset, sp.offset + sp.numel, 2, g.src.H * g.src.W, g.src.C, g.N, g.src.Cs, 0,
+                           g.NT, g.NTb if g.KSb else 0, g.pack_fwd, g.pack_bwd if g.KSb else -1))
+        self.routes_ok = (bool(routes) and len(routes) <= K.MAX_ROUTES and tune("opt_packs", True)
+                          and not tune("dense_opt", False))
+        self.routes = None
+        if self.routes_ok:
+            words = K.PACK_ROUTE_BYTES // 4
+            arr = np.zeros(len(routes) * words, dtype=np.int32)
+            a64 = arr.view(np.int64)
+            for r, rt in enumerate(routes):
+                arr[r * words:r * words + 10] = rt[:10]
+                a64[r * words // 2 + 5] = rt[10]
+                a64[r * words // 2 + 6] = rt[11]
+            self.routes = torch.from_numpy(arr).to(self.device)
 
     # ------------------------------------------------------------------ params / optimizer
     def _optim_args(self, pack_only: bool, defer_pack: bool = False):
@@ -300,6 +324,9 @@ class HipExecutor(Executor):
         a.pack_only = int(pack_only)
         a.defer_pack = int(defer_pack)
         a.arena = self.arena.data_ptr()
+        if self.routes is not None and not pack_only:
+            a.routes = self.routes.data_ptr()
+            a.nroutes = self.routes.numel() * 4 // K.PACK_ROUTE_BYTES
         return a
 
     def params_changed(self):
@@ -521,6 +548,15 @@ class BatchPlan(GeometryMixin):
         self._build_args()
 
     # ---------------------------------------------------------------- helpers
+    def step_inputs(self):
+        """(x [bs, R] bf16, y [bs, C] fp32) of this plan's last step: the gathered batch
+        buffers, or -- prologue-free step -- the dataset rows the conv stack recorded."""
+        if self.srcidx is None:
+            return self.xb, self.yb
+        d = self.ex._bound_ref
+        idx = self.srcidx.long()
+        return d.x[idx], d.y[idx]
+
     def _src_buf(self, src: Src):
         if src.kind == "input":
             return self.xb
@@ -586,6 +622,17 @@ class BatchPlan(GeometryMixin):
         # except with per-bucket optimizers that pack themselves; eval/predict: only if an
         # optimizer ran since the last pack) + the step bookkeeping
         stack = self._conv_stack_args(training) if tune("conv_stack", True) else None
+        # Prologue-free step (conv stack + a hidden dense layer + optimizer-written packs): the
+        # stack reads its images straight from the dataset through the cursor and permutation
+        # (recording each image's dataset row for the first layer's wgrad and the head's
+        # targets), the optimizer keeps the bf16 packs current, and the first dense launch runs
+        # the step bookkeeping -- the step has no prologue launch
+        self.pro_free = bool(stack is not None and ex.denses and ex.routes_ok and tune("pro_free", True))
+        self.srcidx = None
+        if self.pro_free:
+            self.srcidx = torch.zeros(max(bs, 1), dtype=torch.int32, device=ex.device)
+            stack.from_data, stack.training, stack.step_inc = 1, int(training), int(training)
+            stack.srcidx = self.srcidx.data_ptr()
         pa = K.PrologueArgs()
         pa.sb, pa.ga = sb, ga
         pa.gather_gx = 1 if ga.skip_x else K.gather_gx(ga.R)
@@ -598,7 +645,10 @@ class BatchPlan(GeometryMixin):
             pa.gather_blocks = 0
         pa.master = store.master.data_ptr()
         pa.arena = ex.arena.data_ptr()
-        self.launches.append(("prologue", lambda s, a=pa: K.prologue(a, ex.pack_table, s)))
+        if training and ex.routes_ok:
+            pa.pack_mode = 0          # the optimizer writes the packs itself (pack routes)
+        if not self.pro_free:
+            self.launches.append(("prologue", lambda s, a=pa: K.prologue(a, ex.pack_table, s)))
 
         # ---------------- forward convs
         if stack is not None:
@@ -642,6 +692,8 @@ class BatchPlan(GeometryMixin):
             a.NT, a.KS = g.NT, g.KS
             a.splits, a.ks_per_split = splits, kps
             a.part = self.dense_part[g.j].data_ptr()
+            if self.pro_free and g.j == 0 and training:
+                a.book, a.sb = 1, sb      # this step's bookkeeping (the stack read t + 1)
             self.launches.append(("dense_fwd%d" % g.j, lambda s, a=a: K.dense_fwd(a, s)))
             e = K.DenseEpiArgs()
             e.part = a.part
@@ -672,6 +724,8 @@ class BatchPlan(GeometryMixin):
         h.w = store.view(hd.dense, "kernel").data_ptr()
         h.bias = store.view(hd.dense, "bias").data_ptr() if hd.dense.use_bias else 0
         h.y = self.yb.data_ptr() if self.mode != "predict" else 0
+        if self.pro_free and h.y:
+            h.yidx = self.srcidx.data_ptr()      # targets straight from the dataset rows
         h.act = ex.head_act
         if head_epi is not None:
             h.epi = head_epi
@@ -801,6 +855,8 @@ class BatchPlan(GeometryMixin):
                                       "side"))
             else:
                 wa, cfg, slab, bslab = self._wgrad_halo_args(xin, g, bs, cs.conv.use_bias)
+                if g.i == 0 and self.pro_free:      # the images the stack read from the dataset
+                    wa.xidx, wa.xst = self.srcidx.data_ptr(), st_ptr
                 self.launches.append(("wgrad_conv%d" % g.i,
                                       lambda s, a=wa, c=cfg: K.wgrad_halo(a, c[0], c[1], c[2], s), "side"))
             w_at = len(self.launches) - 1
@@ -982,6 +1038,10 @@ class BatchPlan(GeometryMixin):
         """Launch [lo, hi) on the streams ``stream_program`` assigns (concurrent chains that
         join main at the end)."""
         items = self.launches[lo:hi]
+        skip = tune("skip", "")          # timing ablation only (wrong results): "name/name"
+        if skip:
+            drop = set(skip.split("/"))
+            items = [it for it in items if it[0] not in drop]
         tags = [it[2] if len(it) > 2 else "main" for it in items]
         streams = {"main": torch.cuda.current_stream(), "comm": self.comm_stream}
         for op in stream_program(tags, comm=self.comm_stream is not None):

@@ -330,7 +330,7 @@ class GeometryMixin:
         # RPV and MNIST stacks), bounded LDS
         W_in = (g.Wo - 1) * g.stride + g.KW
         px = tune("wgrad_block_px%d" % g.i, tune("wgrad_block_px", 256))
-        R = max(1, min(g.Ho, px // max(1, g.Wo), tune("wgrad_max_rows", 8)))
+        R = max(1, min(g.Ho, px // max(1, g.Wo), tune("wgrad_max_rows%d" % g.i, tune("wgrad_max_rows", 8))))
         # prefer the largest R whose block staging fits the kernel's register pipeline
         # (<= 4 X-halo and 4 dY chunks per thread, wgrad_halo_body.h WH_PX / WH_PY)
         cpp = g.Cs_in // (4 if g.Cs_in == 4 else 8)
@@ -341,7 +341,7 @@ class GeometryMixin:
             nch_y = cdiv(r * g.Wo, 32) * 32 * NTT * 2
             return nch_x <= 1024 and nch_y <= 1024
         for r in range(R, 0, -1):
-            if fits(r):
+            if fits(r) or not tune("wgrad_fit%d" % g.i, True):
                 R = r
                 break
         # LDS layout from the bank-conflict model (pixel / row strides of the X halo, dY rows)
@@ -359,7 +359,8 @@ class GeometryMixin:
         s_budget = max(1, (tune("wgrad_slab_mb", 8) << 20) // per_split_bytes)
         # splits: one round of resident workgroups (occupancy x CUs), not more -- the
         # latency-bound blocks then all stream concurrently instead of a second thin round
-        cap = tune("wgrad_splits", 0) or K.wgrad_halo_resident(a, MT, NTT, bool(bias)) or 768
+        cap = (tune("wgrad_splits%d" % g.i, 0) or tune("wgrad_splits", 0) or K.wgrad_halo_resident(a, MT, NTT, bool(bias))
+               or 768)
         S = max(1, min(nblocks, s_budget, max(1, cap // groups)))
         bps = cdiv(nblocks, S)
         S = cdiv(nblocks, bps)

@@ -42,7 +42,9 @@ def default_timeout_s() -> float:
 
 
 def offset_optim(opt, lo: int):
-    """OptimArgs whose parameter / slot pointers start at flat element ``lo`` (a bucket)."""
+    """OptimArgs whose parameter / slot pointers start at flat element ``lo`` (a bucket);
+    ``opt.lo`` records that start (the kernel's pack routes are in absolute elements)."""
+    opt.lo = lo
     if lo:
         for f in ("p", "s0", "s1"):
             v = getattr(opt, f)

@@ -75,7 +75,7 @@ ALL = [c + (16, 40) for c in CASES] + BENCH_CASES
 def test_conv_forward(kind, drop, cin, hw, n):
     m, ex, bp, wb = _step(kind, drop, cin, hw, n)
     step = int(ex._st_i32[0].item())
-    x = _f(bp.xb).view(bp.bs, ex.in_H, ex.in_W, ex.in_Cs)[..., :ex.in_C]
+    x = _f(bp.step_inputs()[0]).view(bp.bs, ex.in_H, ex.in_W, ex.in_Cs)[..., :ex.in_C]
     for g, cs in zip(ex.convs, ex.plan.convs):
         w = _bf(_w(m, wb, cs.conv, "kernel"))
         b = _w(m, wb, cs.conv, "bias")
@@ -96,7 +96,7 @@ def test_conv_wgrad_and_bias(kind, drop, cin, hw, n):
     m, ex, bp, wb = _step(kind, drop, cin, hw, n)
     for g, cs in zip(ex.convs, ex.plan.convs):
         if g.i == 0:
-            x = _f(bp.xb).view(bp.bs, ex.in_H, ex.in_W, ex.in_Cs)[..., :ex.in_C]
+            x = _f(bp.step_inputs()[0]).view(bp.bs, ex.in_H, ex.in_W, ex.in_Cs)[..., :ex.in_C]
         else:
             pg = ex.convs[g.i - 1]
             x = _f(bp.conv_out[g.i - 1])[..., :pg.Cout]
@@ -136,7 +136,7 @@ def test_dense_and_head(kind, drop, cin, hw, n):
 
     def src_val(src):
         if src.kind == "input":
-            return _f(bp.xb).view(bp.bs, ex.in_H, ex.in_W, ex.in_Cs)[..., :ex.in_C].reshape(bp.bs, -1)
+            return _f(bp.step_inputs()[0]).view(bp.bs, ex.in_H, ex.in_W, ex.in_Cs)[..., :ex.in_C].reshape(bp.bs, -1)
         if src.kind == "conv":
             g = ex.convs[src.idx]
             return _f(bp.conv_out[src.idx])[..., :g.Cout].reshape(bp.bs, -1)
@@ -162,7 +162,7 @@ def test_dense_and_head(kind, drop, cin, hw, n):
     a = src_val(ex.head_src)
     w, b = _w(m, wb, hd.dense, "kernel"), _w(m, wb, hd.dense, "bias")
     z = a @ w + b
-    y = _f(bp.yb)
+    y = _f(bp.step_inputs()[1])
     if hd.activation == "sigmoid":
         _, dz, _ = R.sigmoid_bce(z.reshape(-1), y.reshape(-1))
         dz = dz.reshape(-1, 1)

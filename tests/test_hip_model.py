@@ -362,3 +362,59 @@ def test_nonfinite_loss_reads_nan(kind):
     assert np.isnan(h2.history["loss"][0]) and np.isnan(h2.history["val_loss"][0]), h2.history
     assert np.isnan(figure_of_merit(h2.history["val_loss"]))
     assert figure_of_merit(h.history["val_loss"] + h2.history["val_loss"]) == h.history["val_loss"][0]
+
+
+@pytest.mark.parametrize("kind,drop,cin,hw,opt", [("rpv", 0.2, 3, 64, "Adam"), ("mnist", 0.4, 1, 28, "Nadam"),
+                                                  ("odd", 0.25, 2, 16, "Adadelta")])
+def test_prologue_free_step_matches_prologue(kind, drop, cin, hw, opt, monkeypatch):
+    """The prologue-free step (the conv stack reads its images through the device cursor and
+    permutation, the optimizer writes the bf16 packs through its pack routes, the first dense
+    launch runs the step bookkeeping) trains bit-identically to the step with a prologue
+    launch (gather + re-pack + bookkeeping) -- weights, metrics, iteration count, dropout
+    counters over a multi-step graph -- and leaves the packs equal to a full re-pack."""
+    res = []
+    for tv in ("pro_free=1,opt_packs=1", "pro_free=0,opt_packs=0"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(44)
+        m = _build(kind, "cuda", opt=opt, drop=drop, cin=cin, hw=hw)
+        x, y = _data(m, 320, seed=9)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(5)).to(ex.device)
+        ex.reset_metrics()
+        ex.train_steps(d, perm, 0, 64, 3)
+        ex.train_step(d, perm, 192, 64)
+        torch.cuda.synchronize()
+        names = [it[0] for it in ex._plans[(64, "train")].launches]
+        arena = ex.arena.clone()
+        ex.params_changed()                      # full re-pack from the master
+        torch.cuda.synchronize()
+        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics(), int(m.optimizer.iterations),
+                    names, arena, ex.arena.clone()))
+    (w1, m1, i1, n1, a1, r1), (w0, m0, i0, n0, a0, r0) = res
+    assert "prologue" not in n1 and "prologue" in n0
+    assert torch.equal(w1, w0)
+    assert m1 == m0 and i1 == i0 == 4
+    assert torch.equal(a1, r1), "optimizer-written packs differ from a re-pack of the master"
+    assert torch.equal(r1, r0)     # (a0 is one update behind: the prologue re-packs at step start)
+
+
+def test_optimizer_pack_routes_match_repack():
+    """optim_kernel (the DP path's optimizer) with pack routes writes exactly the bf16 packs a
+    full re-pack of its updated master produces, for a model with conv fwd + dgrad packs
+    and dense fwd + bwd packs (odd channel counts: per-element and float4 route paths)."""
+    set_random_seed(45)
+    m = _build("odd", "cuda", opt="Adam", drop=0.0, cin=2, hw=16)
+    ex = m._executor
+    assert ex.routes is not None
+    g = torch.randn(ex.store.capacity, device=ex.device) * 1e-2
+    ex.store.grad.copy_(g)
+    a = ex._optim_args(False, defer_pack=True)
+    for lo, hi in ((0, ex.store.numel // 3), (ex.store.numel // 3, ex.store.numel)):   # two unaligned ranges
+        a.lo, a.n = lo, hi - lo
+        ex.K.optim(a, ex.pack_table, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    written = ex.arena.clone()
+    ex.params_changed()
+    torch.cuda.synchronize()
+    assert torch.equal(written, ex.arena)
