@@ -58,6 +58,11 @@ struct OptimArgs {
   // weight is also written to its packs (pack_write) and nothing is marked stale
   const PackRoute* routes = nullptr;
   int nroutes = 0;
+  // optim_kernel only: dense routes (identity padding, N % 32 == 0, K % 8 == 0) wholly inside
+  // [lo, lo + n) updated by 2-D tile blocks after the flat blocks (optim_tile_block: whole
+  // 16-byte pack vectors instead of scattered 2-byte stores); the flat blocks skip them
+  int ntile = 0, flat_blocks = 0;
+  int tile_route[4] = {0, 0, 0, 0}, tile_b0[5] = {0, 0, 0, 0, 0};   // tile_b0[ntile] = tile blocks
 };
 
 // Implicit-GEMM convolution / 1x1 "dense as conv" (fwd, dgrad, dense-dX).

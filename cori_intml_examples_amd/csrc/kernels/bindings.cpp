@@ -185,7 +185,12 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(OptimArgs, st) RW(OptimArgs, kind) RW(OptimArgs, beta1) RW(OptimArgs, beta2) RW(OptimArgs, eps)
       RW(OptimArgs, rho) RW(OptimArgs, momentum) RW(OptimArgs, nesterov) RW(OptimArgs, grad_scale)
       RW(OptimArgs, pack_only) RW(OptimArgs, defer_pack) PTR(OptimArgs, arena) PTR(OptimArgs, routes)
-      RW(OptimArgs, nroutes);
+      RW(OptimArgs, nroutes) RW(OptimArgs, ntile) RW(OptimArgs, flat_blocks)
+      .def("set_tile", [](OptimArgs& a, int i, int route, int b0) {
+        if (i < 0 || i > 4) throw std::out_of_range("optim tile index");
+        if (i < 4) a.tile_route[i] = route;
+        a.tile_b0[i] = b0;
+      });
 
   py::class_<PackTable>(m, "PackTable")
       .def(py::init([]() { PackTable t; memset(&t, 0, sizeof(t)); return t; }))

@@ -10,6 +10,8 @@
 //                            Adadelta / RMSprop / SGD with Keras 2.2 math, DP averaging
 //                            folded in (grad_scale), and the bf16 fragment-major weight
 //                            packs the MFMA kernels read scattered out in the same pass
+#include <stdexcept>
+
 #include "args.h"
 #include "optim_math.h"
 #include "reduce_body.h"
@@ -220,11 +222,84 @@ int gather_gx(int R) {
 // The range [lo, lo + n) is processed in aligned float4 groups from lo & ~3; elements of a
 // boundary group outside the range are written back unchanged (no other kernel writes them
 // concurrently: the per-bucket optimizer launches of one step are stream-ordered).
+// One 8(k) x 128(n) tile of a dense route (kind 2, identity padding): wave w updates the
+// 8 x 32 sub-tile at columns 32w.. (lane -> row lane >> 3, 4 columns 4 * (lane & 7)), stages
+// the new bf16 weights in its own LDS slice, then writes whole pack vectors: lanes 0..31 one
+// forward vector each (8 consecutive k of one n: a column of the slice), lanes 32..63 one
+// backward vector each (8 consecutive n of one k: a row segment).  Same per-element math as
+// the flat path (bit-identical weights), 16-byte pack stores.
+template <int KIND>
+__device__ __forceinline__ void optim_tile_block(const OptimArgs& a, int tb, bf16 (*tile)[8][40]) {
+  int i = 0;
+#pragma unroll
+  for (int u = 1; u < 4; ++u)
+    if (u < a.ntile && tb >= a.tile_b0[u]) i = u;
+  const PackRoute R = a.routes[a.tile_route[i]];
+  const int N = R.Cout;
+  const int cbn = (N + 127) >> 7;                     // 128-column blocks per row block
+  const int t = tb - a.tile_b0[i];
+  const int rb = t / cbn, cb = t - rb * cbn;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int col0 = cb * 128 + wave * 32;
+  if (col0 >= N) return;                              // wave-uniform (N % 32 == 0)
+  const int r = lane >> 3, c4 = (lane & 7) * 4;
+  const int row0 = rb * 8;
+  const int e = R.lo + (row0 + r) * N + col0 + c4;
+  float4 p = *reinterpret_cast<const float4*>(a.p + e);
+  const float4 g = *reinterpret_cast<const float4*>(a.g + e);
+  float4 s0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : float4{0.f, 0.f, 0.f, 0.f};
+  float4 s1 = a.s1 ? *reinterpret_cast<const float4*>(a.s1 + e) : float4{0.f, 0.f, 0.f, 0.f};
+  const float gs = a.grad_scale;
+  opt_update<KIND>(a, a.st, p.x, g.x * gs, &s0.x, &s1.x);
+  opt_update<KIND>(a, a.st, p.y, g.y * gs, &s0.y, &s1.y);
+  opt_update<KIND>(a, a.st, p.z, g.z * gs, &s0.z, &s1.z);
+  opt_update<KIND>(a, a.st, p.w, g.w * gs, &s0.w, &s1.w);
+  *reinterpret_cast<float4*>(a.p + e) = p;
+  if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
+  if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
+  bf16 (*sl)[40] = tile[wave];
+  sl[r][c4] = f2bf(p.x);
+  sl[r][c4 + 1] = f2bf(p.y);
+  sl[r][c4 + 2] = f2bf(p.z);
+  sl[r][c4 + 3] = f2bf(p.w);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane < 32) {
+    if (R.fwd >= 0) {   // column lane: k = row0 .. row0+7 (j = 0..7), n = col0 + lane
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = sl[j][lane];
+      *reinterpret_cast<bf16x8*>(a.arena + R.fwd + frag_off(row0, col0 + lane, R.NT)) = v;
+    }
+  } else if (R.bwd >= 0) {   // row (lane-32) >> 2, columns 8 * (lane & 3) ..: k' = n, n' = row
+    const int rr = (lane - 32) >> 2, cc = ((lane - 32) & 3) * 8;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(&sl[rr][cc]);
+    *reinterpret_cast<bf16x8*>(a.arena + R.bwd + frag_off(col0 + cc, row0 + rr, R.NTb)) = v;
+  }
+}
+
+// true when element e lies in a route updated by the tile blocks of this launch
+__device__ __forceinline__ bool in_tiled_route(const OptimArgs& a, int e) {
+  for (int i = 0; i < a.ntile; ++i) {
+    const PackRoute& R = a.routes[a.tile_route[i]];
+    if (e >= R.lo && e < R.hi) return true;
+  }
+  return false;
+}
+
 template <int KIND>
 __global__ __launch_bounds__(256) void optim_kernel(const OptimArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 tile[4][8][40];
+  if (a.ntile && (int)blockIdx.x >= a.flat_blocks) {
+    optim_tile_block<KIND>(a, (int)blockIdx.x - a.flat_blocks, tile);
+    return;
+  }
   const int base = a.lo & ~3, end = a.lo + a.n;
   const int e = base + (blockIdx.x * 256 + threadIdx.x) * 4;
   if (e >= end) return;
+  // (a tiled route starts and ends on multiples of 4: its float4 groups are all-or-nothing)
+  if (a.ntile && in_tiled_route(a, e)) return;
   const StepState* st = a.st;
   float4 p = *reinterpret_cast<const float4*>(a.p + e);
   const float4 g = *reinterpret_cast<const float4*>(a.g + e);
@@ -261,7 +336,9 @@ __global__ __launch_bounds__(256) void optim_kernel(const OptimArgs a) {
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s) {
   if (a.n > 0 && !a.pack_only) {
     const int span = a.lo + a.n - (a.lo & ~3);
-    const dim3 grid(((span + 3) / 4 + 255) / 256);
+    const int flat = ((span + 3) / 4 + 255) / 256;
+    if (a.ntile && a.flat_blocks != flat) throw std::invalid_argument("optim: flat_blocks mismatch");
+    const dim3 grid(flat + (a.ntile ? a.tile_b0[a.ntile] : 0));
     switch (a.kind) {
       case OPT_ADAM: hipLaunchKernelGGL(optim_kernel<OPT_ADAM>, grid, dim3(256), 0, s, a); break;
       case OPT_NADAM: hipLaunchKernelGGL(optim_kernel<OPT_NADAM>, grid, dim3(256), 0, s, a); break;

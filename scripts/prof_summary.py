@@ -5,14 +5,15 @@
 The trace covers warmup, graph capture and the timed steps, so a kernel's call count is
 not a multiple of the timed steps.  Per-step cost is therefore avg_us x launches-per-step,
 where launches-per-step = round(calls / anchor calls) and the anchor is a kernel that runs
-exactly once per training step (default: the prologue kernel).  Kernels that run fewer
+exactly once per training step (default: the head kernel; the prologue-free step has no
+prologue launch).  Kernels that run fewer
 times than the anchor (setup, data generation) are listed but not summed.
 """
 import csv
 import sys
 
 path = sys.argv[1]
-anchor = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].isdigit() else "prologue_kernel"
+anchor = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].isdigit() else "head_kernel"
 rows = list(csv.DictReader(open(path)))
 anchor_calls = max((int(r["Calls"]) for r in rows if anchor in r["Name"]), default=0)
 if anchor_calls == 0:

@@ -399,22 +399,34 @@ def test_prologue_free_step_matches_prologue(kind, drop, cin, hw, opt, monkeypat
     assert torch.equal(r1, r0)     # (a0 is one update behind: the prologue re-packs at step start)
 
 
-def test_optimizer_pack_routes_match_repack():
+@pytest.mark.parametrize("kind,cin,tiled", [("odd", 2, False), ("rpv", 3, False), ("rpv", 3, True)])
+def test_optimizer_pack_routes_match_repack(kind, cin, tiled):
     """optim_kernel (the DP path's optimizer) with pack routes writes exactly the bf16 packs a
-    full re-pack of its updated master produces, for a model with conv fwd + dgrad packs
-    and dense fwd + bwd packs (odd channel counts: per-element and float4 route paths)."""
-    set_random_seed(45)
-    m = _build("odd", "cuda", opt="Adam", drop=0.0, cin=2, hw=16)
-    ex = m._executor
-    assert ex.routes is not None
-    g = torch.randn(ex.store.capacity, device=ex.device) * 1e-2
-    ex.store.grad.copy_(g)
-    a = ex._optim_args(False, defer_pack=True)
-    for lo, hi in ((0, ex.store.numel // 3), (ex.store.numel // 3, ex.store.numel)):   # two unaligned ranges
-        a.lo, a.n = lo, hi - lo
-        ex.K.optim(a, ex.pack_table, torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    written = ex.arena.clone()
-    ex.params_changed()
-    torch.cuda.synchronize()
-    assert torch.equal(written, ex.arena)
+    full re-pack of its updated master produces, for models with conv fwd + dgrad packs and
+    dense fwd + bwd packs: per-element and float4 route paths (odd channel counts, unaligned
+    ranges) and the 2-D tile blocks of a dense route (whole-range launch), whose weights
+    equal the flat path's bit for bit."""
+    outs = []
+    for use_tiles in ((False, True) if tiled else (False,)):
+        set_random_seed(45)
+        m = _build(kind, "cuda", opt="Adam", drop=0.0, cin=cin, hw=16)
+        ex = m._executor
+        assert ex.routes is not None
+        g = torch.randn(ex.store.capacity, generator=torch.Generator().manual_seed(7)) * 1e-2
+        ex.store.grad.copy_(g.to(ex.device))
+        a = ex._optim_args(False, defer_pack=True)
+        ranges = ((0, ex.store.numel),) if use_tiles else ((0, ex.store.numel // 3), (ex.store.numel // 3, ex.store.numel))
+        for lo, hi in ranges:
+            a.lo, a.n = lo, hi - lo
+            if use_tiles:
+                ex.tile_routes(a)
+                assert a.ntile == 1
+            ex.K.optim(a, ex.pack_table, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        written = ex.arena.clone()
+        ex.params_changed()
+        torch.cuda.synchronize()
+        assert torch.equal(written, ex.arena)
+        outs.append(m.store.master.clone())
+    if tiled:
+        assert torch.equal(outs[0], outs[1])
