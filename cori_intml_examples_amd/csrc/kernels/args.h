@@ -304,6 +304,8 @@ struct RedDesc {
   int tpe;             // threads per element (1..256, power of 2): lanes split the S partials
   int blk0;            // first workgroup of this descriptor in the launch
   int vec4;            // 1: identity layout, 4 consecutive elements per thread (float4 traffic)
+  int tile;            // vec4 + a workgroup's 1024 elements are whole 8-row groups (Cout | 128):
+                       // the fused optimizer writes its pack route as whole 16-byte vectors
 };
 
 #define MAX_RED 16

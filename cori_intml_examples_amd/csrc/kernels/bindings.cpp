@@ -249,6 +249,7 @@ PYBIND11_MODULE(_kernels, m) {
         // columns IS the Keras layout: 4 consecutive elements per thread, float4 traffic
         d.vec4 = (type == RED_FLATW && Cin == Cs && ld == Cout && numel % 4 == 0 && dst_off % 4 == 0 &&
                   stride_s % 4 == 0 && S <= 8 && tpe <= 0) ? 1 : 0;
+        d.tile = (d.vec4 && 1024 % Cout == 0 && (1024 / Cout) % 8 == 0 && numel % 1024 == 0) ? 1 : 0;
         // threads per element (power of 2, <= 64): E = 256 / tpe consecutive elements per
         // workgroup keep each slab-row read >= 16 contiguous bytes; each thread sums its
         // S / tpe partials 8 independent loads at a time

@@ -358,7 +358,7 @@ void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s) {
 template <int KIND>
 __global__ __launch_bounds__(256) void reduce_optim_kernel(float* __restrict__ grad, const RedTable tab,
                                                            const OptimArgs a) {
-  __shared__ float red[256];
+  __shared__ __attribute__((aligned(16))) float red[512];   // (>= 2 KB: the tiled pack stage)
   reduce_optim_block<KIND>(grad, tab, a, blockIdx.x, red);
 }
 

@@ -81,6 +81,9 @@ __device__ __forceinline__ int red_desc(const RedTable& tab, int blk) {
   return di;
 }
 
+// first element (flat index) of vec4 table block blk
+__device__ __forceinline__ int e_block0(const RedDesc& d, int blk) { return d.dst_off + (blk - d.blk0) * 1024; }
+
 __device__ __forceinline__ bool slab_reduce_vec4(const RedDesc& d, int blk, int& e, float4& g) {
   const int le = ((blk - d.blk0) * 256 + (int)threadIdx.x) * 4;
   if (le >= d.numel) return false;
@@ -110,6 +113,16 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
   if (dsc.vec4) {
     int e;
     float4 g;
+    // tiled pack writes (dsc.tile): the workgroup's 1024 updated weights are whole 8-row groups
+    // of its dense route -- staged as bf16 in LDS (red: >= 2 KB), written as 16-byte vectors
+    const PackRoute* tr = nullptr;
+    if (a.nroutes && dsc.tile) {
+      for (int r = 0; r < a.nroutes; ++r) {           // uniform: the descriptor's route
+        const PackRoute& R = a.routes[r];
+        if (R.kind == 2 && R.Cin == R.Cs && dsc.dst_off >= R.lo && dsc.dst_off < R.hi) tr = &R;
+      }
+    }
+    bf16* tl = reinterpret_cast<bf16*>(red);
     if (slab_reduce_vec4(dsc, blk, e, g)) {
       *reinterpret_cast<float4*>(grad + e) = g;
       float4 p = *reinterpret_cast<const float4*>(a.p + e);
@@ -123,7 +136,32 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
       *reinterpret_cast<float4*>(a.p + e) = p;
       if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
       if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
-      if (a.nroutes) pack_write4(a, e, p);
+      if (tr) {
+        bf16x4 v;
+        v[0] = f2bf(p.x); v[1] = f2bf(p.y); v[2] = f2bf(p.z); v[3] = f2bf(p.w);
+        *reinterpret_cast<bf16x4*>(tl + 4 * threadIdx.x) = v;
+      } else if (a.nroutes) {
+        pack_write4(a, e, p);
+      }
+    }
+    if (tr) {
+      __syncthreads();
+      const PackRoute R = *tr;
+      const int N = R.Cout, le0 = e_block0(dsc, blk) - R.lo, r0 = le0 / N;
+      const int t = threadIdx.x;
+      if (t < 128) {          // forward: 8 consecutive rows (k) of column n
+        const int gi = t / N, n = t - gi * N;
+        if (R.fwd >= 0) {
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = tl[(gi * 8 + j) * N + n];
+          *reinterpret_cast<bf16x8*>(a.arena + R.fwd + frag_off(r0 + gi * 8, n, R.NT)) = v;
+        }
+      } else if (R.bwd >= 0) {  // backward: 8 consecutive columns (n) of row k
+        const int v8 = t - 128, per = N >> 3, row = v8 / per, c8 = (v8 - row * per) * 8;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(tl + row * N + c8);
+        *reinterpret_cast<bf16x8*>(a.arena + R.bwd + frag_off(c8, r0 + row, R.NTb)) = v;
+      }
     }
   } else {
     int e;
