@@ -407,7 +407,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   const int nv1 = A.n > 1 ? A.L[1].KS * A.L[1].NT * 64 : 0;
   const int nv2 = A.n > 2 ? A.L[2].KS * A.L[2].NT * 64 : 0;
   const int nv3 = A.n > 3 ? A.L[3].KS * A.L[3].NT * 64 : 0;
-  const bool prefetch = !(A.dbg & 8) && A.n > 1 && nv1 + nv2 + nv3 <= PF * STACK_THREADS;
+  const bool prefetch = !(A.dbg & 40) && A.n > 1 && nv1 + nv2 + nv3 <= PF * STACK_THREADS;   // (32: A/B, exact)
   for (int l = 0; l < ((A.dbg & 8) ? 0 : (prefetch ? 1 : A.n)); ++l) {
     const StackLayer& L = A.L[l];
     const int nv = L.KS * L.NT * 64;

@@ -557,7 +557,7 @@ class BatchPlan(GeometryMixin):
                 splits = max(1, min(cdiv(256, K.dense_groups(bs, g.NT, g.KS)), cdiv(g.KS, 8)))
             else:
                 # ~2048 16x16-tile waves: latency-bound small layers want parallelism
-                splits = max(1, min(g.KS, 2048 // max(1, K.dense_groups(bs, g.NT, g.KS))))
+                splits = max(1, min(g.KS, tune("dense_waves", 2048) // max(1, K.dense_groups(bs, g.NT, g.KS))))
             kps = cdiv(g.KS, splits)
             splits = cdiv(g.KS, kps)
             self.dense_splits.append((splits, kps))
@@ -1025,6 +1025,9 @@ class BatchPlan(GeometryMixin):
         # only the FIRST dual launch carries a bucket: every dual launch carrying the previous
         # layer's bucket (conv2's in dual conv1, ...) measured 3% slower on RPV (conv2's
         # many-split slabs stretch dual conv1's tail by ~3 us, more than the reduction sheds)
+        # (the step's last wgrad launch -- the first conv layer's -- carrying the other conv
+        # layers' reductions as extra workgroups measured 2-3 us slower on RPV and MNIST:
+        # profiles/r3_s2_early_wgrad_ab.txt)
         duals = [i for i, nm in enumerate(names) if nm.startswith("wgrad_dgrad_conv")][:1]
         taken = []
         for t in duals:

@@ -296,7 +296,8 @@ class GeometryMixin:
         a.P = P
         tiles = cdiv(a.Ktiles * 16, 128) * cdiv(g.NT, ntc)
         per_split_bytes = a.Ktiles * 16 * g.NT * 16 * 4
-        S = max(1, min(cdiv(1024, tiles), (64 << 20) // per_split_bytes, cdiv(P, 256)))
+        S = max(1, min(cdiv(tune("wgrad_tile_wgs", 1024), tiles), (tune("wgrad_tile_slab_mb", 64) << 20) // per_split_bytes,
+                       cdiv(P, 256)))
         a.px_per_split = cdiv(cdiv(P, S), 64) * 64
         S = cdiv(P, a.px_per_split)
         slab = torch.zeros(S, a.Ktiles * 16, g.NT * 16, dtype=torch.float32, device=dev)

@@ -37,6 +37,7 @@ print("conv_stack: B=%d splits=%d blocks=%d lds_bytes=%d layers=%d" % (a.B, a.sp
 nw = ex.K.STACK_THREADS // 64                 # waves per workgroup (stamp rows per block)
 ts = torch.zeros(nblk * nw * 32, dtype=torch.int64, device=dev)
 a.ts = ts.data_ptr()
+a.dbg = int(os.environ.get("STACK_DBG", "0"))     # timeline of an A/B variant (exact ones: 16, 32)
 for _ in range(20):
     fn(s)
 torch.cuda.synchronize()
@@ -88,12 +89,13 @@ def _t(reps=40):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
-res = {0: [], 16: []}
+a.dbg = 0
+res = {0: [], 16: [], 32: []}
 for _ in range(5):
-    for dbg in (0, 16):
+    for dbg in (0, 16, 32):
         a.dbg = dbg
         _t(5)
         res[dbg].append(_t())
 a.dbg = 0
-print("A/B conv_stack_fwd us: rows path %.2f (min %.2f) | generic %.2f (min %.2f)" % (
-    np.median(res[0]), min(res[0]), np.median(res[16]), min(res[16])))
+print("A/B conv_stack_fwd us: rows path %.2f (min %.2f) | generic %.2f (min %.2f) | no weight prefetch %.2f (min %.2f)"
+      % (np.median(res[0]), min(res[0]), np.median(res[16]), min(res[16]), np.median(res[32]), min(res[32])))
