@@ -25,7 +25,9 @@ def main():
     x, y, _ = synthetic_rpv(512, channels=3, seed=5)
     w0 = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw).get_weights()
     ok = True
-    for label, env in (("single-GPU fused", {}), ("dense opt off", {"INTML_TUNE": "dense_opt=0"}),
+    for label, env in (("single-GPU fused", {}), ("prologue step", {"INTML_TUNE": "pro_free=0"}),
+                       ("prologue re-pack", {"INTML_TUNE": "pro_free=0,opt_packs=0"}),
+                       ("no early reduce", {"INTML_TUNE": "early_reduce=0"}),
                        ("graphs off", {"INTML_GRAPHS": "0"})):
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)

@@ -20,6 +20,7 @@ from cori_intml_examples_amd.apps import zoo  # noqa: E402
 from cori_intml_examples_amd.io.datasets import synthetic_rpv  # noqa: E402
 from cori_intml_examples_amd.parallel import comm as C  # noqa: E402
 from cori_intml_examples_amd.parallel import dist, hvd  # noqa: E402
+from cori_intml_examples_amd.utils import set_random_seed  # noqa: E402
 
 
 def flat(m):
@@ -54,6 +55,11 @@ def main(out):
     x, y, _ = synthetic_rpv(512, channels=3, seed=5)
     np.random.seed(0)
     torch.manual_seed(0)
+    # fixed model seed: the device Glorot init (and so the DP-vs-single distance checked by
+    # the test) is the same in every run -- an unseeded init made the distance vary from
+    # run to run (p999 1e-9 .. 2e-5: Adam amplifies last-ulp gradient differences of the
+    # near-zero-variance weights by different amounts for different initial weights)
+    set_random_seed(1)
     base = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw)
     w0 = base.get_weights()
 
