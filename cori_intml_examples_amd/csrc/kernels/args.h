@@ -104,6 +104,7 @@ struct ConvMMArgs {
   // break the fragment reads' bank conflicts, models/lds_layout.py)
   int xpix = 0;
   int kpipe = 0;                 // software-pipelined k loop with scalar tap offsets (Cs % 32 == 0)
+  int tm = 0;                    // co-scheduled dgrad: m-tiles per wave per pass (0: launch_dual_halo picks)
 };
 
 // Layer-fused forward of a conv stack (conv_stack.hip): one workgroup per image, all

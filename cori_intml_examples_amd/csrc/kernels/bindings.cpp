@@ -90,7 +90,7 @@ PYBIND11_MODULE(_kernels, m) {
       RW(ConvMMArgs, Cs_out) RW(ConvMMArgs, Hp) RW(ConvMMArgs, Wp) PTR(ConvMMArgs, code)
       RW(ConvMMArgs, drop_thr) RW(ConvMMArgs, drop_scale) RW(ConvMMArgs, seed) RW(ConvMMArgs, stream_id)
       PTR(ConvMMArgs, st) RW(ConvMMArgs, bt) RW(ConvMMArgs, R) PTR(ConvMMArgs, in_code) PTR(ConvMMArgs, zero)
-      RW(ConvMMArgs, in_pH) RW(ConvMMArgs, in_pW) RW(ConvMMArgs, dbg) PTR(ConvMMArgs, ts) RW(ConvMMArgs, xpix) RW(ConvMMArgs, kpipe);
+      RW(ConvMMArgs, in_pH) RW(ConvMMArgs, in_pW) RW(ConvMMArgs, dbg) PTR(ConvMMArgs, ts) RW(ConvMMArgs, xpix) RW(ConvMMArgs, kpipe) RW(ConvMMArgs, tm);
 
   py::class_<WgradArgs>(m, "WgradArgs")
       .def(py::init<>())

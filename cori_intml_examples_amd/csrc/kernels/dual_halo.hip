@@ -40,6 +40,7 @@ bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT
     const int load = t * ((ntiles + 4 * t - 1) / (4 * t));   // tiles of the busiest wave
     if (load < best) { best = load; tm = t; }
   }
+  if (ca.tm == 1 || ca.tm == 2 || (ca.tm == 4 && ntc < 8)) tm = ca.tm;   // host override (geometry table)
   switch (ntc) {
     case 1: return dual_launch_n1(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, x, s);
     case 2: return dual_launch_n2(ca, wa, MT, NTT, mtw, tm, wg, cgx, cgy, lds, x, s);

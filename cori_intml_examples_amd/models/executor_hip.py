@@ -913,6 +913,7 @@ class BatchPlan(GeometryMixin):
                 a.mode, a.flat_out = 1, 0
                 a.st = st_ptr
                 a.bt = self._bt_for(Src("conv", prev.i, prev.Cout, prev.Cs_out, prev.Hp, prev.Wp))
+                a.tm = tune("dgrad_tm%d" % g.i, 0)      # co-scheduled dgrad m-tiles per wave per pass
                 dname = "dgrad_conv%d" % g.i
                 dual = (tune("dual_halo", True)
                         and not self._wide(g.Cs_in, g.KS, g.NT) and not self._wide(a.Cs_in, a.KS, g.NTd))

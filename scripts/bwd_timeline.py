@@ -13,12 +13,20 @@ from cori_intml_examples_amd.apps import zoo
 os.environ["INTML_GRAPHS"] = "0"
 dev = torch.device("cuda", 0)
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
-model = zoo.rpv_cnn((64, 64, 3), conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.2, optimizer="Adam",
-                    lr=1e-3, device=dev)
+MODEL = os.environ.get("MODEL", "rpv")
+rs = np.random.RandomState(0)
+if MODEL == "mnist":      # DistTrain_mnist: 28x28x1, conv 32-64 + pool, fc 128, softmax 10
+    model = zoo.mnist_cnn(32, 64, 128, dropout=0.4, optimizer="Adadelta", lr=1.0, input_shape=(28, 28, 1), device=dev)
+    xs = rs.rand(B * 4, 28, 28, 1).astype(np.float32)
+    ys = np.eye(10, dtype=np.float32)[rs.randint(0, 10, B * 4)]
+else:
+    model = zoo.rpv_cnn((64, 64, 3), conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.2, optimizer="Adam",
+                        lr=1e-3, device=dev)
+    xs = rs.rand(B * 4, 64, 64, 3).astype(np.float32)
+    ys = (rs.rand(B * 4) > 0.5).astype(np.float32)
 ex = model._executor
 ex.use_graphs = False
-rs = np.random.RandomState(0)
-d = ex.upload(rs.rand(B * 4, 64, 64, 3).astype(np.float32), (rs.rand(B * 4) > 0.5).astype(np.float32))
+d = ex.upload(xs, ys)
 ex.train_step(d, torch.arange(d.n, device=dev), 0, B)
 torch.cuda.synchronize()
 bp = ex._plans[(B, "train")]
