@@ -15,8 +15,12 @@
 
 __global__ __launch_bounds__(256) void dense_splitk_kernel(const DenseFwdArgs a) {
   // prologue-free step: this step's bookkeeping (no workgroup of this launch reads its
-  // scalars; every later launch of the step does)
-  if (a.book && blockIdx.x == 0 && threadIdx.x == 0) step_bookkeeping(a.sb);
+  // scalars; every later launch of the step does) in an extra LAST workgroup of its own, so
+  // its dependent double-precision chain delays no split-K tile
+  if (a.book && blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x == 0) step_bookkeeping(a.sb);
+    return;
+  }
   dense_splitk_body(a, blockIdx.x);
 }
 
@@ -41,7 +45,10 @@ constexpr long long DL_BIG_BYTES = 8ll << 20;   // weight bytes above which the 
 
 __global__ __launch_bounds__(512) void dense_lds_kernel(const DenseFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (a.book && blockIdx.x == 0 && threadIdx.x == 0) step_bookkeeping(a.sb);   // (as dense_splitk)
+  if (a.book && blockIdx.x == gridDim.x - 1) {   // (as dense_splitk: an extra last workgroup)
+    if (threadIdx.x == 0) step_bookkeeping(a.sb);
+    return;
+  }
   bf16* const As = reinterpret_cast<bf16*>(smem);  // [2][DL_KST][DL_ROWS][DL_LDA]
   constexpr int STG = DL_KST * DL_ROWS * DL_LDA;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
@@ -180,11 +187,11 @@ void launch_dense_fwd(const DenseFwdArgs& a, hipStream_t s) {
   if (dense_big(a.NT, a.KS)) {
     const long long wgs = (long long)dense_groups(a.M, a.NT, a.KS) * a.splits;
     const size_t lds = (size_t)2 * DL_KST * DL_ROWS * DL_LDA * sizeof(bf16);
-    hipLaunchKernelGGL(dense_lds_kernel, dim3((unsigned)wgs), dim3(512), lds, s, a);
+    hipLaunchKernelGGL(dense_lds_kernel, dim3((unsigned)(wgs + (a.book ? 1 : 0))), dim3(512), lds, s, a);
     return;
   }
   const long long waves = (long long)((a.M + 15) / 16) * a.NT * a.splits;
-  hipLaunchKernelGGL(dense_splitk_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(dense_splitk_kernel, dim3((unsigned)((waves + 3) / 4 + (a.book ? 1 : 0))), dim3(256), 0, s, a);
 }
 void launch_dense_epi(const DenseEpiArgs& a, hipStream_t s) {
   const long long n = (long long)a.M * a.Ns;
