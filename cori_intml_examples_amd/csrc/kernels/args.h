@@ -219,7 +219,7 @@ struct DenseFwdArgs {
   int mode = 0;
   const StepState* st = nullptr;
   BwdThrough bt;
-  // book: workgroup 0 runs the step bookkeeping (step_book.h) -- the training step's first
+  // book: an extra last workgroup runs the step bookkeeping (step_book.h) -- the training step's first
   // dense launch takes it over when no prologue launch runs (the conv stack before it reads
   // the iteration count as t + 1, see ConvStackArgs::step_inc)
   int book = 0;
@@ -280,7 +280,7 @@ struct GatherArgs {
 
 // One launch opening every step: batch gather (workgroups [0, gather_blocks)), weight
 // re-pack of the previous update (the rest; pack_mode 1 always, 2 only if st->packs_stale),
-// and the step bookkeeping (workgroup 0).
+// and the step bookkeeping (workgroup 0; in a prologue-free step, an extra workgroup of the first dense launch).
 struct PrologueArgs {
   StepBeginArgs sb;
   GatherArgs ga;

@@ -1,5 +1,5 @@
 // Step bookkeeping (K14 scalars), shared by the prologue kernel (misc.hip) and, in a
-// prologue-free step, workgroup 0 of the step's first dense launch (dense.hip).
+// prologue-free step, an extra last workgroup of the step's first dense launch (dense.hip).
 #pragma once
 #include "args.h"
 
