@@ -35,12 +35,6 @@ PACK_CONV_FWD, PACK_CONV_DGRAD, PACK_DENSE_FWD, PACK_DENSE_BWD = 0, 1, 2, 3
 RED_CONVW, RED_BIAS, RED_FLATW = 0, 1, 2
 
 
-
-
-
-
-
-
 @dataclass
 class Src:
     """An activation buffer feeding the next stage (for flatten mapping / bwd-through)."""
@@ -122,6 +116,31 @@ def splice_bucket_launches(launches, inserts, per_bucket):
         ready[k] = len(out)
     out.extend(launches[pos:])
     return out, ready
+
+
+def defer_after_readers(launches, pattern, spans, readers):
+    """Move each bucket's comm-stream optimizer (launch name ``pattern % k``) behind the
+    last launch that reads a bf16 pack of a parameter in bucket k's span ``spans[k]``.
+
+    The optimizer writes the packs of the weights it updates (pack routes), and a
+    comm-stream launch forks after everything issued on main before it: a bucket whose
+    slabs are final before a later dgrad / dense-dX launch reads the same layer's pack
+    (wide convs have no dual launch, so their dgrad runs after the wgrad) must not update
+    that pack while the reader runs.  ``readers``: [(launch name, param lo, param hi)].
+    Returns the new launch list (the all-reduce stays where it was, so it still overlaps)."""
+    out = list(launches)
+    for k, (lo, hi) in enumerate(spans):
+        names = [it[0] for it in out]
+        name = pattern % k
+        if name not in names:
+            continue
+        at = names.index(name)
+        rd = {rn for rn, rlo, rhi in readers if rlo < hi and rhi > lo}
+        last = max((i for i, n in enumerate(names) if n in rd), default=-1)
+        if last > at:
+            item = out.pop(at)
+            out.insert(last, item)          # (the pop shifted the reader to last - 1)
+    return out
 
 
 def stream_program(tags, comm=True):
@@ -1007,6 +1026,12 @@ class BatchPlan(GeometryMixin):
         self.launches, self.bucket_ready = splice_bucket_launches(
             self.launches, inserts,
             [("reduce_b%d", lambda k: (lambda s: self._launch_bucket_reduce(k, s)), "side")] + extra)
+        if self.comm_in_graph and self.optim_on_comm:
+            # a comm-stream optimizer writes its layers' packs: never while a later
+            # main-stream launch (a wide conv's separate dgrad) still reads one of them
+            self.launches = defer_after_readers(self.launches, "optim_b%d",
+                                                [(lo, hi) for lo, hi, _ in self.bucket_tables],
+                                                self.pack_readers)
         spans = [(lo, hi) for lo, hi, _ in self.bucket_tables]
         spans += [span for _, span in (self.early_red or {}).values()]
         check_bucket_cover(spans, ex.store.numel)
@@ -1052,8 +1077,9 @@ class BatchPlan(GeometryMixin):
         return taken
 
     def _launch_optim_comm(self, k, stream):
-        """Keras update of bucket k's parameters on the comm stream, right after its
-        all-reduce (re-pack deferred to the next prologue)."""
+        """Keras update of bucket k's parameters on the comm stream after its all-reduce;
+        it writes the bf16 packs of the weights it updates (pack routes), so the launch list
+        places it behind the last backward launch reading one of them (defer_after_readers)."""
         ex = self.ex
         lo, hi, _ = self.bucket_tables[k]
         a = ex._optim_args(False, defer_pack=True)   # built at capture time: grad_scale = 1/size

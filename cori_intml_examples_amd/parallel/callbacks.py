@@ -143,16 +143,19 @@ class LearningRateWarmupCallback(Callback):
         self._n = self._spe()
         ex = self.model._executor
         base = getattr(self.model.optimizer, "_base_optimizer", self.model.optimizer)
-        if self.momentum_correction and float(getattr(base, "momentum", 0.0) or 0.0) > 0.0:
-            raise NotImplementedError("LearningRateWarmupCallback(momentum_correction=True) with a momentum "
-                                      "optimizer: pass momentum_correction=False")
         # the ramp is anchored at epoch 0 (as Horovod's, which uses the absolute epoch): a
         # fit() resumed at initial_epoch > 0 continues the ramp where it stands, and one
         # resumed past the warmup window does no warmup at all
         e0 = int(self.params.get("initial_epoch", 0) or 0)
         t0 = int(base.iterations) - e0 * self._n
-        ex.set_lr_warmup(t0, int(round(self.warmup_epochs * self._n)), self._n, dist.size(),
-                         float(self.warmup_epochs), self.initial_lr)
+        window = int(round(self.warmup_epochs * self._n))
+        ramping = window > 0 and e0 * self._n < window
+        if (ramping and self.momentum_correction
+                and float(getattr(base, "momentum", 0.0) or 0.0) > 0.0):
+            # only while the LR actually ramps does momentum correction change anything
+            raise NotImplementedError("LearningRateWarmupCallback(momentum_correction=True) with a momentum "
+                                      "optimizer: pass momentum_correction=False")
+        ex.set_lr_warmup(t0, window, self._n, dist.size(), float(self.warmup_epochs), self.initial_lr)
 
     def on_epoch_end(self, epoch, logs=None):
         if self.warmup_epochs <= 0 or self.initial_lr is None or epoch >= self.warmup_epochs:

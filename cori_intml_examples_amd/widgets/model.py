@@ -33,80 +33,105 @@ import numpy as np
 
 
 class ModelPlotTable:
+    """Per-epoch metric records of one trial.
+
+    Storage is row-major: one tuple per appended record, in the order of ``columns``;
+    a column added later is back-filled with ``None``.  ``rows`` / ``to_dict`` present
+    the column-major view the plot consumes (one list per column)."""
+
     def __init__(self, column_names: Sequence[str]):
-        self._names: List[str] = list(column_names)
-        self._cols: Dict[str, list] = {n: [] for n in self._names}
-        self._n = 0
+        self._order: List[str] = []
+        self._slot: Dict[str, int] = {}
+        self._records: List[tuple] = []
+        for name in column_names:
+            self._add_name(name)
+
+    def _add_name(self, name: str) -> None:
+        if name in self._slot:
+            raise KeyError("duplicate column name %r" % (name,))
+        self._slot[name] = len(self._order)
+        self._order.append(name)
 
     @property
     def columns(self) -> List[str]:
-        return list(self._names)
-
-    @property
-    def rows(self) -> List[list]:
-        """Column-major data (one list per column), as the reference exposes it."""
-        return [self._cols[n] for n in self._names]
+        return list(self._order)
 
     @property
     def num_rows(self) -> int:
-        return self._n
+        return len(self._records)
+
+    def column(self, name: str) -> list:
+        j = self._slot[name]
+        return [rec[j] if j < len(rec) else None for rec in self._records]
+
+    @property
+    def rows(self) -> List[list]:
+        """Column-major view: ``rows[j]`` holds every value of ``columns[j]``."""
+        return [self.column(n) for n in self._order]
 
     def append_column(self, name: str, vals: Optional[Sequence] = None) -> None:
-        if name in self._cols:
-            raise KeyError("column {} is already in this table".format(name))
-        if vals:
-            if len(vals) != self._n:
-                raise ValueError("Number of rows must match table")
-            col = list(vals)
-        else:
-            col = [None] * self._n
-        self._names.append(name)
-        self._cols[name] = col
+        """New column, back-filled from ``vals`` (one per existing record) or with None."""
+        fill = list(vals) if vals is not None and len(vals) else None
+        if fill is not None and len(fill) != len(self._records):
+            raise ValueError("column %r has %d values, table has %d rows" % (name, len(fill), len(self._records)))
+        self._add_name(name)
+        if fill is not None:
+            self._records = [rec + (v,) for rec, v in zip(self._records, fill)]
+        # (without values, older records are shorter than ``columns``: read as None)
 
     def append_row(self, row: Dict[str, Any]) -> None:
-        for n in self._names:
-            self._cols[n].append(row.get(n))
-        self._n += 1
+        """One record; keys that are not columns are ignored, missing columns are None."""
+        self._records.append(tuple(row.get(n) for n in self._order))
 
     def to_dict(self) -> Dict[str, list]:
-        return {n: list(self._cols[n]) for n in self._names}
+        return {n: self.column(n) for n in self._order}
 
 
 class ModelTaskData:
+    """Everything the dashboard knows about one trial: its metric records and its latest
+    status fields, plus a revision count so a renderer can ask what changed since it
+    last looked (``has_updates`` / ``clear_updates``)."""
+
     def __init__(self, plot_columns: Sequence[str], status_columns: Sequence[str]):
-        self._plot_data = ModelPlotTable(plot_columns)
-        self._status_data = {k: None for k in status_columns}
-        self._updated = True
+        self._metric_names = list(plot_columns)
+        self._status_names = list(status_columns)
+        self._table = ModelPlotTable(self._metric_names)
+        self._fields: Dict[str, Any] = dict.fromkeys(self._status_names)
+        self._rev, self._seen = 1, 0
+
+    def _touch(self) -> None:
+        self._rev += 1
 
     @property
     def has_updates(self) -> bool:
-        return self._updated
+        return self._rev != self._seen
 
     def clear_updates(self) -> None:
-        self._updated = False
+        self._seen = self._rev
 
     @property
     def num_data_rows(self) -> int:
-        return self._plot_data.num_rows
+        return self._table.num_rows
 
     def get_plot_data(self) -> Dict[str, list]:
-        return self._plot_data.to_dict()
+        return self._table.to_dict()
 
     def append_plot_data_row(self, d: Dict[str, Any]) -> None:
-        self._plot_data.append_row(d)
-        self._updated = True
+        self._table.append_row(d)
+        self._touch()
 
     def set_status_data(self, d: Dict[str, Any]) -> None:
-        self._status_data.update(d)
-        self._updated = True
+        self._fields.update(d)
+        self._touch()
 
     def get_status_data(self) -> Dict[str, Any]:
-        return dict(self._status_data)
+        return dict(self._fields)
 
     def reset(self) -> None:
-        self._plot_data = ModelPlotTable(self._plot_data.columns)
-        self._status_data = {k: None for k in self._status_data}
-        self._updated = True
+        """Forget the records and status (a restarted trial starts a fresh curve)."""
+        self._table = ModelPlotTable(self._metric_names)
+        self._fields = dict.fromkeys(self._status_names)
+        self._touch()
 
 
 class ModelController:

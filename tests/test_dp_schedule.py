@@ -150,3 +150,43 @@ def test_splice_skips_buckets_a_factory_declines():
     ops = stream_program([o[2] for o in out])
     comm = [out[op[2]][0] for op in ops if op[0] == "run" and op[1] == "comm"]
     assert comm == ["allreduce_b0", "optim_b0"] and ops[-1] == ("wait", "main", "comm")
+
+
+def test_comm_optimizer_waits_for_later_pack_readers():
+    """a comm-stream optimizer writes its layers' bf16 packs, so it must be
+    ordered after every later main-stream launch that reads one of them.  Legacy-shaped step
+    (wide convs: separate dgrad launches after each wgrad), 1 MiB buckets: bucket 1 holds
+    conv3's weights, whose pack dgrad_conv3 reads after the bucket's slabs are final."""
+    from cori_intml_examples_amd.models.executor_hip import defer_after_readers
+    fake = lambda k: (lambda s: None)      # noqa: E731
+    base = [("conv_fwd%d" % i, None, "main") for i in range(4)] + [("head", None, "main"),
+                                                                    ("dense_bwd0", None, "main")]
+    red_ready = [5, 6]
+    for i in (3, 2, 1, 0):
+        base.append(("wgrad_conv%d" % i, None, "side"))
+        red_ready.append(len(base))
+        if i:
+            base.append(("dgrad_conv%d" % i, None, "main"))
+    spans = [(30_000_000, 34_515_201), (20_000_000, 30_000_000), (1_000, 20_000_000), (0, 1_000)]
+    inserts = [(red_ready[0], 0), (red_ready[2], 1), (red_ready[3], 2), (red_ready[5], 3)]
+    per = [("reduce_b%d", fake, "side"), ("allreduce_b%d", fake, "comm"), ("optim_b%d", fake, "comm")]
+    launches, _ = splice_bucket_launches(base, inserts, per)
+    readers = [("dense_bwd0", 30_000_000, 34_515_000), ("dgrad_conv3", 20_000_000, 30_000_000),
+               ("dgrad_conv2", 1_000, 10_000_000), ("dgrad_conv1", 10_000_000, 20_000_000)]
+    before = [l[0] for l in launches]
+    assert before.index("optim_b1") < before.index("dgrad_conv3")        # the race ADVICE found
+    out = defer_after_readers(launches, "optim_b%d", spans, readers)
+    names = [l[0] for l in out]
+    assert sorted(names) == sorted(before)
+    ops, streams, deps = _run(out)
+    for rn, rlo, rhi in readers:
+        for k, (lo, hi) in enumerate(spans):
+            if rlo < hi and rhi > lo:
+                assert _happens_before(streams, deps, rn, "optim_b%d" % k), (rn, k, names)
+    # the all-reduces did not move: bucket 1's still overlaps conv3's dgrad
+    assert names.index("allreduce_b1") < names.index("dgrad_conv3")
+    for k in range(4):
+        assert _happens_before(streams, deps, "allreduce_b%d" % k, "optim_b%d" % k)
+    # nothing to defer: the RPV step's order is unchanged
+    rpv, _, sp = _fake_step()
+    assert defer_after_readers(rpv, "optim_b%d", sp, [("dense_bwd0", 23584, 547712)]) == rpv

@@ -192,6 +192,11 @@ def test_lr_warmup_resume_continues_absolute_ramp():
             m3.fit(x, y, batch_size=16, epochs=1, verbose=0, callbacks=[hcb.LearningRateWarmupCallback(2)])
         m3.fit(x, y, batch_size=16, epochs=1, verbose=0,
                callbacks=[hcb.LearningRateWarmupCallback(2, momentum_correction=False)])
+        # no ramp -> nothing for momentum correction to do: warmup_epochs=0 (what
+        # apps.rpv.train_model always adds) and a resume past the window both train
+        m3.fit(x, y, batch_size=16, epochs=1, verbose=0, callbacks=[hcb.LearningRateWarmupCallback(0)])
+        m3.fit(x, y, batch_size=16, epochs=3, initial_epoch=2, verbose=0,
+               callbacks=[hcb.LearningRateWarmupCallback(2)])
     finally:
         dist.size = orig
     for a, b in zip(wa, wb):
