@@ -33,7 +33,8 @@ and is timed while the engines idle, the data-parallel group shuts down, and the
 runs the DistHPO_mnist random search (``DistHPO_mnist.ipynb:137-255``: 64 trials, 16 epochs,
 60k samples, valid_frac 0.17, batch 128, load-balanced over the engines), capped at
 ``--hpo-budget`` seconds including engine start-up (a capped run reports the trials it
-finished).  ``--no-hpo`` skips it.
+finished), and then BASELINE config 5 as ``"hpo_rpv"``: DistWidgetHPO_rpv's 8 concurrent RPV
+trials monitored live by the dashboard model (``InlineHpo``).  ``--no-hpo`` skips both.
 """
 from __future__ import annotations
 
@@ -245,57 +246,159 @@ def run_hpo(args, extra):
 
 
 class InlineHpo:
-    """The DistHPO_mnist random search on a task farm, started before the training bench
-    touches the GPU and run after it (see the module docstring)."""
+    """The HPO records of the JSON line, on ONE task farm started before the training bench
+    touches the GPU and used after it (see the module docstring):
+
+    * ``hpo``      DistHPO_mnist random search: 64 trials (16 epochs, 60k, valid_frac 0.17,
+                   B=128) load-balanced over ``engines_per_gpu`` engines of every GPU;
+    * ``hpo_rpv``  DistWidgetHPO_rpv (BASELINE config 5): 8 CONCURRENT RPV trials of the
+                   notebook's search space (``DistWidgetHPO_rpv.ipynb:113-125``: conv / fc /
+                   lr / dropout / optimizer, B=64, 2 epochs, 64k train / 32k valid) through
+                   ``apps.rpv.train_model`` with an ``IPyParallelLogger`` each, monitored live
+                   by the headless dashboard model (``widgets.ParamSpanModel.poll``, the
+                   ParamSpanWidget's update loop) -- trials/hour plus the publish -> dashboard
+                   latency of the epoch messages.
+    Both data sets carry 10 % flipped labels (benchmarks/hpo_throughput.LABEL_NOISE)."""
 
     TRIALS, EPOCHS, SAMPLES, BATCH, VALID_FRAC = 64, 16, 60000, 128, 0.17
+    RPV_TRIALS, RPV_EPOCHS, RPV_TRAIN, RPV_VALID, RPV_BATCH = 8, 2, 64000, 32000, 64
 
-    def __init__(self, engines_per_gpu: int, budget_s: float):
+    def __init__(self, engines_per_gpu: int, budget_s: float, rpv_budget_s: float = 60.0):
         from cori_intml_examples_amd import farm
         self.t0 = time.time()
         self.budget_s = budget_s
+        self.rpv_budget_s = rpv_budget_s
         self.n_gpu = farm.detect_gpus()
-        self.engines = max(1, self.n_gpu) * engines_per_gpu
+        g = max(1, self.n_gpu)
+        self.epg = engines_per_gpu
+        # enough engines for the 8 concurrent RPV trials on any GPU count (engine e sits on
+        # GPU e % n_gpu: the first epg * n_gpu engines are the MNIST search's)
+        self.engines = g * max(engines_per_gpu, -(-self.RPV_TRIALS // g))
         self.cl = farm.start_cluster(self.engines, cluster_id="bench_hpo_%d" % os.getpid(),
                                      cpu_only=self.n_gpu == 0, timeout=min(120.0, budget_s))
         self.startup_s = time.time() - self.t0
 
     def run(self):
+        out = {}
+        try:
+            with self.cl.client() as c:
+                out["hpo"] = self._mnist(c)
+                try:
+                    out["hpo_rpv"] = self._rpv(c)
+                except Exception as e:     # noqa: BLE001 -- the MNIST record must survive
+                    out["hpo_rpv"] = {"error": str(e)[:300]}
+        finally:
+            self.cl.stop()
+        return out
+
+    def _mnist(self, c):
         import cloudpickle
         sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
         import hpo_throughput
         from cori_intml_examples_amd.hpo import random_search as rs
         cloudpickle.register_pickle_by_value(hpo_throughput)
         t1 = time.time()
-        capped, done = False, []
-        try:
-            with self.cl.client() as c:
-                trials = rs.mnist_trials(self.TRIALS)
-                ars = rs.submit_trials(c.load_balanced_view(), hpo_throughput.trial_mnist, trials,
-                                       n_train=self.SAMPLES, batch_size=self.BATCH, n_epochs=self.EPOCHS,
-                                       valid_frac=self.VALID_FRAC)
-                deadline = t1 + max(1.0, self.budget_s - self.startup_s)
-                while not all(a.ready() for a in ars) and time.time() < deadline:
-                    time.sleep(0.25)
-                t2 = time.time()
-                capped = not all(a.ready() for a in ars)
-                done = [r for r in rs.collect([a for a in ars if a.ready()]) if r]
-                for a in ars:
-                    if not a.ready():
-                        a.abort()
-        finally:
-            self.cl.stop()
+        g = max(1, self.n_gpu)
+        view = c.load_balanced_view(targets=list(range(self.epg * g)))
+        trials = rs.mnist_trials(self.TRIALS)
+        ars = rs.submit_trials(view, hpo_throughput.trial_mnist, trials, n_train=self.SAMPLES,
+                               batch_size=self.BATCH, n_epochs=self.EPOCHS, valid_frac=self.VALID_FRAC)
+        deadline = t1 + max(1.0, self.budget_s - self.startup_s)
+        while not all(a.ready() for a in ars) and time.time() < deadline:
+            time.sleep(0.25)
+        t2 = time.time()
+        capped = not all(a.ready() for a in ars)
+        done = [r for r in rs.collect([a for a in ars if a.ready()]) if r]
+        for a in ars:
+            if not a.ready():
+                a.abort()
         wall = self.startup_s + (t2 - t1)
         best = min((min(r["val_loss"]) for r in done), default=None)
         return {"metric": "HPO trials/hour (DistHPO_mnist random search)",
                 "trials_per_hour": round(len(done) / wall * 3600, 1), "trials_done": len(done),
                 "trials_submitted": self.TRIALS, "capped": capped, "n_gpus": self.n_gpu,
-                "engines_per_gpu": self.engines // max(1, self.n_gpu), "epochs": self.EPOCHS,
+                "engines_per_gpu": self.epg, "epochs": self.EPOCHS,
                 "samples": self.SAMPLES, "valid_frac": self.VALID_FRAC, "batch": self.BATCH,
                 "wall_s": round(wall, 2), "startup_s": round(self.startup_s, 2),
                 "mean_trial_s": round(sum(r["t1"] - r["t0"] for r in done) / max(1, len(done)), 3),
                 "best_val_loss": best, "budget_s": self.budget_s,
-                "data": "synthetic MNIST (60k) generated on each engine GPU by the K16 kernel, resident; random-init weights"}
+                "label_noise": hpo_throughput.LABEL_NOISE,
+                "data": "synthetic MNIST (60k, 10% flipped labels) generated on each engine GPU by the K16 "
+                        "kernel, resident; random-init weights"}
+
+    def _rpv(self, c):
+        import functools
+        import numpy as np
+        sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+        import hpo_throughput
+        from cori_intml_examples_amd.hpo import random_search as rs
+        from cori_intml_examples_amd.widgets.model import ModelController, ParamSpanModel
+        trials = rs.rpv_trials(self.RPV_TRIALS)            # DistWidgetHPO_rpv.ipynb:113-125, seed 0
+        params = {k: [t[k] for t in trials] for k in ("conv_sizes", "fc_sizes", "dropout", "optimizer", "lr")}
+        fn = functools.partial(hpo_throughput.trial_rpv_widget, n_train=self.RPV_TRAIN, n_valid=self.RPV_VALID,
+                               batch_size=self.RPV_BATCH, n_epochs=self.RPV_EPOCHS)
+        ctl = ModelController(client=c, view=c.load_balanced_view(targets=list(range(self.RPV_TRIALS))))
+        psm = ParamSpanModel(fn, params, controller=ctl)
+        seen = {}                                           # (row, epoch) -> first time on the dashboard
+
+        def on_change(what, i):
+            if what == "row":
+                now = time.time()
+                for e in range(psm.data[i].num_data_rows):
+                    seen.setdefault((i, e), now)
+
+        psm.listeners.append(on_change)
+        t1 = time.time()
+        psm.submit_computations(poll=False)
+        deadline = t1 + self.rpv_budget_s
+        polls = 0
+        while time.time() < deadline:
+            psm.poll()
+            polls += 1
+            if not ctl.get_running_models():
+                break
+            time.sleep(0.02)
+        t2 = time.time()
+        futs = psm.results
+        capped = not all(f is not None and f.ready() for f in futs)
+        done = []
+        for f in futs:
+            if f is not None and f.ready():
+                try:
+                    done.append(f.get())
+                except Exception:   # noqa: BLE001
+                    pass
+            elif f is not None:
+                f.abort()
+        lat = []
+        for i, f in enumerate(futs):
+            if f is None or not f.ready():
+                continue
+            try:
+                r = f.get()
+            except Exception:       # noqa: BLE001
+                continue
+            for status, epoch, tp in r["published"]:
+                if status == "Ended Epoch" and (i, epoch) in seen:
+                    lat.append(seen[(i, epoch)] - tp)
+        wall = t2 - t1
+        best = min((min(r["val_loss"]) for r in done), default=None)
+        return {"metric": "HPO trials/hour (DistWidgetHPO_rpv: %d concurrent RPV trials, live dashboard)"
+                          % self.RPV_TRIALS,
+                "trials_per_hour": round(len(done) / wall * 3600, 1), "trials_done": len(done),
+                "trials_submitted": self.RPV_TRIALS, "capped": capped, "n_gpus": self.n_gpu,
+                "engines_per_gpu": -(-self.RPV_TRIALS // max(1, self.n_gpu)), "concurrent": self.RPV_TRIALS,
+                "epochs": self.RPV_EPOCHS, "n_train": self.RPV_TRAIN, "n_valid": self.RPV_VALID,
+                "batch": self.RPV_BATCH, "wall_s": round(wall, 2),
+                "mean_trial_s": round(sum(r["t1"] - r["t0"] for r in done) / max(1, len(done)), 3),
+                "best_val_loss": best, "dashboard_polls": polls,
+                "publish_to_dashboard_ms_p50": round(float(np.median(lat)) * 1e3, 2) if lat else None,
+                "publish_to_dashboard_ms_max": round(float(np.max(lat)) * 1e3, 2) if lat else None,
+                "epoch_messages_seen": len(lat),
+                "dashboard_rows_final": [int(psm.data[i].num_data_rows) for i in range(psm.n_models)],
+                "label_noise": hpo_throughput.LABEL_NOISE,
+                "data": "synthetic RPV (1-channel 64x64, 10% flipped labels) generated on each engine GPU by the "
+                        "K16 kernel, resident; random-init weights"}
 
     def stop(self):
         try:
@@ -440,13 +543,13 @@ def main():
     value = size * B * steps / elapsed
     # every rank leaves the data-parallel group; rank 0 then runs the HPO on the farm
     hvd.shutdown()
-    hpo_rec = None
+    hpo_recs = None
     if inline_hpo is not None:
         try:
-            hpo_rec = inline_hpo.run()
+            hpo_recs = inline_hpo.run()
         except Exception as e:   # noqa: BLE001
             inline_hpo.stop()
-            hpo_rec = {"error": str(e)[:300]}
+            hpo_recs = {"hpo": {"error": str(e)[:300]}}
     if rank == 0:
         out = {"metric": metric,
                "value": round(value, 1), "unit": "images/s", "n_gpus": size, "steps": steps,
@@ -465,8 +568,8 @@ def main():
             out["config"]["lr_warmup_epochs"] = args.lr_warmup_epochs
         if selfcheck is not None:
             out["selfcheck"] = selfcheck
-        if hpo_rec is not None:
-            out["hpo"] = hpo_rec
+        if hpo_recs is not None:
+            out.update(hpo_recs)
         print(json.dumps(out), flush=True)
     if not ok:
         print("bench self-check FAILED: %s" % json.dumps(selfcheck), file=sys.stderr, flush=True)

@@ -28,6 +28,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 REF_EVALS_PER_HOUR = 128 / (3 * 3600 + 6 * 60 + 36) * 3600     # 41.2
+# flipped labels in every synthetic HPO data set: the tasks are not separable, so trials end
+# at different val_loss above a ~H(0.1) floor and "best trial" is a real choice (the clean
+# synthetic MNIST reached val_loss 1e-5 in round 3's driver run)
+LABEL_NOISE = 0.1
 
 
 def _cache():
@@ -50,8 +54,8 @@ def trial(conv_sizes, fc_sizes, lr, dropout, optimizer, n_train=64000, n_valid=3
     _CACHE = _cache()
     key = (n_train, n_valid, channels)
     if key not in _CACHE:
-        _CACHE[key] = (synth.for_model(model, "rpv", n_train, seed=1),
-                       synth.for_model(model, "rpv", n_valid, seed=2))
+        _CACHE[key] = (synth.flip_labels(synth.for_model(model, "rpv", n_train, seed=1), LABEL_NOISE, 101),
+                       synth.flip_labels(synth.for_model(model, "rpv", n_valid, seed=2), LABEL_NOISE, 102))
     tr, va = _CACHE[key]
     t1 = _t.time()
     h = model.fit(tr, None, batch_size=batch_size, epochs=n_epochs, validation_data=(va, None), verbose=0)
@@ -69,12 +73,50 @@ def trial_mnist(h1, h2, h3, dropout, optimizer, n_train=60000, batch_size=128, n
     _CACHE = _cache()
     key = ("mnist", n_train)
     if key not in _CACHE:      # generated on the engine's GPU (K16 synth kernel), resident
-        _CACHE[key] = synth.for_model(model, "mnist", n_train, seed=1)
+        _CACHE[key] = synth.flip_labels(synth.for_model(model, "mnist", n_train, seed=1), LABEL_NOISE, 103)
     data = _CACHE[key]
     t1 = _t.time()
     h = model.fit(data, None, batch_size=batch_size, epochs=n_epochs, validation_split=valid_frac, verbose=0)
     return {"val_loss": h.history["val_loss"], "data_s": t1 - t0, "train_s": _t.time() - t1,
             "device": str(model.device), "t0": t0, "t1": _t.time()}
+
+
+def trial_rpv_widget(conv_sizes, fc_sizes, dropout, optimizer, lr, n_train=64000, n_valid=32000, batch_size=64,
+                     n_epochs=2, channels=1):
+    """DistWidgetHPO_rpv's build_and_train (``DistWidgetHPO_rpv.ipynb:160-168``): the RPV recipe
+    (``apps.rpv.build_model`` / ``train_model``) with an ``IPyParallelLogger`` publishing
+    every epoch to the dashboard, on cached synthetic RPV with label noise.  The logger also
+    records when it published each message (same host clock as the polling client), so the
+    driver can measure publish -> dashboard latency."""
+    import time as _t
+    t0 = _t.time()
+    from cori_intml_examples_amd.apps.mlextras import IPyParallelLogger
+    from cori_intml_examples_amd.apps.rpv import build_model, train_model
+    from cori_intml_examples_amd.io import synth
+
+    class StampedLogger(IPyParallelLogger):
+        def __init__(self):
+            super().__init__()
+            self.published = []          # (status, epoch, wall time)
+
+        def _pub(self, status, epoch=None):
+            super()._pub(status, epoch)
+            self.published.append((status, epoch, _t.time()))
+
+    model = build_model((64, 64, channels), conv_sizes=conv_sizes, fc_sizes=fc_sizes, dropout=dropout,
+                        optimizer=optimizer, lr=lr)
+    _CACHE = _cache()
+    key = ("rpvw", n_train, n_valid, channels)
+    if key not in _CACHE:
+        _CACHE[key] = (synth.flip_labels(synth.for_model(model, "rpv", n_train, seed=1), LABEL_NOISE, 101),
+                       synth.flip_labels(synth.for_model(model, "rpv", n_valid, seed=2), LABEL_NOISE, 102))
+    tr, va = _CACHE[key]
+    logger = StampedLogger()
+    t1 = _t.time()
+    h = train_model(model, tr, None, va, None, batch_size=batch_size, n_epochs=n_epochs, verbose=0,
+                    callbacks=[logger])
+    return {"val_loss": h.history["val_loss"], "data_s": t1 - t0, "train_s": _t.time() - t1,
+            "published": logger.published, "device": str(model.device), "t0": t0, "t1": _t.time()}
 
 
 def run_cray(a, n_gpu):

@@ -143,3 +143,30 @@ def split(data, frac: float):
     from ..models.executor_base import DeviceData
     s = int(data.n * (1.0 - frac))
     return (DeviceData(data.x[:s], data.y[:s], s), DeviceData(data.x[s:], data.y[s:], data.n - s))
+
+
+S_FLIP, S_RELABEL = 12, 13
+
+
+def flip_labels(data, frac: float, seed: int, first: int = 0):
+    """Label noise in place: each sample ``i`` (counted from ``first``) keeps its label unless
+    ``u01(rng(i, seed)) < frac``; a flipped binary label becomes ``1 - y``, a flipped one-hot
+    class moves to a uniformly drawn OTHER class.  Pure integer hashing (ops/rng), so the
+    device and CPU data sets agree bit for bit.  Makes the synthetic tasks non-separable: the
+    best trial of an HPO sits above the ~H(frac) noise floor instead of at 1e-5, so choosing
+    it means something (tests/test_convergence.py uses the same 10 %)."""
+    if frac <= 0:
+        return data
+    y = data.y
+    dev = y.device
+    i = (torch.arange(first, first + data.n, dtype=torch.int64, device=dev)) & _M32
+    flip = u01_of(rng_u32(i, seed & _M32, S_FLIP, 0)) < _f(frac).to(dev)
+    ncls = y.shape[1]
+    if ncls == 1:
+        y[:, 0] = torch.where(flip, 1.0 - y[:, 0], y[:, 0])
+    else:
+        cls = y.argmax(1)
+        new = (cls + 1 + uint_below(rng_u32(i, seed & _M32, S_RELABEL, 0), ncls - 1)) % ncls
+        cls = torch.where(flip, new, cls)
+        y.copy_(torch.nn.functional.one_hot(cls, ncls).to(y.dtype))
+    return data

@@ -150,15 +150,25 @@ class NativeComm:
             self._c = None
 
 
-def comm_mode(use_gpu: bool, backend: Optional[str]) -> str:
-    """'native' (RCCL engine + gloo control plane) or 'torch' (torch.distributed only).
+def comm_mode(use_gpu: bool, backend: Optional[str], local_size: Optional[int] = None,
+              n_devices: Optional[int] = None) -> str:
+    """'native' (RCCL engine + gloo control plane), 'xgmi' (NO RCCL communicator: the fused
+    xGMI all-reduce + optimizer kernel is the data plane, gloo the control plane) or 'torch'
+    (torch.distributed only).
 
-    ``INTML_COMM=torch`` forces the torch.distributed data plane; an explicit
-    ``INTML_DP_BACKEND``/``backend`` (e.g. gloo for 2 ranks sharing one GPU in tests)
-    also keeps the torch path."""
+    ``INTML_COMM=torch`` forces the torch.distributed data plane and ``INTML_COMM=xgmi`` the
+    RCCL-free one; an explicit ``INTML_DP_BACKEND``/``backend`` keeps the torch path.  With
+    more ranks on this node than GPUs (ranks sharing a GPU: nested HPO x DP evaluations on
+    one card, the one-GPU rehearsal of the 8-GPU step) RCCL refuses to build a communicator,
+    so the native mode becomes 'xgmi': its protocol does not care whether a peer's inbox is
+    on this GPU or another."""
     mode = os.environ.get("INTML_COMM", "native").lower()
     if not use_gpu or mode == "torch" or backend or os.environ.get("INTML_DP_BACKEND"):
         return "torch"
+    if mode == "xgmi":
+        return "xgmi"
+    if local_size is not None and n_devices and local_size > n_devices:
+        return "xgmi"
     if not available():
         raise RuntimeError("INTML_COMM=native but the _comm extension is not built "
                            "(python -m cori_intml_examples_amd._build); set INTML_COMM=torch to "

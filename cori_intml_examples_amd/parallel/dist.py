@@ -57,16 +57,17 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
     force = os.environ.get("INTML_DP_FORCE", "0") not in ("0", "", "false", "False")
     use_gpu = torch.cuda.is_available() and os.environ.get("INTML_DEVICE", "cuda").startswith("cuda")
     timeout_s = float(os.environ.get("INTML_DP_TIMEOUT", 600))
-    owns, comm = False, None
+    owns, comm, xgmi_only = False, None, False
     if tdist.is_available() and tdist.is_initialized():
         world, rank = tdist.get_world_size(), tdist.get_rank()
         be = tdist.get_backend()
     elif world > 1:
         from . import comm as C
-        mode = C.comm_mode(use_gpu, backend)
+        mode = C.comm_mode(use_gpu, backend, local_size, torch.cuda.device_count() if use_gpu else 0)
         be = backend or os.environ.get("INTML_DP_BACKEND") or ("nccl" if use_gpu else "gloo")
-        if mode == "native":
-            be = "gloo"                  # control plane only; RCCL is driven natively
+        if mode in ("native", "xgmi"):
+            be = "gloo"                  # control plane only; the data plane is native
+        xgmi_only = mode == "xgmi"
         if use_gpu:
             torch.cuda.set_device(local_rank % torch.cuda.device_count())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -87,7 +88,7 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
                 be = "rccl"
     st = S.DPState(rank=rank, size=world, local_rank=local_rank, local_size=local_size,
                    backend=be, shard_data=shard_data, bucket_bytes=bucket_bytes, owns_pg=owns,
-                   comm=comm)
+                   comm=comm, xgmi_only=xgmi_only)
     S.set_state(st)
     return st
 
@@ -380,14 +381,19 @@ class NativeGradReducer:
     (fp32 -> bf16 staging copy, bf16 all-reduce, copy back), all on the comm stream."""
     capturable = True
 
-    def __init__(self, store, comm, compression=None, bucket_bytes: int = 1 << 20):
+    def __init__(self, store, comm, compression=None, bucket_bytes: int = 1 << 20,
+                 rank: Optional[int] = None, size: Optional[int] = None, device=None):
         self.store, self.comm = store, comm
         self.compression = compression
         self.bucket_bytes = bucket_bytes
-        self.size = comm.size
+        # comm None: the RCCL-free data plane (state.xgmi_only) -- the whole gradient is ONE
+        # bucket through the fused xGMI kernel, rank / size from the control plane
+        self.rank = comm.rank if comm is not None else int(rank)
+        self.size = comm.size if comm is not None else int(size)
+        self.device = comm.device if comm is not None else device
         self.buckets: List[Tuple[int, int]] = [(0, store.numel)]
         self.bucket_groups: List[List[int]] = [[0]]
-        self.stream = torch.cuda.Stream(device=comm.device)   # for the segmented (uncaptured) mode
+        self.stream = torch.cuda.Stream(device=self.device)   # for the segmented (uncaptured) mode
         self._stage = {}
         self._configured = False
         self.xgmi = None               # parallel.xgmi.XgmiAllreduce when the fused path is on
@@ -400,7 +406,7 @@ class NativeGradReducer:
         return True
 
     def configure(self, groups: Sequence[Tuple[int, int]]) -> List[List[int]]:
-        self.plane = data_plane()
+        self.plane = data_plane() if self.comm is not None else "xgmi"
         bb = self.bucket_bytes
         if self.plane == "xgmi":
             bb = 1 << 62                    # the whole gradient is ONE fused xGMI bucket
@@ -416,7 +422,7 @@ class NativeGradReducer:
         if self.compression == "bf16":
             for k, (lo, hi) in enumerate(self.buckets):
                 if k != self.xgmi_bucket:
-                    self._stage[k] = torch.empty(hi - lo, dtype=torch.bfloat16, device=self.comm.device)
+                    self._stage[k] = torch.empty(hi - lo, dtype=torch.bfloat16, device=self.device)
         return self.bucket_groups
 
     def _setup_xgmi(self):
@@ -426,7 +432,9 @@ class NativeGradReducer:
         RCCL) while the earlier ones stay on RCCL, forked onto the comm stream so they overlap
         the conv backward.  fp32 wire only; collective setup + self-test, same decision on
         every rank (else every bucket stays on RCCL)."""
-        want = self.plane in ("xgmi", "hybrid") and self.compression is None
+        # (without an RCCL communicator the wire is always fp32 xGMI: Compression.fp16 is
+        # a bandwidth option, the result is the fp32 all-reduce either way)
+        want = self.plane in ("xgmi", "hybrid") and (self.compression is None or self.comm is None)
         k = len(self.buckets) - 1 if want else None
         n = (self.buckets[k][1] - self.buckets[k][0]) if want else 0
         if self.xgmi is not None and (not want or self.xgmi.n != n):
@@ -435,11 +443,14 @@ class NativeGradReducer:
         self.xgmi_bucket = None
         if want and self.xgmi is None:
             from . import xgmi as X
-            self.xgmi = X.create(self.comm.rank, self.size, n, self.comm.device, allgather)
+            self.xgmi = X.create(self.rank, self.size, n, self.device, allgather)
             if self.xgmi is not None:
                 self._xgmi_err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
         if self.xgmi is not None:
             self.xgmi_bucket = k
+        elif self.comm is None:
+            raise RuntimeError("data parallel without RCCL (INTML_COMM=xgmi, or ranks sharing a GPU): the "
+                               "fused xGMI all-reduce failed its collective setup / self-test (see stderr)")
 
     def launch_fused(self, grad: torch.Tensor, opt_args, stream: int) -> None:
         """The fused all-reduce + optimizer of the xGMI bucket (capturable); ``opt_args``
@@ -451,6 +462,10 @@ class NativeGradReducer:
     def launch(self, bucket: int, grad: torch.Tensor, stream: torch.cuda.Stream) -> None:
         """Enqueue bucket ``bucket``'s all-reduce on ``stream`` (capturable)."""
         lo, hi = self.buckets[bucket]
+        if bucket == self.xgmi_bucket:      # segmented mode: the fused kernel as a plain all-reduce
+            self.xgmi.launch(grad.data_ptr() + 4 * lo, stream.cuda_stream if hasattr(stream, "cuda_stream")
+                             else stream)
+            return
         view = grad[lo:hi]
         buf = self._stage.get(bucket)
         if buf is None:
@@ -475,7 +490,8 @@ class NativeGradReducer:
     def after_step(self) -> None:
         """Watchdog marker after a step (raises if a peer failed / RCCL reported an error);
         with the xGMI path, the error word of an earlier launch (async copy, no sync)."""
-        self.comm.mark()
+        if self.comm is not None:
+            self.comm.mark()
         if self.xgmi is not None:
             if int(self._xgmi_err_host[0]):
                 from . import xgmi as X
@@ -496,6 +512,10 @@ def make_reducer(executor, optimizer):
     st = _st()
     bb = getattr(optimizer, "bucket_bytes", None) or st.bucket_bytes
     comp = getattr(optimizer, "compression", None)
-    if st.comm is not None and getattr(executor.store, "device", torch.device("cpu")).type == "cuda":
+    on_gpu = getattr(executor.store, "device", torch.device("cpu")).type == "cuda"
+    if on_gpu and st.comm is not None:
         return NativeGradReducer(executor.store, st.comm, comp, bb)
+    if on_gpu and st.xgmi_only and st.size > 1:
+        return NativeGradReducer(executor.store, None, comp, bb, rank=st.rank, size=st.size,
+                                 device=executor.store.device)
     return GradReducer(executor.store, comp, bb)

@@ -16,6 +16,7 @@ class DPState:
     bucket_bytes: Optional[int] = None   # None: adaptive (dist.adaptive_bucket_bytes)
     owns_pg: bool = False
     comm: Any = None              # parallel.comm.NativeComm (RCCL data plane) or None
+    xgmi_only: bool = False       # no RCCL communicator: the fused xGMI kernel is the data plane
 
 
 _STATE: Optional[DPState] = None

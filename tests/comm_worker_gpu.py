@@ -118,6 +118,35 @@ def main(out):
     w = train(m)
     step = np.linalg.norm(wb - np.concatenate([a.reshape(-1) for a in w0]))
     results["bf16_wire"] = {"rel_diff": float(np.linalg.norm(w - wb) / max(step, 1e-30))}
+    # legacy model (wide convs: each layer's dgrad is a separate launch AFTER its wgrad) with
+    # 1 MiB buckets: every bucket's optimizer runs on the comm stream and writes its layers'
+    # packs, so it must wait for the dgrad that reads them (defer_after_readers)
+    set_random_seed(2)
+    lkw = dict(device="cuda:0", lr=1e-4)
+    lb = zoo.rpv_legacy_cnn((64, 64, 3), use_horovod=False, **lkw)
+    lw0 = lb.get_weights()
+
+    def train_l(m):
+        for i in range(3):
+            m.train_on_batch(x[i * 32:(i + 1) * 32], y[i * 32:(i + 1) * 32])
+        torch.cuda.synchronize()
+        return flat(m)
+
+    wlb = train_l(lb)
+    lm = zoo.rpv_legacy_cnn((64, 64, 3), use_horovod=False, **lkw)
+    lm.compile(optimizer=hvd.DistributedOptimizer("Adam", bucket_bytes=1 << 20), loss="binary_crossentropy",
+               metrics=["accuracy"])
+    lm.set_weights(lw0)
+    wl = train_l(lm)
+    plan = next(iter(lm._executor._plans.values()))
+    names = [it[0] for it in plan.launches]
+    order_ok = all(names.index("optim_b%d" % k) > max([names.index(nm) for nm, rlo, rhi in plan.pack_readers
+                                                        if rlo < hi and rhi > lo] + [-1])
+                   for k, (lo, hi, _) in enumerate(plan.bucket_tables))
+    dl = np.abs(wl - wlb)
+    results["legacy_buckets"] = {"n_buckets": len(plan.bucket_tables), "order_ok": bool(order_ok),
+                                 "comm_fork": bool(plan.comm_fork),
+                                 "max_abs_diff": float(dl.max()), "p999_abs_diff": float(np.quantile(dl, 0.999))}
     rep["train"] = results
 
     # failure detection: an aborted communicator raises on its next use

@@ -1,0 +1,92 @@
+"""GPU worker for tests/test_comm.py::test_dp_step_xgmi_ranks_one_gpu: the 8-GPU data-parallel
+training step, rehearsed with P ranks on ONE MI355X.
+
+RCCL refuses two ranks on one GPU; the RCCL-free data plane (``INTML_COMM=xgmi``, chosen on
+its own when ranks share a GPU) is the same fused xGMI all-reduce + Adam kernel, captured into
+the same HIP graph, that an 8-GPU job uses -- only the peers' inboxes live on this card.
+
+Every rank trains the RPV bench model (conv [16,32,64], fc [128], dropout 0 so the rows of a
+global batch see the same masks wherever they run) for 24 steps as 3 graph replays of 8
+captured steps, per-rank batch 128/P: global step t uses rows perm[128t : 128t+128] of one
+device-resident synthetic data set, rank r rows perm[128t + r*128/P : ...].  Rank 0 then
+trains a single-process model from the same initial weights on the same permutation at
+batch 128.  Writes one JSON per rank:
+  err            the fused kernel's error word (0: no wait timed out)
+  digest         sha256 of the rank's trained fp32 weights (all ranks must agree bitwise)
+  vs_single      rank 0: p999 / max |w_dp - w_single|
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from cori_intml_examples_amd.apps import zoo  # noqa: E402
+from cori_intml_examples_amd.io import synth  # noqa: E402
+from cori_intml_examples_amd.parallel import dist, hvd  # noqa: E402
+from cori_intml_examples_amd.utils import set_random_seed  # noqa: E402
+
+GLOBAL_B, STEPS, SPG, N = 128, 24, 8, 4096
+
+
+def flat(m):
+    return np.concatenate([w.reshape(-1) for w in m.get_weights()])
+
+
+def train(m, data, perm, bs):
+    ex = m._executor
+    for i in range(STEPS // SPG):
+        ex.train_steps(data, perm, i * SPG * bs, bs, SPG)
+    torch.cuda.synchronize()
+    return flat(m)
+
+
+def main(outdir):
+    st = hvd.init()
+    r, P = hvd.rank(), hvd.size()
+    dev = torch.device("cuda", 0)
+    rep = {"rank": r, "size": P, "xgmi_only": bool(st.xgmi_only), "rccl": st.comm is not None}
+    kw = dict(conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.0, optimizer="Adam", lr=1e-3, device="cuda:0")
+    set_random_seed(1 + r)                       # different on purpose: the broadcast must fix it
+    m = zoo.rpv_cnn((64, 64, 3), use_horovod=True, **kw)
+    hvd.broadcast_global_variables(0, model=m)
+    w0 = m.get_weights()
+    ex = m._executor
+    data = synth.synth_device("rpv", N, (64, 64, 3), 1, ex.in_Cs, 7, dev)
+    g = torch.Generator(device=dev).manual_seed(11)
+    perm = torch.randperm(N, device=dev, generator=g)[:STEPS * GLOBAL_B]
+    b = GLOBAL_B // P
+    mine = perm.view(STEPS, P, b)[:, r, :].reshape(-1).contiguous()
+    w = train(m, data, mine, b)
+    red = ex.reducer
+    plan = next(iter(ex._plans.values()))
+    rep["reducer"] = type(red).__name__
+    rep["plane"] = red.plane
+    rep["buckets"] = [list(x) for x in red.buckets]
+    rep["comm_in_graph"] = bool(plan.comm_in_graph)
+    rep["fused_launches"] = [it[0] for it in plan.launches if "xgmi" in it[0] or "allreduce" in it[0]]
+    rep["err"] = int(red.xgmi.err.item()) if red.xgmi is not None else -1
+    rep["digest"] = hashlib.sha256(w.tobytes()).hexdigest()
+    rep["finite"] = bool(np.isfinite(w).all())
+    rep["moved"] = float(np.abs(w - np.concatenate([a.reshape(-1) for a in w0])).max())
+    red.after_step()                             # raises if an earlier launch's wait timed out
+    if r == 0:
+        single = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw)
+        single.set_weights(w0)
+        ws = train(single, data, perm.contiguous(), GLOBAL_B)
+        d = np.abs(w - ws)
+        rep["vs_single"] = {"p999": float(np.quantile(d, 0.999)), "max": float(d.max()),
+                            "step_norm": float(np.linalg.norm(ws - np.concatenate([a.reshape(-1) for a in w0])))}
+    hvd.barrier()
+    with open(os.path.join(outdir, "dpx%d.json" % r), "w") as f:
+        json.dump(rep, f, indent=1)
+    dist.shutdown()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -103,11 +103,24 @@ def test_inline_hpo_record_on_cpu(monkeypatch):
     monkeypatch.setattr(bench.InlineHpo, "TRIALS", 3)
     monkeypatch.setattr(bench.InlineHpo, "EPOCHS", 1)
     monkeypatch.setattr(bench.InlineHpo, "SAMPLES", 600)
-    h = bench.InlineHpo(engines_per_gpu=2, budget_s=120.0)
+    # DistWidgetHPO_rpv record: 3 concurrent trials (8 on the GPU), tiny data
+    monkeypatch.setattr(bench.InlineHpo, "RPV_TRIALS", 3)
+    monkeypatch.setattr(bench.InlineHpo, "RPV_TRAIN", 256)
+    monkeypatch.setattr(bench.InlineHpo, "RPV_VALID", 128)
+    h = bench.InlineHpo(engines_per_gpu=2, budget_s=120.0, rpv_budget_s=240.0)
     try:
-        rec = h.run()
+        recs = h.run()
     finally:
         h.stop()
+    assert h.engines == 3               # max(engines_per_gpu, concurrent RPV trials) per GPU
+    rec = recs["hpo"]
     assert rec["trials_done"] == 3 and not rec["capped"], rec
     assert rec["trials_per_hour"] > 0 and rec["wall_s"] >= rec["startup_s"] > 0
     assert rec["epochs"] == 1 and rec["samples"] == 600 and rec["engines_per_gpu"] == 2
+    assert rec["label_noise"] == 0.1
+    rr = recs["hpo_rpv"]
+    assert rr["trials_done"] == 3 and not rr["capped"] and rr["concurrent"] == 3, rr
+    # every trial's epochs reached the dashboard model (2 epochs each) and were timed
+    assert rr["dashboard_rows_final"] == [2, 2, 2], rr
+    assert rr["epoch_messages_seen"] == 6 and rr["publish_to_dashboard_ms_p50"] is not None, rr
+    assert rr["publish_to_dashboard_ms_p50"] >= 0 and rr["best_val_loss"] > 0, rr

@@ -78,6 +78,9 @@ def test_native_comm_engine_gpu(tmp_path):
     assert hy["xgmi_bucket"] == 1 and len(hy["buckets"]) == 2 and hy["comm_fork"], hy
     assert [list(x) for x in hy["launches"]] == [["allreduce_b0", "comm"], ["optim_b0", "comm"],
                                                  ["xgmi_allreduce_optim_b1", "main"]], hy
+    lg = rep["train"]["legacy_buckets"]
+    assert lg["n_buckets"] > 2 and lg["comm_fork"] and lg["order_ok"], lg
+    assert lg["p999_abs_diff"] < 1e-5 and lg["max_abs_diff"] < 1e-3, lg
     assert hy["p999_abs_diff"] < 1e-5 and hy["max_abs_diff"] < 2e-3, hy
     assert rep["abort_raises"] and rep["healthy"], rep
 
@@ -160,3 +163,83 @@ def test_xgmi_late_rank_aborts_cleanly(tmp_path):
     for rep in reps:
         assert rep["err2"] != 0 and rep["second_untouched"] and rep["second_launch_s"] < 1.0, rep
         assert rep["check_raised"], rep
+
+
+def test_comm_mode_xgmi_only(monkeypatch):
+    """No RCCL communicator when ranks share a GPU (RCCL refuses it) or on request: the
+    fused xGMI kernel is then the data plane."""
+    from cori_intml_examples_amd.parallel import comm as C
+    for k in ("INTML_COMM", "INTML_DP_BACKEND"):
+        monkeypatch.delenv(k, raising=False)
+    assert C.comm_mode(True, None, local_size=8, n_devices=1) == "xgmi"
+    assert C.comm_mode(True, None, local_size=2, n_devices=1) == "xgmi"
+    assert C.comm_mode(False, None, local_size=8, n_devices=1) == "torch"     # CPU: gloo
+    monkeypatch.setenv("INTML_COMM", "xgmi")
+    assert C.comm_mode(True, None, local_size=8, n_devices=8) == "xgmi"
+    assert C.comm_mode(True, "gloo") == "torch"                              # explicit backend wins
+
+
+def test_xgmi_only_reducer_is_one_fused_bucket():
+    """The RCCL-free reducer: the whole gradient is one bucket, no RCCL launch exists for it,
+    and the segmented (uncaptured) protocol routes that bucket through the fused kernel."""
+    from cori_intml_examples_amd.parallel.dist import NativeGradReducer
+
+    class _Store:
+        numel = 547841
+        device = None
+
+    class _X:
+        n, launched = 547841, []
+
+        def launch(self, ptr, stream, opt=None):
+            self.launched.append((ptr, stream, opt))
+
+    red = NativeGradReducer.__new__(NativeGradReducer)
+    red.store, red.comm, red.compression, red.bucket_bytes = _Store(), None, None, None
+    red.rank, red.size, red.device = 1, 4, None
+    red.buckets, red.bucket_groups, red._stage, red._configured = [(0, 547841)], [[0]], {}, False
+    red.xgmi, red.xgmi_bucket, red.plane, red._xgmi_err_host = _X(), None, "rccl", None
+    red._setup_xgmi = lambda: setattr(red, "xgmi_bucket", 0)
+    groups = [(547712, 547841), (23584, 547712), (5088, 23584), (448, 5088), (0, 448)]
+    assert red.configure(groups) == [[0, 1, 2, 3, 4]]
+    assert red.plane == "xgmi" and red.buckets == [(0, 547841)] and red.xgmi_bucket == 0
+
+    class _Grad:
+        def data_ptr(self):
+            return 4096
+
+    red.launch(0, _Grad(), 77)
+    assert red.xgmi.launched == [(4096, 77, None)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
+    """the 8-GPU data-parallel step end to end on one GPU.  P ranks (torchrun,
+    all on GPU 0, so the RCCL-free plane is chosen on its own) train 24 captured steps (3
+    replays x 8) at per-rank batch 128/P through the fused xGMI all-reduce + Adam kernel:
+    no wait times out, every rank ends with bit-identical weights, and those match a
+    single-process run at global batch 128 from the same weights and permutation within the
+    bounds of the size-1 DP test (Adam amplifies last-ulp differences of near-zero grads)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, INTML_DP_TIMEOUT="60")
+    for k in ("WORLD_SIZE", "RANK", "INTML_DP_BACKEND", "INTML_COMM", "INTML_XGMI", "INTML_BUCKET_BYTES"):
+        env.pop(k, None)
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(P),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "tests", "dp_xgmi_worker_gpu.py"), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=420, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    reps = [json.load(open(tmp_path / ("dpx%d.json" % i))) for i in range(P)]
+    for rep in reps:
+        assert rep["xgmi_only"] and not rep["rccl"] and rep["reducer"] == "NativeGradReducer", rep
+        assert rep["plane"] == "xgmi" and rep["comm_in_graph"] and len(rep["buckets"]) == 1, rep
+        assert rep["fused_launches"] == ["xgmi_allreduce_optim_b0"], rep
+        assert rep["err"] == 0 and rep["finite"] and rep["moved"] > 1e-4, rep
+    assert len({rep["digest"] for rep in reps}) == 1, [rep["digest"] for rep in reps]
+    vs = reps[0]["vs_single"]
+    assert vs["p999"] < 1e-5 and vs["max"] < 2e-3, vs

@@ -129,3 +129,26 @@ def test_synth_kernel_matches_cpu_twin(kind, shape, ncls, Cs):
     assert torch.equal(xg[..., :C], v.to(torch.bfloat16)), (kind, (xg[..., :C].float() - v).abs().max())
     assert not xg[..., C:].float().any()
     assert torch.equal(d.y.cpu(), y)
+
+
+def test_flip_labels_rate_and_semantics():
+    """HPO label noise: ~frac of the labels change, binary ones to 1 - y, one-hot ones to a
+    different class; deterministic in (seed, sample index); frac 0 is the identity."""
+    from cori_intml_examples_amd.io.synth import flip_labels
+    from cori_intml_examples_amd.models.executor_base import DeviceData
+    n = 20000
+    yb = (torch.arange(n) % 2).float()[:, None]
+    d = flip_labels(DeviceData(torch.zeros(n, 1), yb.clone(), n), 0.1, 7)
+    changed = (d.y != yb).float().mean().item()
+    assert 0.09 < changed < 0.11 and set(d.y.unique().tolist()) <= {0.0, 1.0}
+    assert torch.equal(flip_labels(DeviceData(torch.zeros(n, 1), yb.clone(), n), 0.1, 7).y, d.y)
+    cls = torch.arange(n) % 10
+    y10 = torch.nn.functional.one_hot(cls, 10).float()
+    d10 = flip_labels(DeviceData(torch.zeros(n, 1), y10.clone(), n), 0.1, 7)
+    assert torch.equal(d10.y.sum(1), torch.ones(n))                  # still one-hot
+    moved = d10.y.argmax(1) != cls
+    assert 0.09 < moved.float().mean().item() < 0.11
+    # a shard [first, first + m) sees the same flips as the whole set
+    part = flip_labels(DeviceData(torch.zeros(100, 1), yb[500:600].clone(), 100), 0.1, 7, first=500)
+    assert torch.equal(part.y, d.y[500:600])
+    assert torch.equal(flip_labels(DeviceData(torch.zeros(n, 1), yb.clone(), n), 0.0, 7).y, yb)
