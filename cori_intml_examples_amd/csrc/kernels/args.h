@@ -264,6 +264,9 @@ struct HeadArgs {
   unsigned long long* ts = nullptr;   // diagnostics: [block][8] phase stamps (null = off)
   // yidx != null: row m's targets are dataset row yidx[m] of st->data_y (prologue-free step)
   const int* yidx = nullptr;
+  // A/B + tests: 1 = the generic serial epilogue / loss path even where the fast paths apply
+  // (bit-identical results: tests/test_hip_model.py::test_head_fast_paths_bit_identical)
+  int generic = 0;
 };
 
 struct GatherArgs {

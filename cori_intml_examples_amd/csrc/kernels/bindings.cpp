@@ -124,7 +124,7 @@ PYBIND11_MODULE(_kernels, m) {
       RW(HeadArgs, flat_C) RW(HeadArgs, flat_Cs) PTR(HeadArgs, w) PTR(HeadArgs, bias) PTR(HeadArgs, y)
       RW(HeadArgs, act) RW(HeadArgs, training) RW(HeadArgs, inv_bs) PTR(HeadArgs, st) PTR(HeadArgs, probs)
       PTR(HeadArgs, wslab) PTR(HeadArgs, bslab) RW(HeadArgs, bt) RW(HeadArgs, epi) PTR(HeadArgs, ts)
-      PTR(HeadArgs, yidx);
+      PTR(HeadArgs, yidx) RW(HeadArgs, generic);
 
   py::class_<GatherArgs>(m, "GatherArgs")
       .def(py::init<>())

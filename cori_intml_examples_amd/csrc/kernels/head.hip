@@ -176,7 +176,60 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
   }
   bool done_epi = false;
   if constexpr (RB == 1) {
-   if (fused && a.epi.splits <= 64) {
+   if (fused && !a.generic && a.epi.splits <= 32 && a.epi.Ns <= 128) {
+    done_epi = true;
+    // one row per workgroup, <= 32 splits, <= 128 columns: thread -> column n = tid % 128,
+    // split groups sg = tid / 128 and sg + 2; the <= 8 partials of BOTH groups are loaded in
+    // one batch (one memory round trip, no clamped duplicates), then summed in
+    // dense_epi_value's order (bit-identical)
+    const DenseEpiArgs& e = a.epi;
+    const int n = tid & 127, sg0 = tid >> 7;
+    const bool col = n < e.N;
+    const size_t stride = (size_t)e.M * e.ldp;
+    const float* p = e.part + (size_t)row0 * e.ldp + (col ? n : 0);
+    float v[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int sp = sg0 + 2 * h + 4 * j;
+        v[h][j] = (col && sp < e.splits) ? p[(size_t)sp * stride] : 0.f;
+      }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int sg = sg0 + 2 * h;
+      float a0 = 0.f, a1 = 0.f;
+      int jn = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (sg + 8 * i + 4 < e.splits) {
+          a0 += v[h][2 * i];
+          a1 += v[h][2 * i + 1];
+          jn = 2 * i + 2;
+        }
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj)
+        if (jj >= jn && sg + 4 * jj < e.splits) a0 += v[h][jj];
+      if (n < e.Ns) red4[sg][n] = a0 + a1;
+    }
+    __syncthreads();
+    for (int c = tid; c < e.Ns; c += 256) {
+      float val = 0.f;
+      if (c < e.N) {
+        val = (red4[0][c] + red4[1][c]) + (red4[2][c] + red4[3][c]);
+        if (e.bias) val += e.bias[c];
+        if (e.relu) val = fmaxf(val, 0.f);
+        if (e.drop_thr)
+          val = dropout_keep((uint32_t)(row0 * e.N + c), e.seed, e.stream_id, step, e.drop_thr) ? val * e.drop_scale
+                                                                                                 : 0.f;
+      }
+      const bf16 hb = f2bf(val);
+      hs[0][c] = hb;
+      e.out[(size_t)row0 * e.Ns + c] = hb;     // saved activation (ReLU mask of the backward)
+    }
+    __syncthreads();
+   }
+   if (fused && !done_epi && a.epi.splits <= 64) {
     done_epi = true;
     // one row per workgroup: the four split groups of every column in parallel (all their
     // loads in flight), combined in dense_epi_value's fixed order
@@ -247,6 +300,72 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs a) {
     for (int n = 0; n < NM; ++n) z[n] += __shfl_xor(z[n], off);
   }
   HEAD_STAMP(7);
+  if constexpr (RB == 1 && NM == 1) {
+    // Binary head of a fused hidden dense layer (the RPV step): only dz gates the backward,
+    // so lane 0 publishes it first; then wave 0 computes the loss / accuracy and the metric
+    // atomics (a serial log / exp chain) WHILE waves 1-3 write the dW / db slabs and dh --
+    // the loss is off the critical path.  Same formulas and rounding points as below.
+    const BwdThrough& t = a.bt;
+    if (a.act == 1 && fused && !a.generic && a.training && t.dy && t.prev_out == a.epi.out && t.pH == 1 &&
+        t.pW == 1 && N == 1) {
+      const float eps = 1e-7f;
+      const float z0 = z[0] + bsh[0];
+      if (tid == 0) {
+        const float p = 1.f / (1.f + expf(-z0));
+        if (a.probs) a.probs[row] = p;
+        float dz = 0.f;
+        if (a.y) {
+          const float pc = clip_nan(p, eps, 1.f - eps);
+          dz = ((p >= eps) && (p <= 1.f - eps)) ? (pc - ysh[0][0]) : 0.f;
+        }
+        dz_s[0][0] = dz * a.inv_bs;
+      }
+      HEAD_STAMP(2);
+      __syncthreads();
+      HEAD_STAMP(3);
+      if (wave == 0) {
+        if (tid == 0 && a.y && a.st) {
+          const float p = 1.f / (1.f + expf(-z0));
+          const float yv = ysh[0][0];
+          const float pc = clip_nan(p, eps, 1.f - eps);
+          const float lg = logf(pc / (1.f - pc));
+          const float ls = fmaxf(lg, 0.f) - lg * yv + log1pf(expf(-fabsf(lg)));
+          const float cs = (rintf(p) == yv) ? 1.f : 0.f;
+          long long* slot = a.st->metric_slots[blockIdx.x & 15];
+          const bool loss_ok = isfinite(ls) && fabsf(ls) < 1073741824.f;
+          if (loss_ok) atomicAdd((unsigned long long*)&slot[0], (unsigned long long)llrint((double)ls * 4294967296.0));
+          else atomicAdd((unsigned long long*)&slot[3], 1ull);
+          atomicAdd((unsigned long long*)&slot[1], (unsigned long long)llrintf(cs));
+          atomicAdd((unsigned long long*)&slot[2], 1ull);
+        }
+        HEAD_STAMP(4);
+        return;
+      }
+      const int t2 = tid - 64;                       // waves 1-3
+      const float dz = dz_s[0][0];
+      float* ws = a.wslab + (size_t)blockIdx.x * a.K;
+      for (int k = t2; k < a.K; k += 192) {
+        const int kp = a.flat_C ? flat_keras_to_padded(k, a.flat_C, a.flat_Cs) : k;
+        ws[k] = 0.f + bf2f(hs[0][kp]) * dz;      // (0 + x: the serial path's +0 for -0 products)
+      }
+      if (t2 == 0 && a.bslab) a.bslab[blockIdx.x] = dz;
+      if (tid == 64 && a.ts) a.ts[(size_t)blockIdx.x * 8 + 5] = wall_clock64();
+      for (int c = t2; c < t.pCs; c += 192) {
+        float gs = 0.f;
+        if (c < t.pC) {
+          gs = 0.f + dz * (wlds ? wsh[c] : a.w[c]);
+          if (t.drop_thr) {
+            const uint32_t di = (uint32_t)((size_t)row0 * t.pC + c);
+            gs = dropout_keep(di, t.seed, t.stream_id, step, t.drop_thr) ? gs * t.drop_scale : 0.f;
+          }
+          if (t.prev_relu && !(bf2f(hs[0][c]) > 0.f)) gs = 0.f;
+        }
+        t.dy[(size_t)row0 * t.pCs + c] = f2bf(gs);
+      }
+      if (tid == 64 && a.ts) a.ts[(size_t)blockIdx.x * 8 + 6] = wall_clock64();
+      return;
+    }
+  }
   if constexpr (NM > 1) {
     if (a.act == 2 && row_wave) {
       // softmax + categorical cross-entropy, one class per lane (lanes 0..15 of the row's

@@ -63,6 +63,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
     ktab[c] = e;
   }
   __syncthreads();
+  WH_STAMP(8);
 
   // per-wave m-tile descriptors (constant over blocks and k-steps)
   int ko[MTW];
@@ -334,6 +335,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
         *reinterpret_cast<uint4*>(dyl + (size_t)p * ldb + (idx - p * cpr) * 8) = v;
       }
     };
+    WH_STAMP(9);
     fetch(blk0);
     WH_STAMP(1);
     for (int blk = blk0; blk < blk1; ++blk) {

@@ -774,6 +774,7 @@ class BatchPlan(GeometryMixin):
         if head_epi is not None:
             h.epi = head_epi
         h.training = int(training)
+        h.generic = int(tune("head_generic", False))
         h.inv_bs = 1.0 / bs
         h.st = st_ptr
         if self.probs is not None:

@@ -3,6 +3,12 @@
 CPU (plumbing, no GPU)" configuration of BASELINE.json and the oracle for the
 whole-model HIP tests.  Forward/backward are written out explicitly (no autograd
 graph) in exactly the stage order the HIP executor uses.
+
+``INTML_TUNE=ref_bf16=1`` makes it a bf16-FAITHFUL oracle: values are rounded to bf16 at
+exactly the points where the HIP step stores them in bf16 (weight packs of the convs and
+hidden denses, every stage output after its dropout, the hidden denses' dH and every pooled
+dP after their masks), everything else in fp32 -- so the whole-step gradient test can use
+the per-kernel tests' tight tolerances instead of the loose fp32-vs-bf16 bound.
 """
 from __future__ import annotations
 
@@ -13,6 +19,7 @@ import torch
 
 from ..ops import reference as R
 from ..ops.rng import dropout_keep
+from ..utils.env import tune
 from .executor_base import DeviceData, Executor, prepare_targets
 from .plan import Plan
 
@@ -26,6 +33,7 @@ class RefExecutor(Executor):
         self.m_schedule = 1.0
         self._acc = torch.zeros(3, dtype=torch.float64)
         self._last = (0.0, 0.0)
+        self.emulate_bf16 = bool(tune("ref_bf16", False))
 
     # ------------------------------------------------------------------------------ data
     def upload(self, x, y):
@@ -41,12 +49,16 @@ class RefExecutor(Executor):
         keep = dropout_keep(numel, rate, self.seed, stream, step)
         return keep.to(torch.float32) / (1.0 - rate)
 
+    def _q(self, t):
+        """bf16 rounding at a HIP storage point (identity unless emulating bf16)."""
+        return t.to(torch.bfloat16).to(torch.float32) if self.emulate_bf16 else t
+
     def _forward(self, x, training: bool, step: int):
         st = self.store
         saved = []
         a = x
         for cs in self.plan.convs:
-            w = st.view(cs.conv, "kernel")
+            w = self._q(st.view(cs.conv, "kernel"))
             b = st.view(cs.conv, "bias") if cs.conv.use_bias else None
             z = R.conv2d(a, w, b, cs.stride, cs.conv.padding)
             r = torch.relu(z) if cs.relu else z
@@ -59,10 +71,10 @@ class RefExecutor(Executor):
                 mask = self._mask(p.numel(), cs.rate, cs.stream, step).view(p.shape)
                 p = p * mask
             saved.append((a, r, code, mask))
-            a = p
+            a = self._q(p)
         a = a.reshape(a.shape[0], -1)
         for ds in self.plan.denses:
-            w = st.view(ds.dense, "kernel")
+            w = self._q(st.view(ds.dense, "kernel"))
             z = a @ w
             if ds.dense.use_bias:
                 z = z + st.view(ds.dense, "bias")
@@ -72,7 +84,7 @@ class RefExecutor(Executor):
                 mask = self._mask(r.numel(), ds.rate, ds.stream, step).view(r.shape)
                 r = r * mask
             saved.append((a, z, None, mask))
-            a = r
+            a = self._q(r)
         hd = self.plan.head
         z = a @ st.view(hd.dense, "kernel")
         if hd.dense.use_bias:
@@ -103,10 +115,11 @@ class RefExecutor(Executor):
                 da = da * mask
             if ds.relu:
                 da = da * (z > 0).to(da.dtype)
+            da = self._q(da)                                   # the stored bf16 dH
             st.view(ds.dense, "kernel", grad=True).copy_(a_in.t() @ da)
             if ds.dense.use_bias:
                 st.view(ds.dense, "bias", grad=True).copy_(da.sum(0))
-            da = da @ st.view(ds.dense, "kernel").t()
+            da = da @ self._q(st.view(ds.dense, "kernel")).t()
         if nconv:
             cs_last = self.plan.convs[-1]
             da = da.reshape((da.shape[0],) + tuple(cs_last.out_shape))
@@ -115,11 +128,18 @@ class RefExecutor(Executor):
             a_in, r, code, mask = saved[i]
             if mask is not None:
                 da = da * mask
+            if self.emulate_bf16:
+                # the HIP step stores this gradient (masked by the dropout and the ReLU of
+                # the stage output, at the stage's output resolution) as bf16 before routing it
+                if cs.relu:
+                    pooled = R.maxpool2x2(r)[0] if cs.pool is not None else r
+                    da = da * (pooled > 0).to(da.dtype)
+                da = self._q(da)
             if cs.pool is not None:
                 da = R.maxpool2x2_backward(da, code, r.shape[1:3])
             if cs.relu:
                 da = da * (r > 0).to(da.dtype)
-            dx, dw, db = R.conv2d_backward(a_in, st.view(cs.conv, "kernel"), da, cs.stride,
+            dx, dw, db = R.conv2d_backward(a_in, self._q(st.view(cs.conv, "kernel")), da, cs.stride,
                                            cs.conv.padding, need_dx=i > 0)
             st.view(cs.conv, "kernel", grad=True).copy_(dw)
             if cs.conv.use_bias:

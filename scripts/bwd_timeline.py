@@ -78,6 +78,10 @@ for name, fn, *_ in bp.launches:
         if len(d):
             parts.append("%s->%s +%.2f" % (segs[k] if k < len(segs) else "?", "slab" if idx[k + 1] == 15 else "", np.median(d)))
     print("   wgrad phases (wave 0, median us):", ", ".join(parts))
+    if (q[:, 8] > 0).any():
+        m = lambda a_, b_: np.median((q[:, b_] - q[:, a_])[(q[:, a_] > 0) & (q[:, b_] > 0)])
+        print("   wgrad start detail: ktab+barrier %.2f, per-lane setup %.2f, fetch issue %.2f" % (
+            m(0, 8), m(8, 9), m(9, 1)))
     if ca is not None:
         ca.ts = 0
         p = ph.view(-1, 8).cpu().numpy().astype(np.float64)[n_w:] * 0.01

@@ -122,7 +122,7 @@ def main(out):
     # 1 MiB buckets: every bucket's optimizer runs on the comm stream and writes its layers'
     # packs, so it must wait for the dgrad that reads them (defer_after_readers)
     set_random_seed(2)
-    lkw = dict(device="cuda:0", lr=1e-4)
+    lkw = dict(device="cuda:0", lr=1e-3)      # = the Adam default the DistributedOptimizer below gets
     lb = zoo.rpv_legacy_cnn((64, 64, 3), use_horovod=False, **lkw)
     lw0 = lb.get_weights()
 

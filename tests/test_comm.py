@@ -80,7 +80,7 @@ def test_native_comm_engine_gpu(tmp_path):
                                                  ["xgmi_allreduce_optim_b1", "main"]], hy
     lg = rep["train"]["legacy_buckets"]
     assert lg["n_buckets"] > 2 and lg["comm_fork"] and lg["order_ok"], lg
-    assert lg["p999_abs_diff"] < 1e-5 and lg["max_abs_diff"] < 1e-3, lg
+    assert lg["p999_abs_diff"] < 1e-5 and lg["max_abs_diff"] < 2e-3, lg
     assert hy["p999_abs_diff"] < 1e-5 and hy["max_abs_diff"] < 2e-3, hy
     assert rep["abort_raises"] and rep["healthy"], rep
 

@@ -16,6 +16,7 @@ from cori_intml_examples_amd.models import (Conv2D, Dense, Dropout, Flatten, Inp
 from cori_intml_examples_amd.ops import reference as R
 from cori_intml_examples_amd.ops.rng import dropout_keep, keep_threshold, rng_u32
 from cori_intml_examples_amd.train import callbacks as cbks
+from cori_intml_examples_amd.utils import set_random_seed
 
 GOLDEN_SUMMARY = """\
 _________________________________________________________________
@@ -303,3 +304,23 @@ def test_profiling_hooks_and_resume(tmp_path):
     m2 = load_model(p)
     h2 = m2.fit(x, y, batch_size=16, epochs=3, initial_epoch=2, verbose=0)
     assert h2.epoch == [2] and m2.optimizer.iterations == m.optimizer.iterations + 4
+
+
+def test_reference_bf16_mode_runs_and_stays_close(monkeypatch):
+    """executor_ref's bf16-faithful mode (the HIP step's storage roundings; the GPU tests'
+    tight whole-step oracle): finite gradients within bf16 noise of the fp32 reference."""
+    import torch
+    x, y, _ = synthetic_rpv(32, size=16, seed=3)
+    grads = []
+    for tv in ("ref_bf16=0", "ref_bf16=1"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(7)
+        m = zoo.rpv_cnn((16, 16, 1), [4, 8, 8], [16], dropout=0.2, optimizer="Adam", lr=1e-3, device="cpu")
+        assert m._executor.emulate_bf16 == (tv == "ref_bf16=1")
+        ex = m._executor
+        d = ex.upload(torch.tensor(x).to(torch.bfloat16).float().numpy(), y)
+        ex.train_step(d, torch.arange(d.n), 0, d.n)
+        grads.append(m.store.grad[:m.store.numel].clone())
+    a, b = grads
+    assert torch.isfinite(b).all() and not torch.equal(a, b)
+    assert float((a - b).norm() / a.norm()) < 0.1

@@ -172,6 +172,34 @@ def test_grads_match_reference(kind, drop, cin, hw, n):
     assert abs(lg - lc) < 2e-2 * max(1.0, abs(lc))
 
 
+@pytest.mark.parametrize("kind,drop,cin,hw,n", [
+    ("rpv_bench", 0.2, 3, 64, 128), ("mnist_bench", 0.4, 1, 28, 128), ("rpv", 0.3, 3, 16, 48),
+    ("odd", 0.25, 2, 16, 48)])
+def test_grads_match_bf16_reference(kind, drop, cin, hw, n, monkeypatch):
+    """Whole-step gradients at the bench shapes against the bf16-FAITHFUL CPU oracle
+    (executor_ref with ref_bf16: the same bf16 storage points as the HIP step, fp32
+    everywhere else): every weight / bias gradient within the per-kernel tests' standard
+    (relative error < 5e-2, cosine > 0.995).  What remains is fp32 summation
+    order and the rare max-pool argmax tie it flips."""
+    monkeypatch.setenv("INTML_TUNE", "ref_bf16=1")
+    g, c = _pair(kind, drop=drop, cin=cin, hw=hw)
+    assert c._executor.emulate_bf16
+    x, y = _data(g, n)
+    gg, cg = _one_step(g, c, x, y)
+    worst = []
+    for s in g.store.specs:
+        a = gg[s.offset:s.offset + s.numel]
+        b = cg[s.offset:s.offset + s.numel]
+        err = _rel(a, b)
+        cos = float(np.dot(a, b) / max(np.linalg.norm(a) * np.linalg.norm(b), 1e-30))
+        worst.append((err, cos, s.name))
+        assert err < 5e-2 and cos > 0.995, "%s: grad rel err %.3g cos %.6f" % (s.name, err, cos)
+    lg, ag, _ = g._executor.read_metrics()
+    lc, ac, _ = c._executor.read_metrics()
+    assert abs(lg - lc) < 1e-3 * max(1.0, abs(lc)) and ag == ac, (lg, lc, ag, ac)
+    print("worst grad rel err %.3g (cos %.6f) at %s" % max(worst))
+
+
 @pytest.mark.parametrize("opt", ["Adam", "Nadam", "Adadelta", "SGD", "RMSprop"])
 def test_optimizer_kernel_matches_keras_math(opt):
     """Fused optimizer kernel vs Keras-2.2 update math applied to the SAME gradients,
@@ -430,3 +458,27 @@ def test_optimizer_pack_routes_match_repack(kind, cin, tiled):
         outs.append(m.store.master.clone())
     if tiled:
         assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("kind,drop,cin,hw,opt", [("rpv", 0.2, 3, 64, "Adam"), ("mnist", 0.4, 1, 28, "Nadam")])
+def test_head_fast_paths_bit_identical(kind, drop, cin, hw, opt, monkeypatch):
+    """The head kernel's fast paths (one-round-trip split-K epilogue loads; the binary head's
+    dz published before its loss, with the loss / metric atomics on wave 0 while waves 1-3
+    write the slabs and dh) train bit-identically to the generic serial path: weights,
+    metrics and iteration count over a multi-step graph."""
+    res = []
+    for tv in ("head_generic=0", "head_generic=1"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(46)
+        m = _build(kind, "cuda", opt=opt, drop=drop, cin=cin, hw=hw)
+        x, y = _data(m, 512, seed=10)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(6)).to(ex.device)
+        ex.reset_metrics()
+        ex.train_steps(d, perm, 0, 128, 3)
+        torch.cuda.synchronize()
+        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics(), int(m.optimizer.iterations)))
+    (w1, m1, i1), (w0, m0, i0) = res
+    assert torch.equal(w1, w0)
+    assert m1 == m0 and i1 == i0 == 3
