@@ -156,6 +156,10 @@ struct ConvStackArgs {
   // runs after this launch, so the dropout counter is st->t + 1
   int from_data = 0, training = 0, step_inc = 0;
   int* srcidx = nullptr;
+  // k16: a 4-channel first layer's second k-step (ONLY tap 8: k 32..35 of the 36-wide K)
+  // as one v_mfma_f32_16x16x16_bf16 with a single 8-byte A read, instead of a 16x16x32 whose
+  // other 28 k are zero weights
+  int k16 = 0;
 };
 
 // Weight gradient: dW[k][n] = sum_pixels im2col(x)[p][k] * dY[p][n]  (split over pixels)

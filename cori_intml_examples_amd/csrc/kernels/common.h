@@ -26,6 +26,13 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f32_16x16x16_bf16: lane l holds A[l & 15][k = 4 (l >> 4) + j] / B[k][l & 15], j < 4
+__device__ __forceinline__ f32x4 mfma16k16(const bf16x4& a, const bf16x4& b, const f32x4& c) {
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c,
+                                                   0, 0, 0);
+}
+
 __device__ __forceinline__ bf16x8 zero_bf16x8() {
   bf16x8 z;
 #pragma unroll

@@ -285,6 +285,34 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) bv[nt] = *reinterpret_cast<const LDS bf16x8*>(wl + ((ks * NT + nt) * 64 + lane) * 8);
     };
+    if constexpr (CS4 && KS == 2) {
+      if (A.k16) {
+        // k-step 1 holds only tap 8 (k 32..35): one 16x16x16 MFMA (lane group g holds k
+        // 4g..4g+3 of the 16-wide step) on the lane's 8-byte tap-8 read; B = the 32-wide pack
+        // vector's first four k of lane (r, 0), zero for g > 0 (k >= 36: no tap)
+        load_k(0, af[0], bf[0]);
+        bf16x4 a16[TM], b16[NT];
+        const bf16x4 z4 = {(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+#pragma unroll
+        for (int t = 0; t < TM; ++t) a16[t] = *reinterpret_cast<const LDS bf16x4*>(in + base[t] + e0[1]);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const bf16x4 w4 = *reinterpret_cast<const LDS bf16x4*>(wl + ((NT + nt) * 64 + r) * 8);
+          b16[nt] = g == 0 ? w4 : z4;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int t = 0; t < TM; ++t) acc[t][nt] = mfma16(af[0][t], bf[0][nt], acc[t][nt]);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int t = 0; t < TM; ++t) acc[t][nt] = mfma16k16(a16[t], b16[nt], acc[t][nt]);
+        __builtin_amdgcn_sched_barrier(0);
+        goto k_done;
+      }
+    }
     load_k(0, af[0], bf[0]);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -296,6 +324,7 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
         for (int t = 0; t < TM; ++t) acc[t][nt] = mfma16(af[ks & 1][t], bf[ks & 1][nt], acc[t][nt]);
       __builtin_amdgcn_sched_barrier(0);
     }
+  k_done:
     if (stamp && tb == wave * TM) {
       asm volatile("" ::"v"(acc[0][0][0]));
       STACK_STAMP(14);

@@ -805,6 +805,7 @@ class BatchPlan(GeometryMixin):
         self.red_groups.append((lo, hi, descs))
         self._add_group_reduce()
         self.wgrad_slabs = []
+        self.tail_capable = set()          # halo wgrad launches that can carry a tail reduction
         self.dense_fused_opt = []          # (WgradArgs, params) updated inside dense_wgrad
         # opt-in: the dense layer's optimizer update inside its (one-split) wgrad kernel.  Measured
         # slower on RPV at batch 128: the 128 wgrad workgroups move the layer's 14 MB of optimizer
@@ -902,8 +903,9 @@ class BatchPlan(GeometryMixin):
                 wa, cfg, slab, bslab = self._wgrad_halo_args(xin, g, bs, cs.conv.use_bias)
                 if g.i == 0 and self.pro_free:      # the images the stack read from the dataset
                     wa.xidx, wa.xst = self.srcidx.data_ptr(), st_ptr
-                self.launches.append(("wgrad_conv%d" % g.i,
-                                      lambda s, a=wa, c=cfg: K.wgrad_halo(a, c[0], c[1], c[2], s), "side"))
+                wname = "wgrad_conv%d" % g.i
+                self.tail_capable.add(wname)
+                self.launches.append((wname, lambda s, a=wa, c=cfg, nm=wname: self._wgrad_h(a, c, s, nm), "side"))
             w_at = len(self.launches) - 1
             sp = store.spec(cs.conv, "kernel")
             S, ld = cfg[2], g.NT * 16
@@ -1039,10 +1041,10 @@ class BatchPlan(GeometryMixin):
 
     def _early_groups(self):
         """Single-GPU fused-optimizer step: slab groups whose gradients are final before a dual
-        conv backward launch (the head and dense layers before the first one, each conv layer
-        before the next) are reduced and updated by extra workgroups OF that launch
-        (DualExtra) instead of in the end-of-step reduction -- their latency-bound reduce +
-        update overlaps the conv backward.  Only groups no later launch reads the weights of
+        conv backward launch (the head and dense layers before the first one) are reduced and
+        updated by extra workgroups OF that launch (DualExtra) instead of in the end-of-step
+        reduction -- their latency-bound reduce + update overlaps the conv backward; the groups
+        final before the last (first-layer) wgrad launch run in ITS workgroups' tails.  Only groups no later launch reads the weights of
         (pack readers), each launch's as one contiguous parameter span.  Sets
         self.early_red = {launch name: (RedTable, (lo, hi))}; returns the groups assigned."""
         self.early_red = {}
@@ -1056,6 +1058,13 @@ class BatchPlan(GeometryMixin):
         # layers' reductions as extra workgroups measured 2-3 us slower on RPV and MNIST:
         # profiles/r3_s2_early_wgrad_ab.txt)
         duals = [i for i, nm in enumerate(names) if nm.startswith("wgrad_dgrad_conv")][:1]
+        # Tail reduction: the step's LAST launch, when it is a halo wgrad (the first conv
+        # layer's), reduces + updates the earlier conv layers' slabs in its OWN workgroups after
+        # their wgrad work (wgrad_halo.hip) -- not as extra workgroups (measured slower, above):
+        # the early finishers absorb it while the stragglers run, and the separate end-of-step
+        # reduction is left with the first layer's slabs only
+        if tune("tail_reduce", True) and names and names[-1] in getattr(self, "tail_capable", ()):
+            duals.append(len(names) - 1)
         taken = []
         for t in duals:
             late_readers = [(rlo, rhi) for nm, rlo, rhi in self.pack_readers if nm not in names[:t]]

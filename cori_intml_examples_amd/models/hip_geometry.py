@@ -61,6 +61,7 @@ class GeometryMixin:
         a.off_w, (a.off_codes, a.off_codes2), a.lds_bytes = off_w, off_codes, lds
         a.off_bias = off_bias
         a.dbg = tune("stack_dbg", 0)
+        a.k16 = int(tune("stack_k16", False))
         a.set_buf_offsets(off_b0, off_b1)
         a.splits = splits
         for l in range(n):
@@ -224,6 +225,17 @@ class GeometryMixin:
             K.conv_halo(a, ntc, s)
             if early is not None:
                 K.reduce_optim(ex.store.grad.data_ptr(), early[0], ex._optim_args(False, defer_pack=True), s)
+
+    def _wgrad_h(self, wa, cfg, s, name=None):
+        """A halo wgrad launch; when _early_groups gave it a table, its workgroups then run that
+        table's reduction + optimizer (tail reduction, wgrad_halo.hip)."""
+        K, ex = self.ex.K, self.ex
+        early = (self.early_red or {}).get(name)
+        if early is None:
+            K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
+        else:
+            K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s, rt=early[0], ro=ex._optim_args(False, defer_pack=True),
+                         rgrad=ex.store.grad.data_ptr())
 
     def _halo_cfg(self, a, NT, pool, dual=False):
         """Pick n-tiles per workgroup (weight LDS slice) and R output rows per block: the

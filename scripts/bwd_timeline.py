@@ -48,7 +48,7 @@ for name, fn, *_ in bp.launches:
     if name.startswith("wgrad_dgrad"):
         ca, ntc, wa, cfg = dfl[:4]
     else:
-        ca, ntc, (wa, cfg) = None, None, dfl
+        ca, ntc, (wa, cfg) = None, None, dfl[:2]
     MT, NTT, S = cfg
     n_w = S * cdiv(wa.NT, NTT) * cdiv(wa.Ktiles, MT)
     n_c = 0
