@@ -193,6 +193,12 @@ struct WgradArgs {
   // bias, opt_b + n) as soon as their gradient is final -- no slab reduction for the layer
   OptimArgs opt;
   int opt_w = -1, opt_b = -1;
+  // ... and (pk_fwd >= 0) the updated weights' bf16 copies written into the layer's forward /
+  // backward fragment packs (element offsets in opt.arena, their n-tile counts) as whole
+  // 16-byte vectors from an LDS tile -- the workgroup's 32 features x NTT*16 outputs are
+  // complete pack vectors of both packs, so no re-pack pass is needed for the layer
+  long long pk_fwd = -1, pk_bwd = -1;
+  int pk_NT = 0, pk_NTb = 0;
   // wgrad_halo LDS layout (models/lds_layout.py picks it with a bank-conflict model; 0 =
   // dense): X-halo pixel stride in elements, X-halo row stride in pixels, dY row stride
   int xpix = 0, xrow = 0, dyld = 0;

@@ -102,7 +102,8 @@ PYBIND11_MODULE(_kernels, m) {
       RW(WgradArgs, blocks_per_split) PTR(WgradArgs, dy_code) PTR(WgradArgs, zero) RW(WgradArgs, dHp) RW(WgradArgs, dWp)
       RW(WgradArgs, dbg) PTR(WgradArgs, ts) PTR(WgradArgs, ts2) RW(WgradArgs, opt) RW(WgradArgs, opt_w)
       RW(WgradArgs, opt_b) RW(WgradArgs, xpix) RW(WgradArgs, xrow) RW(WgradArgs, dyld) RW(WgradArgs, kperm)
-      PTR(WgradArgs, xidx) PTR(WgradArgs, xst);
+      PTR(WgradArgs, xidx) PTR(WgradArgs, xst) RW(WgradArgs, pk_fwd) RW(WgradArgs, pk_bwd) RW(WgradArgs, pk_NT)
+      RW(WgradArgs, pk_NTb);
 
   py::class_<DenseFwdArgs>(m, "DenseFwdArgs")
       .def(py::init<>())

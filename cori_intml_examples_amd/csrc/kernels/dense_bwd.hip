@@ -71,8 +71,8 @@ __device__ __forceinline__ void dw_opt(const OptimArgs& o, float& p, float g, fl
 }
 
 // fused update of 4 consecutive elements [e, e+4) whose gradient is g; p / s0 / s1 are
-// their current values (loaded early by the caller)
-__device__ __forceinline__ void dw_opt4(const OptimArgs& o, size_t e, const f32x4& g, f32x4 p, f32x4 s0, f32x4 s1) {
+// their current values (loaded early by the caller); returns the updated weights
+__device__ __forceinline__ f32x4 dw_opt4(const OptimArgs& o, size_t e, const f32x4& g, f32x4 p, f32x4 s0, f32x4 s1) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     float pq = p[q], m = s0[q], v = s1[q];
@@ -82,7 +82,10 @@ __device__ __forceinline__ void dw_opt4(const OptimArgs& o, size_t e, const f32x
   *reinterpret_cast<f32x4*>(o.p + e) = p;
   if (o.s0) *reinterpret_cast<f32x4*>(o.s0 + e) = s0;
   if (o.s1) *reinterpret_cast<f32x4*>(o.s1 + e) = s1;
+  return p;
 }
+
+constexpr int DW_PKLD = 128 + 8;   // bf16 row stride of the updated-weight tile (<= 128 outputs)
 }   // namespace
 
 size_t dense_wgrad_lds_bytes(int kg, int ntt) {
@@ -94,7 +97,8 @@ size_t dense_wgrad_lds_bytes(int kg, int ntt) {
     default: stage = 4 * DwGeom<8>::WAVE_BYTES; red = (size_t)4 * 16 * DwGeom<8>::LDR * 4; break;
   }
   (void)kg;
-  return std::max(stage, red + 16 * 128 * 4);
+  // + the updated-weight bf16 tile of the fused optimizer's pack writes (32 x <= 128)
+  return std::max(stage, red + 16 * 128 * 4 + (size_t)32 * DW_PKLD * 2);
 }
 
 template <int KG, int NTT, bool OPT>
@@ -205,6 +209,8 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);                   // [4 waves][16][LDR]
   float* bred = red + 4 * 16 * G::LDR;                           // [4 waves][4 groups][128]
+  bf16* pkt = reinterpret_cast<bf16*>(bred + 16 * 128);          // [KG*16][DW_PKLD] updated weights
+  const bool packs = OPT && a.pk_fwd >= 0;
   float* slab = a.slab + (size_t)bx * a.Ktiles * 16 * ld;
   if (do_bias) {
 #pragma unroll
@@ -229,10 +235,44 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
       for (int w = 1; w < 4; ++w) s += *reinterpret_cast<const f32x4*>(red + (w * 16 + row) * G::LDR + c4 * 4);
       if (f < a.Ktiles * 16 && n < ld) {
         *reinterpret_cast<f32x4*>(slab + (size_t)f * ld + n) = s;
-        if constexpr (OPT) dw_opt4(a.opt, (size_t)a.opt_w + (size_t)f * ld + n, s, op[kt][q], om[kt][q], ov[kt][q]);
+        if constexpr (OPT) {
+          const f32x4 pn = dw_opt4(a.opt, (size_t)a.opt_w + (size_t)f * ld + n, s, op[kt][q], om[kt][q], ov[kt][q]);
+          if (packs) {
+            bf16* d = pkt + (kt * 16 + row) * DW_PKLD + c4 * 4;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) d[u] = f2bf(pn[u]);
+          }
+        }
       }
     }
     __syncthreads();
+  }
+  if constexpr (OPT) {
+    if (packs && KG * 16 == 32) {
+      // whole 16-byte vectors of both packs from the tile (the loop's last barrier published it):
+      //   fwd  B[k = feature][n = output]: vector (ks = f0/32, nt, lane) = 8 features of one output
+      //   bwd  B[k = output][n = feature]: vector (ksb, ntb, lane)       = 8 outputs of one feature
+      bf16* ar = a.opt.arena;
+      const int ks = f0 >> 5;
+      for (int v = tid; v < NTT * 64; v += 256) {
+        const int ntl = v >> 6, lane_ = v & 63, nt = (n0 >> 4) + ntl;
+        if (nt >= a.NT) continue;
+        bf16x8 w;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = pkt[(8 * (lane_ >> 4) + j) * DW_PKLD + ntl * 16 + (lane_ & 15)];
+        *reinterpret_cast<bf16x8*>(ar + a.pk_fwd + ((size_t)(ks * a.pk_NT + nt) * 64 + lane_) * 8) = w;
+      }
+      if (a.pk_bwd >= 0 && (NTT & 1) == 0) {
+        for (int v = tid; v < (NTT / 2) * KG * 64; v += 256) {
+          const int lane_ = v & 63, t2 = v >> 6, ntbl = t2 % KG, ksbl = t2 / KG;
+          const int ksb = (n0 >> 5) + ksbl, ntb = (f0 >> 4) + ntbl;
+          if (n0 + ksbl * 32 >= ld) continue;
+          const bf16x8 w = *reinterpret_cast<const bf16x8*>(pkt + (ntbl * 16 + (lane_ & 15)) * DW_PKLD + ksbl * 32 +
+                                                            8 * (lane_ >> 4));
+          *reinterpret_cast<bf16x8*>(ar + a.pk_bwd + ((size_t)(ksb * a.pk_NTb + ntb) * 64 + lane_) * 8) = w;
+        }
+      }
+    }
   }
   if (do_bias && tid < NTT * 16 && n0 + tid < ld) {
     float b = 0.f;
@@ -249,7 +289,7 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
       if (o.s1) o.s1[e] = s1;
     }
   }
-  if (OPT && a.opt.defer_pack && bx == 0 && by == 0 && bz == 0 && tid == 0) a.opt.st->packs_stale = 1;
+  if (OPT && !packs && a.opt.defer_pack && bx == 0 && by == 0 && bz == 0 && tid == 0) a.opt.st->packs_stale = 1;
 }
 
 template <int NTC>
@@ -349,6 +389,10 @@ static void dense_wgrad_check(const WgradArgs& a, int kg, int ntt, int splits) {
   if (a.opt_w >= 0 && (splits != 1 || a.opt.p == nullptr || a.opt.st == nullptr || a.opt_w % 4 ||
                        (a.NT * 16) % 4))
     throw std::runtime_error("dense_wgrad: fused optimizer needs one split and float4-aligned rows");
+  if (a.pk_fwd >= 0 && (a.opt_w < 0 || a.opt.arena == nullptr || kg != 2 || (a.pk_bwd >= 0 && (ntt & 1)) ||
+                        a.Cs_in % 32 || (a.NT * 16) % 32))
+    throw std::runtime_error("dense_wgrad: fused pack writes need the fused optimizer, 32-feature tiles and "
+                             "32-aligned widths");
 }
 static void dense_dx_check(const DenseFwdArgs& a, int ntc) {
   if (!(ntc == 1 || ntc == 2 || ntc == 4) || a.mode != 1 || a.splits != 1 || a.bt.pCs % 8 || a.Ks % 8)

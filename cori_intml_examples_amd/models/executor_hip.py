@@ -306,8 +306,9 @@ class HipExecutor(Executor):
             sp = st.spec(ds.dense, "kernel")
             routes.append((sp.offset, sp.offset + sp.numel, 2, g.src.H * g.src.W, g.src.C, g.N, g.src.Cs, 0,
                            g.NT, g.NTb if g.KSb else 0, g.pack_fwd, g.pack_bwd if g.KSb else -1))
-        self.routes_ok = (bool(routes) and len(routes) <= K.MAX_ROUTES and tune("opt_packs", True)
-                          and not tune("dense_opt", False))
+        # (a dense layer whose optimizer runs inside its wgrad kernel writes its packs there
+        # too -- WgradArgs.pk_fwd -- or is not fused: see BatchPlan._build_args)
+        self.routes_ok = bool(routes) and len(routes) <= K.MAX_ROUTES and tune("opt_packs", True)
         self.routes = None
         self.route_list = routes
         if self.routes_ok:
@@ -811,7 +812,14 @@ class BatchPlan(GeometryMixin):
         # slower on RPV at batch 128: the 128 wgrad workgroups move the layer's 14 MB of optimizer
         # state at per-CU bandwidth (wgrad 6.1 -> 9.7 us) while the end-of-step reduction, which
         # spreads it over thousands of workgroups, only drops 10.8 -> 8.2 us
-        self.dense_opt_ok = ex.reducer is None and tune("fuse_optim", True) and tune("dense_opt", False)
+        # dense_opt: "auto" = only layers whose gradient is written in place (> 16 MB, the legacy
+        # model's 33.5M-weight Dense(512)): their update moves ~1 GB either way, and fusing it
+        # saves the gradient's own write + re-read; "1" = every one-split layer (measured slower
+        # on the 0.5M-weight RPV dense at batch 128: 128 workgroups carry 14 MB of state)
+        dense_opt = str(tune("dense_opt", "auto")).lower()
+        self.dense_opt_ok = (ex.reducer is None and tune("fuse_optim", True)
+                             and dense_opt not in ("0", "false", "off", "no"))
+        self.dense_opt_all = dense_opt in ("1", "true", "on", "yes")
 
         for g, ds in reversed(list(zip(ex.denses, ex.plan.denses))):
             xin = self._src_buf(g.src)
@@ -832,13 +840,21 @@ class BatchPlan(GeometryMixin):
                 # one split + identity layout: the kernel's fixed-order sum IS the Keras
                 # gradient -- write it in place and apply the optimizer there (single GPU,
                 # fused-optimizer step), so the layer skips the end-of-step reduction
-                fused_opt = (self.dense_opt_ok and cfg[2] == 1 and g.src.C == g.src.Cs and g.N % 16 == 0
-                             and sp.offset % 4 == 0)
+                fused_opt = (self.dense_opt_ok and (self.dense_opt_all or direct)
+                             and cfg[2] == 1 and g.src.C == g.src.Cs and g.N % 16 == 0 and sp.offset % 4 == 0)
+                # with optimizer-written packs the kernel must write this layer's packs itself
+                pk_ok = (cfg[0] == 2 and g.src.width % 32 == 0 and g.N % 32 == 0
+                         and (not g.KSb or cfg[1] % 2 == 0))
+                if fused_opt and ex.routes_ok and not pk_ok:
+                    fused_opt = False
                 if fused_opt:
                     grad = store.grad.data_ptr()
                     wa.slab = grad + 4 * sp.offset
                     wa.opt = ex._optim_args(False, defer_pack=True)
                     wa.opt_w = sp.offset
+                    if ex.routes_ok:
+                        wa.pk_fwd, wa.pk_NT = g.pack_fwd, g.NT
+                        wa.pk_bwd, wa.pk_NTb = (g.pack_bwd, g.NTb) if g.KSb else (-1, 0)
                     if ds.dense.use_bias:
                         wa.bslab = grad + 4 * store.spec(ds.dense, "bias").offset
                         wa.opt_b = store.spec(ds.dense, "bias").offset

@@ -83,3 +83,39 @@ def test_dense_fused_optimizer_matches_reduction(monkeypatch):
     assert out["0"][1] == 0 and out["1"][1] == 1, "fused path not taken / taken by default"
     d = np.abs(out["1"][0] - out["0"][0])
     assert np.quantile(d, 0.999) < 1e-5 and d.max() < 2e-3, (np.quantile(d, 0.999), d.max())
+
+
+@gpu
+def test_dense_fused_optimizer_writes_packs_legacy(monkeypatch):
+    """Legacy RPV (Dense(512) on a flattened 16384-wide input: its gradient is written in
+    place) with the optimizer fused into the dense wgrad by default (dense_opt=auto): the
+    kernel also writes the layer's forward / backward bf16 packs from its updated-weight tile,
+    so after a few steps (a) the packs equal a full re-pack of the master bit for bit and
+    (b) the weights match the unfused path (update in the end-of-step optimizer) within
+    Adam's last-ulp bound."""
+    from cori_intml_examples_amd.apps import zoo
+    rs = np.random.RandomState(4)
+    x = torch.tensor(rs.rand(96, 32, 32, 3).astype(np.float32)).to(torch.bfloat16).float().numpy()
+    y = (rs.rand(96) > 0.5).astype(np.float32)
+    np.random.seed(2)
+    torch.manual_seed(2)
+    w0 = zoo.rpv_legacy_cnn((32, 32, 3), lr=1e-3, device="cuda:0").get_weights()
+    out = {}
+    for flag in ("auto", "0"):
+        monkeypatch.setenv("INTML_TUNE", "dense_opt=" + flag)
+        m = zoo.rpv_legacy_cnn((32, 32, 3), lr=1e-3, device="cuda:0")
+        m.set_weights(w0)
+        for i in range(3):
+            m.train_on_batch(x[i * 32:(i + 1) * 32], y[i * 32:(i + 1) * 32])
+        torch.cuda.synchronize()
+        ex = m._executor
+        plan = next(iter(ex._plans.values()))
+        arena = ex.arena.clone()
+        ex.params_changed()                  # full re-pack from the master
+        torch.cuda.synchronize()
+        out[flag] = (np.concatenate([w.ravel() for w in m.get_weights()]), len(plan.dense_fused_opt),
+                     bool(plan.optim_fused), torch.equal(arena, ex.arena))
+    assert out["auto"][1] == 1 and out["0"][1] == 0, "fused path not taken by default / taken with dense_opt=0"
+    assert out["auto"][3], "packs written by the fused dense optimizer differ from a re-pack"
+    d = np.abs(out["auto"][0] - out["0"][0])
+    assert np.quantile(d, 0.999) < 1e-5 and d.max() < 3e-3, (np.quantile(d, 0.999), d.max())
