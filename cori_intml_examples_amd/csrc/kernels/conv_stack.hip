@@ -419,15 +419,6 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   const uint32_t step = A.st ? (uint32_t)A.st->t + (uint32_t)A.step_inc : 0u;
   STACK_STAMP(0);
   if (tid < 8) ((LDS uint32_t*)zl)[tid] = 0u;
-  // biases -> LDS [layer][64] (read by the epilogues: no global load after the prefetch
-  // below, which would otherwise make its first use wait for every prefetched vector)
-  LDS float* lbias = (LDS float*)(smem + A.off_bias);
-  for (int i = tid; i < A.n * 64; i += STACK_THREADS) {
-    const StackLayer& L = A.L[i >> 6];
-    const int c = i & 63;
-    lbias[i] = (L.bias && c < L.Cout) ? L.bias[c] : 0.f;
-  }
-
   // Weight packs -> LDS.  Layer 0's synchronously; the later layers' are loaded into
   // registers now (issued after the image, so waiting for the image does not wait for them)
   // and written to LDS only before layer 1 -- their latency hides behind layer 0.
@@ -437,60 +428,117 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   const int nv2 = A.n > 2 ? A.L[2].KS * A.L[2].NT * 64 : 0;
   const int nv3 = A.n > 3 ? A.L[3].KS * A.L[3].NT * 64 : 0;
   const bool prefetch = !(A.dbg & 40) && A.n > 1 && nv1 + nv2 + nv3 <= PF * STACK_THREADS;   // (32: A/B, exact)
-  for (int l = 0; l < ((A.dbg & 8) ? 0 : (prefetch ? 1 : A.n)); ++l) {
-    const StackLayer& L = A.L[l];
-    const int nv = L.KS * L.NT * 64;
-    const bf16* src = L.wpk;
-    lbf16* dst = wlds + L.w_lds;
-    staged_copy<4, bf16x8>(
-        nv, tid, STACK_THREADS, [&](int i) { return load_bf16x8(src + (size_t)i * 8); },
-        [&](int i, const bf16x8& v) { *reinterpret_cast<LDS bf16x8*>(dst + i * 8) = v; });
-  }
-  // the image rows layer 0 needs -> its zero-padded halo image
-  if (!(A.dbg & 8)) {
+  // Fast prologue (the RPV / MNIST stacks: 4-channel input, one batch of image loads per
+  // thread): every global round trip of the staging in ONE batch -- the biases and layer 0's
+  // weight pack are loaded first (independent of the image), then the image's dataset row
+  // (scalar chain through the cursor and permutation) and its pixels, and only then are all
+  // of them stored to LDS.  The sequential form (biases, weights, row lookup, pixels: five
+  // dependent round trips) is kept for the other shapes and as the A/B reference (dbg 128).
+  LDS float* lbias = (LDS float*)(smem + A.off_bias);
+  const int nv0 = A.L[0].KS * A.L[0].NT * 64;
+  const int hiwi0 = A.rows[0][sp][5] * (A.L[0].Wo + A.L[0].KW - 1);
+  const bool fastpro = !(A.dbg & (8 | 128)) && prefetch && A.L[0].Cs_in == 4 && nv0 <= STACK_THREADS &&
+                       A.n * 64 <= STACK_THREADS && hiwi0 <= 4 * STACK_THREADS;
+  if (fastpro) {
     const StackLayer& L = A.L[0];
+    const int bl = min(tid, A.n * 64 - 1), bc = bl & 63;
+    const StackLayer& LB = A.L[bl >> 6];
+    const bool bok = tid < A.n * 64 && LB.bias != nullptr && bc < LB.Cout;
+    const float braw = *(bok ? LB.bias + bc : reinterpret_cast<const float*>(L.wpk));
+    const bf16x8 wv = load_bf16x8(L.wpk + (size_t)min(tid, nv0 - 1) * 8);
     lbf16* img = (lbf16*)(smem + A.off_buf[0]);
-    const int Hi = A.rows[0][sp][5], Wi = L.Wo + L.KW - 1, Cs = L.Cs_in;
-    const int XR = L.xrow, XP = L.xpix;
-    const int y0 = A.rows[0][sp][4];
-    const bf16* x = A.x + (size_t)b * L.H * L.W * Cs;
-    if (A.from_data) {   // straight from the bound dataset: no gather launch
+    const int Wi = L.Wo + L.KW - 1, XR = L.xrow, XP = L.xpix, y0 = A.rows[0][sp][4];
+    const bf16* x = A.x + (size_t)b * L.H * L.W * 4;
+    if (A.from_data) {
       const int src = step_src_row(A.st, A.training, b);
       x = reinterpret_cast<const bf16*>(A.st->data_x) + (size_t)src * A.st->data_R;
       if (sp == 0 && tid == 0 && A.srcidx) A.srcidx[b] = src;
     }
-    if (Cs == 4) {
-      const FastDiv fwi(Wi);
-      staged_copy<8, bf16x4>(
-          Hi * Wi, tid, STACK_THREADS,
-          [&](int i) {
-            const int hy = fwi.div(i), hx = i - hy * Wi;
-            const int iy = y0 + hy, ix = hx - L.pad_l;
-            const bool ok = iy >= 0 && ix >= 0 && iy < L.H && ix < L.W;
-            return load_bf16x4_if(ok, x + (iy * L.W + ix) * 4, x);
-          },
-          [&](int i, const bf16x4& v) {
-            const int hy = fwi.div(i);
-            *reinterpret_cast<LDS bf16x4*>(img + (hy * XR + (i - hy * Wi)) * XP) = v;
-          });
-    } else {
-      const int cpp = Cs >> 3;
-      const FastDiv fcpp(cpp), fwi(Wi);
-      staged_copy<8, bf16x8>(
-          Hi * Wi * cpp, tid, STACK_THREADS,
-          [&](int i) {
-            const int pix = fcpp.div(i), c = (i - pix * cpp) * 8;
-            const int hy = fwi.div(pix), hx = pix - hy * Wi;
-            const int iy = y0 + hy, ix = hx - L.pad_l;
-            const bool ok = iy >= 0 && ix >= 0 && iy < L.H && ix < L.W;
-            return load_bf16x8_if(ok, x + (iy * L.W + ix) * Cs + c, x);
-          },
-          [&](int i, const bf16x8& v) {
-            const int pix = fcpp.div(i), c = (i - pix * cpp) * 8;
-            const int hy = fwi.div(pix);
-            *reinterpret_cast<LDS bf16x8*>(img + (hy * XR + (pix - hy * Wi)) * XP + c) = v;
-          });
+    const FastDiv fwi(Wi);
+    bf16x4 iv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(tid + u * STACK_THREADS, hiwi0 - 1);
+      const int hy = fwi.div(i), hx = i - hy * Wi;
+      const int iy = y0 + hy, ix = hx - L.pad_l;
+      const bool ok = iy >= 0 && ix >= 0 && iy < L.H && ix < L.W;
+      iv[u] = load_bf16x4_if(ok, x + (iy * L.W + ix) * 4, x);
     }
+    if (tid < A.n * 64) lbias[tid] = bok ? braw : 0.f;
+    if (tid < nv0) *reinterpret_cast<LDS bf16x8*>(wlds + L.w_lds + tid * 8) = wv;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + u * STACK_THREADS;
+      if (i < hiwi0) {
+        const int hy = fwi.div(i);
+        *reinterpret_cast<LDS bf16x4*>(img + (hy * XR + (i - hy * Wi)) * XP) = iv[u];
+      }
+    }
+  } else {
+    // biases -> LDS [layer][64] (read by the epilogues: no global load after the prefetch
+    // below, which would otherwise make its first use wait for every prefetched vector)
+    for (int i = tid; i < A.n * 64; i += STACK_THREADS) {
+      const StackLayer& L = A.L[i >> 6];
+      const int c = i & 63;
+      lbias[i] = (L.bias && c < L.Cout) ? L.bias[c] : 0.f;
+    }
+
+    for (int l = 0; l < ((A.dbg & 8) ? 0 : (prefetch ? 1 : A.n)); ++l) {
+      const StackLayer& L = A.L[l];
+      const int nv = L.KS * L.NT * 64;
+      const bf16* src = L.wpk;
+      lbf16* dst = wlds + L.w_lds;
+      staged_copy<4, bf16x8>(
+          nv, tid, STACK_THREADS, [&](int i) { return load_bf16x8(src + (size_t)i * 8); },
+          [&](int i, const bf16x8& v) { *reinterpret_cast<LDS bf16x8*>(dst + i * 8) = v; });
+    }
+    // the image rows layer 0 needs -> its zero-padded halo image
+    if (!(A.dbg & 8)) {
+      const StackLayer& L = A.L[0];
+      lbf16* img = (lbf16*)(smem + A.off_buf[0]);
+      const int Hi = A.rows[0][sp][5], Wi = L.Wo + L.KW - 1, Cs = L.Cs_in;
+      const int XR = L.xrow, XP = L.xpix;
+      const int y0 = A.rows[0][sp][4];
+      const bf16* x = A.x + (size_t)b * L.H * L.W * Cs;
+      if (A.from_data) {   // straight from the bound dataset: no gather launch
+        const int src = step_src_row(A.st, A.training, b);
+        x = reinterpret_cast<const bf16*>(A.st->data_x) + (size_t)src * A.st->data_R;
+        if (sp == 0 && tid == 0 && A.srcidx) A.srcidx[b] = src;
+      }
+      if (Cs == 4) {
+        const FastDiv fwi(Wi);
+        staged_copy<8, bf16x4>(
+            Hi * Wi, tid, STACK_THREADS,
+            [&](int i) {
+              const int hy = fwi.div(i), hx = i - hy * Wi;
+              const int iy = y0 + hy, ix = hx - L.pad_l;
+              const bool ok = iy >= 0 && ix >= 0 && iy < L.H && ix < L.W;
+              return load_bf16x4_if(ok, x + (iy * L.W + ix) * 4, x);
+            },
+            [&](int i, const bf16x4& v) {
+              const int hy = fwi.div(i);
+              *reinterpret_cast<LDS bf16x4*>(img + (hy * XR + (i - hy * Wi)) * XP) = v;
+            });
+      } else {
+        const int cpp = Cs >> 3;
+        const FastDiv fcpp(cpp), fwi(Wi);
+        staged_copy<8, bf16x8>(
+            Hi * Wi * cpp, tid, STACK_THREADS,
+            [&](int i) {
+              const int pix = fcpp.div(i), c = (i - pix * cpp) * 8;
+              const int hy = fwi.div(pix), hx = pix - hy * Wi;
+              const int iy = y0 + hy, ix = hx - L.pad_l;
+              const bool ok = iy >= 0 && ix >= 0 && iy < L.H && ix < L.W;
+              return load_bf16x8_if(ok, x + (iy * L.W + ix) * Cs + c, x);
+            },
+            [&](int i, const bf16x8& v) {
+              const int pix = fcpp.div(i), c = (i - pix * cpp) * 8;
+              const int hy = fwi.div(pix);
+              *reinterpret_cast<LDS bf16x8*>(img + (hy * XR + (pix - hy * Wi)) * XP + c) = v;
+            });
+      }
+    }
+
   }
 
   // k-chunk -> halo offset tables of every layer (the generic path reads them; the

@@ -527,3 +527,24 @@ def test_stack_k16_tail_bit_identical(kind, drop, cin, hw, monkeypatch):
         torch.cuda.synchronize()
         res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
     assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
+
+
+@pytest.mark.parametrize("kind,drop,cin,hw", [("rpv", 0.2, 3, 64), ("mnist", 0.3, 1, 28)])
+def test_stack_fast_prologue_bit_identical(kind, drop, cin, hw, monkeypatch):
+    """The conv stack's one-batch prologue (biases, layer-0 weights, the image's dataset row
+    and pixels loaded together before any LDS store) stages exactly what the sequential
+    prologue (stack_dbg=128) does: whole training steps bit-identical."""
+    res = []
+    for tv in ("stack_dbg=0", "stack_dbg=128"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(49)
+        m = _build(kind, "cuda", opt="Adam", drop=drop, cin=cin, hw=hw)
+        x, y = _data(m, 256, seed=13)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(9)).to(ex.device)
+        ex.reset_metrics()
+        ex.train_steps(d, perm, 0, 128, 2)
+        torch.cuda.synchronize()
+        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
+    assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
