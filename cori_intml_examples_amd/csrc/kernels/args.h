@@ -63,6 +63,9 @@ struct OptimArgs {
   // 16-byte pack vectors instead of scattered 2-byte stores); the flat blocks skip them
   int ntile = 0, flat_blocks = 0;
   int tile_route[4] = {0, 0, 0, 0}, tile_b0[5] = {0, 0, 0, 0, 0};   // tile_b0[ntile] = tile blocks
+  // reduction kernels only: write the reduced gradient and stop (no update, no packs) -- the
+  // data-parallel step reduces early buckets' slabs ahead of the all-reduce this way
+  int grad_only = 0;
 };
 
 // Implicit-GEMM convolution / 1x1 "dense as conv" (fwd, dgrad, dense-dX).

@@ -185,6 +185,7 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(OptimArgs, p) PTR(OptimArgs, g) PTR(OptimArgs, s0) PTR(OptimArgs, s1) RW(OptimArgs, n) RW(OptimArgs, lo)
       PTR(OptimArgs, st) RW(OptimArgs, kind) RW(OptimArgs, beta1) RW(OptimArgs, beta2) RW(OptimArgs, eps)
       RW(OptimArgs, rho) RW(OptimArgs, momentum) RW(OptimArgs, nesterov) RW(OptimArgs, grad_scale)
+      RW(OptimArgs, grad_only)
       RW(OptimArgs, pack_only) RW(OptimArgs, defer_pack) PTR(OptimArgs, arena) PTR(OptimArgs, routes)
       RW(OptimArgs, nroutes) RW(OptimArgs, ntile) RW(OptimArgs, flat_blocks)
       .def("set_tile", [](OptimArgs& a, int i, int route, int b0) {

@@ -116,15 +116,16 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
     // tiled pack writes (dsc.tile): the workgroup's 1024 updated weights are whole 8-row groups
     // of its dense route -- staged as bf16 in LDS (red: >= 2 KB), written as 16-byte vectors
     const PackRoute* tr = nullptr;
-    if (a.nroutes && dsc.tile) {
+    if (a.nroutes && dsc.tile && !a.grad_only) {
       for (int r = 0; r < a.nroutes; ++r) {           // uniform: the descriptor's route
         const PackRoute& R = a.routes[r];
         if (R.kind == 2 && R.Cin == R.Cs && dsc.dst_off >= R.lo && dsc.dst_off < R.hi) tr = &R;
       }
     }
     bf16* tl = reinterpret_cast<bf16*>(red);
-    if (slab_reduce_vec4(dsc, blk, e, g)) {
-      *reinterpret_cast<float4*>(grad + e) = g;
+    const bool mine = slab_reduce_vec4(dsc, blk, e, g);
+    if (mine) *reinterpret_cast<float4*>(grad + e) = g;
+    if (mine && !a.grad_only) {           // (grad_only: the reduced gradient is all)
       float4 p = *reinterpret_cast<const float4*>(a.p + e);
       float4 s0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : float4{0.f, 0.f, 0.f, 0.f};
       float4 s1 = a.s1 ? *reinterpret_cast<const float4*>(a.s1 + e) : float4{0.f, 0.f, 0.f, 0.f};
@@ -166,8 +167,9 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
   } else {
     int e;
     float g;
-    if (slab_reduce_elem(tab, blk, red, e, g)) {
-      grad[e] = g;
+    const bool mine = slab_reduce_elem(tab, blk, red, e, g);
+    if (mine) grad[e] = g;
+    if (mine && !a.grad_only) {
       float p = a.p[e];
       float s0 = a.s0 ? a.s0[e] : 0.f, s1 = a.s1 ? a.s1[e] : 0.f;
       opt_update<KIND>(a, a.st, p, g * a.grad_scale, &s0, &s1);
@@ -177,7 +179,7 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
       if (a.nroutes) pack_write(a, e, p);
     }
   }
-  if (a.defer_pack && !a.nroutes && blk == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
+  if (a.defer_pack && !a.nroutes && !a.grad_only && blk == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
 }
 
 // the same with the optimizer kind chosen at run time (a workgroup-uniform switch)

@@ -979,8 +979,16 @@ class BatchPlan(GeometryMixin):
         ex, K = self.ex, self.ex.K
         groups = [(lo, hi) for lo, hi, _ in self.red_groups]
         reducer = ex.reducer
+        dp_early = []
         if reducer is not None:
             bucket_groups = reducer.configure(groups)
+            # one bucket at the end of the backward (the adaptive plan for gradients <= 16 MB):
+            # the groups final before a carrier launch (the first dual launch, the last wgrad
+            # launch -- the single-GPU step's carriers) are REDUCED early there (grad_only: no
+            # update), so the end-of-backward reduction ahead of the all-reduce only has the
+            # first layer's slabs left (the update stays behind the all-reduce)
+            if len(bucket_groups) == 1 and self.comm_in_graph and tune("dp_early", True):
+                dp_early = self._early_groups(grad_only=True)
         else:
             # single stream, no all-reduce to overlap: ONE reduction launch at the end of the
             # backward (each launch boundary costs ~5 us here), if the descriptors fit a table
@@ -1015,7 +1023,8 @@ class BatchPlan(GeometryMixin):
             tab = K.RedTable()
             # longest reductions (most slabs) first: their workgroups dispatch first and their
             # memory round trips overlap the many short ones instead of trailing the launch
-            for d in sorted((d for i in bg for d in self.red_groups[i][2]), key=lambda d: -d[2]):
+            for d in sorted((d for i in bg if i not in dp_early for d in self.red_groups[i][2]),
+                            key=lambda d: -d[2]):
                 tab.add(*d)
             lo = min(self.red_groups[i][0] for i in bg)
             hi = max(self.red_groups[i][1] for i in bg)
@@ -1052,17 +1061,20 @@ class BatchPlan(GeometryMixin):
                                                 [(lo, hi) for lo, hi, _ in self.bucket_tables],
                                                 self.pack_readers)
         spans = [(lo, hi) for lo, hi, _ in self.bucket_tables]
-        spans += [span for _, span in (self.early_red or {}).values()]
+        # (grad-only early reductions lie inside their all-reduce bucket's span)
+        spans += [e[1] for e in (self.early_red or {}).values() if not e[2]]
         check_bucket_cover(spans, ex.store.numel)
 
-    def _early_groups(self):
+    def _early_groups(self, grad_only: bool = False):
         """Single-GPU fused-optimizer step: slab groups whose gradients are final before a dual
         conv backward launch (the head and dense layers before the first one) are reduced and
         updated by extra workgroups OF that launch (DualExtra) instead of in the end-of-step
         reduction -- their latency-bound reduce + update overlaps the conv backward; the groups
         final before the last (first-layer) wgrad launch run in ITS workgroups' tails.  Only groups no later launch reads the weights of
         (pack readers), each launch's as one contiguous parameter span.  Sets
-        self.early_red = {launch name: (RedTable, (lo, hi))}; returns the groups assigned."""
+        self.early_red = {launch name: (RedTable, (lo, hi), grad_only)}; returns the groups
+        assigned.  grad_only (data-parallel step): reduction only -- no update, no pack
+        writes, so later pack readers do not matter."""
         self.early_red = {}
         if not tune("early_reduce", True):
             return []
@@ -1083,7 +1095,8 @@ class BatchPlan(GeometryMixin):
             duals.append(len(names) - 1)
         taken = []
         for t in duals:
-            late_readers = [(rlo, rhi) for nm, rlo, rhi in self.pack_readers if nm not in names[:t]]
+            late_readers = [] if grad_only else [(rlo, rhi) for nm, rlo, rhi in self.pack_readers
+                                                 if nm not in names[:t]]
             grp = [gi for gi in range(len(self.red_groups)) if gi not in taken and self.red_ready[gi] <= t
                    and not any(rlo < self.red_groups[gi][1] and rhi > self.red_groups[gi][0]
                                for rlo, rhi in late_readers)]
@@ -1098,7 +1111,7 @@ class BatchPlan(GeometryMixin):
             tab = self.ex.K.RedTable()
             for d in sorted(descs, key=lambda d: -d[2]):
                 tab.add(*d)
-            self.early_red[names[t]] = (tab, (lo, hi))
+            self.early_red[names[t]] = (tab, (lo, hi), grad_only)
             taken += grp
         return taken
 

@@ -217,14 +217,14 @@ class GeometryMixin:
         K, ex = self.ex.K, self.ex
         early = (self.early_red or {}).get(name)
         kw = {}
-        if early is not None:   # this launch also carries an early bucket's reduction + optimizer
-            kw.update(rt=early[0], ro=ex._optim_args(False, defer_pack=True), rgrad=ex.store.grad.data_ptr())
+        if early is not None:   # this launch also carries an early bucket's reduction (+ optimizer)
+            kw.update(rt=early[0], ro=self._early_ro(early), rgrad=ex.store.grad.data_ptr())
         ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, **kw)
         if not ok:   # unsupported combination
             K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
             K.conv_halo(a, ntc, s)
             if early is not None:
-                K.reduce_optim(ex.store.grad.data_ptr(), early[0], ex._optim_args(False, defer_pack=True), s)
+                K.reduce_optim(ex.store.grad.data_ptr(), early[0], self._early_ro(early), s)
 
     def _wgrad_h(self, wa, cfg, s, name=None):
         """A halo wgrad launch; when _early_groups gave it a table, its workgroups then run that
@@ -234,8 +234,15 @@ class GeometryMixin:
         if early is None:
             K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
         else:
-            K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s, rt=early[0], ro=ex._optim_args(False, defer_pack=True),
+            K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s, rt=early[0], ro=self._early_ro(early),
                          rgrad=ex.store.grad.data_ptr())
+
+    def _early_ro(self, early):
+        """OptimArgs of an early reduction table: the Keras update, or (data-parallel step,
+        early[2]) the reduction only -- the update follows the all-reduce."""
+        ro = self.ex._optim_args(False, defer_pack=True)
+        ro.grad_only = int(early[2])
+        return ro
 
     def _halo_cfg(self, a, NT, pool, dual=False):
         """Pick n-tiles per workgroup (weight LDS slice) and R output rows per block: the
