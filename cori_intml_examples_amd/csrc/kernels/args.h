@@ -18,6 +18,7 @@ struct BwdThrough {
   float drop_scale = 1.f;
   uint32_t seed = 0, stream_id = 0;
   bf16* dy = nullptr;                   // output [B, cH, cW, pCs] (or [B, pH, pW, pCs])
+  int wt = 0;                           // dy stored write-through (16-byte sc1 stores; < 2 GB)
 };
 
 // Where an updated master element goes in the bf16 fragment packs (pack_write, optim_math.h):
@@ -163,6 +164,8 @@ struct ConvStackArgs {
   // as one v_mfma_f32_16x16x16_bf16 with a single 8-byte A read, instead of a 16x16x32 whose
   // other 28 k are zero weights
   int k16 = 0;
+  // wt: stage outputs and argmax codes stored write-through (16-byte sc1 buffer stores)
+  int wt = 0;
 };
 
 // Weight gradient: dW[k][n] = sum_pixels im2col(x)[p][k] * dY[p][n]  (split over pixels)
@@ -202,6 +205,7 @@ struct WgradArgs {
   // complete pack vectors of both packs, so no re-pack pass is needed for the layer
   long long pk_fwd = -1, pk_bwd = -1;
   int pk_NT = 0, pk_NTb = 0;
+  int wt = 0;                    // halo kernels: slabs stored write-through (16-byte sc1 stores; < 2 GB)
   // wgrad_halo LDS layout (models/lds_layout.py picks it with a bank-conflict model; 0 =
   // dense): X-halo pixel stride in elements, X-halo row stride in pixels, dY row stride
   int xpix = 0, xrow = 0, dyld = 0;

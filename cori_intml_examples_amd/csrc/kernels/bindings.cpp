@@ -78,7 +78,7 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(BwdThrough, prev_out) PTR(BwdThrough, prev_code) RW(BwdThrough, prev_relu)
       RW(BwdThrough, prev_pool) RW(BwdThrough, pH) RW(BwdThrough, pW) RW(BwdThrough, pC)
       RW(BwdThrough, pCs) RW(BwdThrough, cH) RW(BwdThrough, cW) RW(BwdThrough, drop_thr)
-      RW(BwdThrough, drop_scale) RW(BwdThrough, seed) RW(BwdThrough, stream_id) PTR(BwdThrough, dy);
+      RW(BwdThrough, drop_scale) RW(BwdThrough, seed) RW(BwdThrough, stream_id) PTR(BwdThrough, dy) RW(BwdThrough, wt);
 
   py::class_<ConvMMArgs>(m, "ConvMMArgs")
       .def(py::init<>())
@@ -103,7 +103,7 @@ PYBIND11_MODULE(_kernels, m) {
       RW(WgradArgs, dbg) PTR(WgradArgs, ts) PTR(WgradArgs, ts2) RW(WgradArgs, opt) RW(WgradArgs, opt_w)
       RW(WgradArgs, opt_b) RW(WgradArgs, xpix) RW(WgradArgs, xrow) RW(WgradArgs, dyld) RW(WgradArgs, kperm)
       PTR(WgradArgs, xidx) PTR(WgradArgs, xst) RW(WgradArgs, pk_fwd) RW(WgradArgs, pk_bwd) RW(WgradArgs, pk_NT)
-      RW(WgradArgs, pk_NTb);
+      RW(WgradArgs, pk_NTb) RW(WgradArgs, wt);
 
   py::class_<DenseFwdArgs>(m, "DenseFwdArgs")
       .def(py::init<>())
@@ -154,7 +154,7 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(ConvStackArgs, st) RW(ConvStackArgs, dbg) RW(ConvStackArgs, off_w) RW(ConvStackArgs, off_codes) RW(ConvStackArgs, off_codes2) RW(ConvStackArgs, lds_bytes)
       .def("set_buf_offsets", [](ConvStackArgs& a, int b0, int b1) { a.off_buf[0] = b0; a.off_buf[1] = b1; })
       RW(ConvStackArgs, splits) PTR(ConvStackArgs, ts) RW(ConvStackArgs, off_bias)
-      RW(ConvStackArgs, from_data) RW(ConvStackArgs, training) RW(ConvStackArgs, step_inc) PTR(ConvStackArgs, srcidx) RW(ConvStackArgs, k16)
+      RW(ConvStackArgs, from_data) RW(ConvStackArgs, training) RW(ConvStackArgs, step_inc) PTR(ConvStackArgs, srcidx) RW(ConvStackArgs, k16) RW(ConvStackArgs, wt)
       .def("set_rows", [](ConvStackArgs& a, int l, int sp, int c0, int c1, int o0, int o1, int ib, int ih) {
         if (l < 0 || l >= MAX_STACK || sp < 0 || sp >= MAX_STACK_SPLIT) throw std::out_of_range("conv stack rows");
         const int v[6] = {c0, c1, o0, o1, ib, ih};

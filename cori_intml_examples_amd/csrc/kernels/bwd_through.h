@@ -50,7 +50,8 @@ __device__ __forceinline__ void bwd_through_store8(const BwdThrough& t, size_t q
     }
     outv[k] = f2bf(v);
   }
-  *reinterpret_cast<bf16x8*>(t.dy + o) = outv;
+  if (t.wt) st_wt16(t.dy, (unsigned)(o * 2), __builtin_bit_cast(u32x4, outv));
+  else *reinterpret_cast<bf16x8*>(t.dy + o) = outv;
 }
 
 // Full-resolution gradient of a max-pooled conv at pixel (y, x), channels [c, c+8), rebuilt

@@ -19,6 +19,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
@@ -31,6 +32,16 @@ __device__ __forceinline__ f32x4 mfma16k16(const bf16x4& a, const bf16x4& b, con
   typedef short s16x4 __attribute__((ext_vector_type(4)));
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c,
                                                    0, 0, 0);
+}
+
+// 16-byte write-through store (vector buffer store, sc1): the line leaves the XCD's L2 with
+// the store, so the launch's end-of-kernel release finds none of these bytes dirty (a
+// boundary costs ~bytes / 6 TB/s behind a kernel that leaves its output dirty in L2).
+// `base` must be wave-uniform; `off` is a byte offset < 2^31.
+__device__ __forceinline__ void st_wt16(const void* base, unsigned off, u32x4 v) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
 }
 
 __device__ __forceinline__ bf16x8 zero_bf16x8() {

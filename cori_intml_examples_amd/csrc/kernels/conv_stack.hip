@@ -696,18 +696,27 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       const int n = (own1 - own0) * L.Wp * cch;
       const FastDiv fc(cch), fw(L.Wp);
       bf16* gout = L.out + ((size_t)b * L.Hp + own0) * L.Wp * L.Cs_out;
+      // write-through (A.wt): the next launch reads these rows from other XCDs anyway
+      const bool wt = A.wt && (L.Cs_out & 15) == 0;
       for (int i = tid; i < n; i += STACK_THREADS) {
         const int pix = fc.div(i), c = (i - pix * cch) * 8;
         const int pyo = fw.div(pix), px = pix - pyo * L.Wp;
-        *reinterpret_cast<bf16x8*>(gout + pix * L.Cs_out + c) =
-            *reinterpret_cast<const LDS bf16x8*>(out + ((own0 + pyo - obase) * ORS + px + ol) * OPS + c);
+        const u32x4 v = *reinterpret_cast<const LDS u32x4*>(out + ((own0 + pyo - obase) * ORS + px + ol) * OPS + c);
+        if (wt) st_wt16(gout, (unsigned)(pix * L.Cs_out + c) * 2u, v);
+        else *reinterpret_cast<u32x4*>(gout + pix * L.Cs_out + c) = v;
       }
       if (L.pool && L.code) {
-        const int nb = ((own1 - own0) * L.Wp * L.Cs_out) >> 3;
-        unsigned long long* gc =
-            reinterpret_cast<unsigned long long*>(L.code + ((size_t)b * L.Hp + own0) * L.Wp * L.Cs_out);
-        const LDS unsigned long long* lc = (const LDS unsigned long long*)(codes + (own0 - p0) * L.Wp * L.Cs_out);
-        for (int i = tid; i < nb; i += STACK_THREADS) gc[i] = lc[i];
+        const int nbytes = (own1 - own0) * L.Wp * L.Cs_out;
+        uint8_t* gcb = L.code + ((size_t)b * L.Hp + own0) * L.Wp * L.Cs_out;
+        const LDS uint8_t* lcb = codes + (own0 - p0) * L.Wp * L.Cs_out;
+        if (wt) {   // 16-byte code vectors (Cs_out % 16 == 0: whole vectors, 16-byte aligned)
+          for (int i = tid; i < (nbytes >> 4); i += STACK_THREADS)
+            st_wt16(gcb, (unsigned)i * 16u, *reinterpret_cast<const LDS u32x4*>(lcb + i * 16));
+        } else {
+          unsigned long long* gc = reinterpret_cast<unsigned long long*>(gcb);
+          const LDS unsigned long long* lc = (const LDS unsigned long long*)lcb;
+          for (int i = tid; i < (nbytes >> 3); i += STACK_THREADS) gc[i] = lc[i];
+        }
       }
     }
     STACK_STAMP(5 + 4 * l);

@@ -50,8 +50,9 @@ size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT) {
   const int ldb = a.dyld ? a.dyld : NTT * 16 + 8;
   const size_t x_elems = (size_t)(((R_in * XR * XP) + 7) & ~7);
   const size_t npb32 = (size_t)((a.R * a.Wo + 31) & ~31);
-  // (>= 4 KB: a tail reduction block's LDS tree / tiled pack staging reuses the buffer)
-  return std::max<size_t>(x_elems * 2 + npb32 * ldb * 2 + 64 + (size_t)(MT * 4 + 4) * 4, 4096);
+  // (>= 5 KB: a tail reduction block's LDS tree / tiled pack staging and the write-through
+  // slab squares, 4 x 16 x WH_SQ floats, reuse the buffer)
+  return std::max<size_t>(x_elems * 2 + npb32 * ldb * 2 + 64 + (size_t)(MT * 4 + 4) * 4, 4 * 16 * WH_SQ * 4);
 }
 
 template <int MTW, int NTT, bool CS4>

@@ -25,6 +25,10 @@ __device__ __forceinline__ const bf16* wg_xbase(const WgradArgs& a, int b) {
   return a.x + (size_t)b * a.H * a.W * a.Cs_in;
 }
 
+// row stride (floats) of a wave's 16x16 write-through staging square: rows 4 apart land
+// 16 banks apart (conflict-free lane writes), rows stay 16-byte aligned for the vector read
+#define WH_SQ 20
+
 template <int MTW, int NTT, bool CS4, bool PIPE>
 __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT, const int bx, const int by,
                                                 const int bz, char* smem) {
@@ -444,6 +448,11 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
         asm volatile("" ::"v"(acc[u][v][0]), "v"(acc[u][v][1]), "v"(acc[u][v][2]), "v"(acc[u][v][3]));
     return;
   }
+  // write-through slabs (a.wt): each 16x16 tile goes through a wave-private LDS square and
+  // leaves as one 16-byte sc1 store per lane (4 rows x 64 B), so the launch ends with none
+  // of its partial bytes dirty in L2; plain form: 4 scalar stores per lane
+  float* sq = reinterpret_cast<float*>(smem) + wave * (16 * WH_SQ);
+  if (a.wt) __syncthreads();   // the staging images' last readers are done: LDS is scratch
 #pragma unroll
   for (int u = 0; u < MTW; ++u) {
     const int mt = wave + 4 * u;
@@ -456,6 +465,17 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
         continue;
       }
       if (mt0 + mt >= a.Ktiles) continue;
+      if (a.wt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sq[(g * 4 + j) * WH_SQ + i] = acc[u][v][j];
+        __builtin_amdgcn_wave_barrier();
+        const int row = lane >> 2, c4 = (lane & 3) * 4;
+        const u32x4 val = *reinterpret_cast<const u32x4*>(sq + row * WH_SQ + c4);
+        const size_t off = (size_t)bx * a.Ktiles * 16 * ld + (size_t)((mt0 + mt) * 16 + row) * ld + (nt0 + v) * 16 + c4;
+        st_wt16(a.slab, (unsigned)(off * 4), val);
+        __builtin_amdgcn_wave_barrier();
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         slab[(size_t)((mt0 + mt) * 16 + g * 4 + j) * ld + (nt0 + v) * 16 + i] = acc[u][v][j];

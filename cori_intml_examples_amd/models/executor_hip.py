@@ -637,6 +637,9 @@ class BatchPlan(GeometryMixin):
             bt.drop_thr = keep_threshold(rate)
             bt.drop_scale = 1.0 / (1.0 - rate)
         bt.seed, bt.stream_id = ex.seed, stream
+        # write-through gradient stores (16-byte sc1; byte offsets < 2 GB)
+        dyb = self.conv_dy[g.i] if src.kind == "conv" else self.dense_dh[g.j]
+        bt.wt = int(bool(int(tune("wt", 0)) & 2) and dyb.numel() * 2 < (1 << 31))
         return bt
 
     def _build_args(self):

@@ -62,6 +62,7 @@ class GeometryMixin:
         a.off_bias = off_bias
         a.dbg = tune("stack_dbg", 0)
         a.k16 = int(tune("stack_k16", False))
+        a.wt = int(bool(int(tune("wt", 0)) & 1))      # write-through stage outputs / codes
         a.set_buf_offsets(off_b0, off_b1)
         a.splits = splits
         for l in range(n):
@@ -392,6 +393,8 @@ class GeometryMixin:
         bslab = torch.zeros(S, NT * 16, dtype=torch.float32, device=dev) if bias else None
         a.slab = slab.data_ptr()
         a.bslab = bslab.data_ptr() if bslab is not None else 0
+        # write-through slabs (16-byte sc1 stores, byte offsets < 2 GB)
+        a.wt = int(bool(int(tune("wt", 0)) & 4) and slab.numel() * 4 < (1 << 31))
         self.wgrad_slabs.append((slab, bslab))
         return a, (MT, NTT, S), slab, bslab
 

@@ -9,5 +9,5 @@ mkdir -p gpurun_out
 T="timeout -k 10"
 $T 900 python -u -m pytest -v --timeout 450 --timeout-method thread tests/test_comm.py -m gpu > gpurun_out/r4_comm.log 2>&1
 echo "comm rc=$?"; grep -E "PASSED|FAILED|ERROR" gpurun_out/r4_comm.log | head -20
-$T 700 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_hip_model.py tests/test_dense_bwd.py -m gpu -k "head_fast or tail_reduction or stack_k16 or fast_prologue or bf16_reference or grads_match_reference or dense_fused" -s > gpurun_out/r4_numerics.log 2>&1
+$T 700 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_hip_model.py tests/test_dense_bwd.py -m gpu -k "head_fast or tail_reduction or stack_k16 or fast_prologue or bf16_reference or grads_match_reference or dense_fused or write_through" -s > gpurun_out/r4_numerics.log 2>&1
 echo "numerics rc=$?"; grep -E "PASSED|FAILED|ERROR|worst grad" gpurun_out/r4_numerics.log | head -40

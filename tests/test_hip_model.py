@@ -548,3 +548,25 @@ def test_stack_fast_prologue_bit_identical(kind, drop, cin, hw, monkeypatch):
         torch.cuda.synchronize()
         res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
     assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
+
+
+@pytest.mark.parametrize("kind,drop,cin,hw", [("rpv", 0.2, 3, 64), ("mnist", 0.3, 1, 28)])
+def test_write_through_stores_bit_identical(kind, drop, cin, hw, monkeypatch):
+    """Write-through (16-byte sc1) stores of the stage outputs / argmax codes (wt & 1), the
+    backward gradients dP / dH (wt & 2) and the weight-gradient slabs (wt & 4, through a
+    wave-private LDS square) store exactly the plain stores' bytes: whole training steps
+    bit-identical."""
+    res = []
+    for tv in ("wt=7", "wt=0"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(50)
+        m = _build(kind, "cuda", opt="Adam", drop=drop, cin=cin, hw=hw)
+        x, y = _data(m, 256, seed=14)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(10)).to(ex.device)
+        ex.reset_metrics()
+        ex.train_steps(d, perm, 0, 128, 2)
+        torch.cuda.synchronize()
+        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
+    assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
