@@ -175,7 +175,7 @@ def probe_data_planes(args, size, dev, g, B, chunk):
             on = plane not in ("xgmi", "hybrid") or x is not None
             # a plane is only eligible if it trained correctly here: no timed-out wait and
             # bit-identical weights on every rank after the probe steps
-            sane = [weight_checksum(model), bool(x is None or int(x.err.item()) == 0)]
+            sane = [weight_checksum(model), bool(x is None or int(x.err[0].item()) == 0)]
             sane = hvd.allgather(sane) if size > 1 else [sane]
             ok = all(c == sane[0][0] and f for c, f in sane)
             res[plane] = (round((max(hvd.allgather(e)) if size > 1 else e) / probe * 1e3, 4)

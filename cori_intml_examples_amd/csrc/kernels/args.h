@@ -376,7 +376,8 @@ struct XgmiArgs {
   unsigned* flag2[XGMI_MAX_RANKS] = {};  // rank j's phase-2 flags [XGMI_MAX_WG][P]
   unsigned* abort_[XGMI_MAX_RANKS] = {}; // rank j's sticky abort word (set by any rank that gives up)
   unsigned* ctr = nullptr;       // [XGMI_MAX_WG] local sequence counters
-  int* err = nullptr;            // phase (1, 2) of a timed-out wait; 3 = a peer aborted
+  int* err = nullptr;            // [4]: phase (1, 2) of a timed-out wait, 3 = a peer aborted;
+                                 // on a timeout also seq waited for, flag value seen, wg * 64 + peer
   OptimArgs opt;                 // p / s0 / s1 point at the bucket's first element
 };
 

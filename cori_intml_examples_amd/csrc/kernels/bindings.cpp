@@ -17,7 +17,7 @@ long long conv_tile_big_blocks(const ConvMMArgs& a, int ntc);
 size_t conv_tile_lds_bytes(int ntc);
 void launch_wgrad_tile(const WgradArgs& a, int ntc, hipStream_t s);
 size_t wgrad_tile_lds_bytes(int ntc);
-void launch_wgrad_halo(const WgradArgs& a, int MT, int NTT, int splits, const DualExtra& x, hipStream_t s);
+void launch_wgrad_halo(const WgradArgs& a, int MT, int NTT, int splits, hipStream_t s);
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT);
 int wgrad_halo_resident(const WgradArgs& a, int MT, int NTT, bool bias);
 int head_rows_per_block(bool fused);
@@ -295,22 +295,8 @@ PYBIND11_MODULE(_kernels, m) {
     launch_wgrad_tile(a, ntc, S(s)); check_last("wgrad_tile"); });
   m.def("conv_halo", [](const ConvMMArgs& a, int ntc, uintptr_t s) {
     launch_conv_halo(a, ntc, S(s)); check_last("conv_halo"); });
-  m.def(
-      "wgrad_halo",
-      [](const WgradArgs& a, int MT, int NTT, int splits, uintptr_t s, const RedTable* rt, const OptimArgs* ro,
-         uintptr_t rgrad) {
-        DualExtra x;
-        if (rt && ro && rt->nblocks > 0) {
-          x.rt = *rt, x.ro = *ro, x.grad = reinterpret_cast<float*>(rgrad);
-          x.n_r = rt->nblocks;
-        }
-        launch_wgrad_halo(a, MT, NTT, splits, x, S(s));
-        check_last("wgrad_halo");
-      },
-      py::arg("a"), py::arg("MT"), py::arg("NTT"), py::arg("splits"), py::arg("s"), py::arg("rt") = nullptr,
-      py::arg("ro") = nullptr, py::arg("rgrad") = 0,
-      "halo-staged conv weight gradient; with (rt, ro, rgrad) its workgroups then run that table's reduction + "
-      "optimizer (tail reduction)");
+  m.def("wgrad_halo", [](const WgradArgs& a, int MT, int NTT, int splits, uintptr_t s) {
+    launch_wgrad_halo(a, MT, NTT, splits, S(s)); check_last("wgrad_halo"); });
   m.def("wgrad", [](const WgradArgs& a, int ktw, int ntt, int splits, uintptr_t s) {
     launch_wgrad(a, ktw, ntt, splits, S(s)); check_last("wgrad"); });
   m.def("dense_fwd", [](const DenseFwdArgs& a, uintptr_t s) { launch_dense_fwd(a, S(s)); check_last("dense_fwd"); });

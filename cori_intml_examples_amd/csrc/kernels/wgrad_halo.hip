@@ -11,32 +11,18 @@
 // of "its" pixel row, with the tap shift folded into the per-lane address (im2col without
 // materialising it).  The bias gradient is one extra MFMA tile with an all-ones A operand.
 // Partials: one fp32 slab per split, summed in fixed order by slab_reduce (deterministic).
-//
-// Tail reduction (x.n_r > 0): the step's LAST weight-gradient launch also reduces the slabs
-// of earlier layers (final since earlier launches) and applies their optimizer update --
-// each workgroup, once its own slab is stored, runs reduction-table blocks lin, lin + grid,
-// ...  The work sits in the launch's own workgroups, after their MFMA work: the early
-// finishers absorb it while the stragglers still run, instead of a separate reduction launch
-// (or extra workgroups competing for the CU slots the wgrad grid already fills).
+
 #include <algorithm>
 #include <cstdlib>
 
-#include "reduce_body.h"
 #include "wgrad_halo_body.h"
 
 template <int MTW, int NTT, bool CS4, bool PIPE>
-__global__ __launch_bounds__(256) void wgrad_halo_kernel(const WgradArgs a, const int MT, const DualExtra x) {
+__global__ __launch_bounds__(256) void wgrad_halo_kernel(const WgradArgs a, const int MT) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const size_t lin = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
   if (a.ts && threadIdx.x == 0) a.ts[2 * lin] = wall_clock64();
   wgrad_halo_body<MTW, NTT, CS4, PIPE>(a, MT, blockIdx.x, blockIdx.y, blockIdx.z, smem);
-  if (x.n_r) {
-    const int nwg = (int)(gridDim.x * gridDim.y * gridDim.z);
-    for (int r = (int)lin; r < x.n_r; r += nwg) {
-      __syncthreads();     // the staging buffers' (or the previous block's) last LDS readers are done
-      reduce_optim_block_rt(x.grad, x.rt, x.ro, r, reinterpret_cast<float*>(smem));
-    }
-  }
   if (a.ts) {
     __syncthreads();
     if (threadIdx.x == 0) a.ts[2 * lin + 1] = wall_clock64();
@@ -50,32 +36,31 @@ size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT) {
   const int ldb = a.dyld ? a.dyld : NTT * 16 + 8;
   const size_t x_elems = (size_t)(((R_in * XR * XP) + 7) & ~7);
   const size_t npb32 = (size_t)((a.R * a.Wo + 31) & ~31);
-  // (>= 5 KB: a tail reduction block's LDS tree / tiled pack staging and the write-through
-  // slab squares, 4 x 16 x WH_SQ floats, reuse the buffer)
+  // (>= the write-through slab squares, 4 x 16 x WH_SQ floats, which reuse the buffer)
   return std::max<size_t>(x_elems * 2 + npb32 * ldb * 2 + 64 + (size_t)(MT * 4 + 4) * 4, 4 * 16 * WH_SQ * 4);
 }
 
 template <int MTW, int NTT, bool CS4>
-static void wh_t(const WgradArgs& a, int MT, dim3 grid, size_t lds, const DualExtra& x, hipStream_t s) {
+static void wh_t(const WgradArgs& a, int MT, dim3 grid, size_t lds, hipStream_t s) {
   // few workgroups streaming several blocks each: pipeline their staging; a large grid
   // already hides it with resident workgroups (and keeps the lower VGPR count)
   const bool pipe = grid.x * grid.y * grid.z < 512 && a.blocks_per_split > 1;
   auto k = pipe ? wgrad_halo_kernel<MTW, NTT, CS4, true> : wgrad_halo_kernel<MTW, NTT, CS4, false>;
   if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a, MT, x);
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a, MT);
 }
 
 // MT m-tiles x NTT n-tiles per workgroup; each wave owns ceil((MT+bias)/4) m-tiles
 // (MTW <= 4, MTW*NTT <= 16); grid = (splits, n-groups, m-groups)
-void launch_wgrad_halo(const WgradArgs& a, int MT, int NTT, int splits, const DualExtra& x, hipStream_t s) {
+void launch_wgrad_halo(const WgradArgs& a, int MT, int NTT, int splits, hipStream_t s) {
   const bool cs4 = a.Cs_in == 4;
   dim3 grid(splits, (a.NT + NTT - 1) / NTT, (a.Ktiles + MT - 1) / MT);
   const size_t lds = wgrad_halo_lds_bytes(a, MT, NTT);
   const int mtw = (MT + (a.bslab ? 1 : 0) + 3) / 4;
 #define C(M_, N_)                                            \
   if (mtw <= M_ && NTT == N_) {                              \
-    if (cs4) wh_t<M_, N_, true>(a, MT, grid, lds, x, s);     \
-    else wh_t<M_, N_, false>(a, MT, grid, lds, x, s);        \
+    if (cs4) wh_t<M_, N_, true>(a, MT, grid, lds, s);     \
+    else wh_t<M_, N_, false>(a, MT, grid, lds, s);        \
     return;                                                  \
   }
   C(1, 1) C(2, 1) C(4, 1) C(1, 2) C(2, 2) C(4, 2) C(1, 4) C(2, 4) C(4, 4) C(1, 8) C(2, 8)

@@ -28,10 +28,11 @@ __device__ __forceinline__ void sys_store(unsigned* p, unsigned v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // first cause wins: a timeout recorded by one workgroup is not overwritten by the abort the
-// rank's other workgroups then observe
-__device__ __forceinline__ void set_err(int* err, int v) {
+// rank's other workgroups then observe; returns true for the lane that recorded it
+__device__ __forceinline__ bool set_err(int* err, int v) {
   int zero = 0;
-  __hip_atomic_compare_exchange_strong(err, &zero, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_compare_exchange_strong(err, &zero, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Lanes 0..P-1 of wave 0 each raise flag `slot` of rank `lane` to seq.
@@ -70,7 +71,11 @@ __device__ __forceinline__ bool wait_all(const XgmiArgs& a, const unsigned* flag
       }
       if ((long long)(wall_clock64() - t0) > a.timeout_ticks) {
         s_ok = 0;
-        set_err(a.err, phase);
+        if (set_err(a.err, phase)) {   // diagnostics of the first timeout: what was awaited / seen
+          a.err[1] = (int)seq;
+          a.err[2] = (int)sys_load(flags + t);
+          a.err[3] = (int)blockIdx.x * 64 + t;
+        }
         for (int j = 0; j < P; ++j) sys_store(a.abort_[j], 1u);
         break;
       }

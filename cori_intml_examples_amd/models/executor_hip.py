@@ -639,7 +639,7 @@ class BatchPlan(GeometryMixin):
         bt.seed, bt.stream_id = ex.seed, stream
         # write-through gradient stores (16-byte sc1; byte offsets < 2 GB)
         dyb = self.conv_dy[g.i] if src.kind == "conv" else self.dense_dh[g.j]
-        bt.wt = int(bool(int(tune("wt", 0)) & 2) and dyb.numel() * 2 < (1 << 31))
+        bt.wt = int(bool(int(tune("wt", 7)) & 2) and dyb.numel() * 2 < (1 << 31))
         return bt
 
     def _build_args(self):
@@ -809,17 +809,16 @@ class BatchPlan(GeometryMixin):
         self.red_groups.append((lo, hi, descs))
         self._add_group_reduce()
         self.wgrad_slabs = []
-        self.tail_capable = set()          # halo wgrad launches that can carry a tail reduction
         self.dense_fused_opt = []          # (WgradArgs, params) updated inside dense_wgrad
         # opt-in: the dense layer's optimizer update inside its (one-split) wgrad kernel.  Measured
         # slower on RPV at batch 128: the 128 wgrad workgroups move the layer's 14 MB of optimizer
         # state at per-CU bandwidth (wgrad 6.1 -> 9.7 us) while the end-of-step reduction, which
         # spreads it over thousands of workgroups, only drops 10.8 -> 8.2 us
         # dense_opt: "auto" = only layers whose gradient is written in place (> 16 MB, the legacy
-        # model's 33.5M-weight Dense(512)): their update moves ~1 GB either way, and fusing it
-        # saves the gradient's own write + re-read; "1" = every one-split layer (measured slower
-        # on the 0.5M-weight RPV dense at batch 128: 128 workgroups carry 14 MB of state)
-        dense_opt = str(tune("dense_opt", "auto")).lower()
+        # model's 33.5M-weight Dense(512)) -- measured slower there too (1.27 -> 1.35 ms/step:
+        # the wgrad's few workgroups move ~1 GB of optimizer state, and the layer's dX becomes a
+        # launch of its own); "1" = every one-split layer; default "0"
+        dense_opt = str(tune("dense_opt", "0")).lower()
         self.dense_opt_ok = (ex.reducer is None and tune("fuse_optim", True)
                              and dense_opt not in ("0", "false", "off", "no"))
         self.dense_opt_all = dense_opt in ("1", "true", "on", "yes")
@@ -895,7 +894,16 @@ class BatchPlan(GeometryMixin):
                 dname = "dense_dx%d" % g.j
                 ntc = self._dense_dx_ntc(a) if (bwd2 and a.bt.pCs % 8 == 0 and a.Ks % 8 == 0
                                                and not K.dense_big(a.NT, a.KS)) else 0
-                if tune("dual_dense", True):
+                if fused_opt:
+                    # the wgrad's fused optimizer rewrites this layer's backward pack: its dX (that
+                    # pack's reader) runs first, as a launch of its own on the same stream -- never
+                    # in one launch with it (dense_bwd_pair: dX workgroups would read a pack the
+                    # wgrad workgroups are rewriting)
+                    fn = ((lambda s, a=a, n=ntc: K.dense_dx(a, n, s)) if ntc else (lambda s, a=a: K.dense_fwd(a, s)))
+                    self.launches[w_at] = (self.launches[w_at][0], self.launches[w_at][1], "main")
+                    self.launches.insert(w_at, (dname, fn, "main"))
+                    self.red_ready[-1] += 1
+                elif tune("dual_dense", True):
                     # one launch for the dense wgrad and dX (independent GEMMs over dH), in the
                     # wgrad's slot (its slabs are final after it)
                     dname = "dense_bwd%d" % g.j
@@ -922,9 +930,8 @@ class BatchPlan(GeometryMixin):
                 wa, cfg, slab, bslab = self._wgrad_halo_args(xin, g, bs, cs.conv.use_bias)
                 if g.i == 0 and self.pro_free:      # the images the stack read from the dataset
                     wa.xidx, wa.xst = self.srcidx.data_ptr(), st_ptr
-                wname = "wgrad_conv%d" % g.i
-                self.tail_capable.add(wname)
-                self.launches.append((wname, lambda s, a=wa, c=cfg, nm=wname: self._wgrad_h(a, c, s, nm), "side"))
+                self.launches.append(("wgrad_conv%d" % g.i,
+                                      lambda s, a=wa, c=cfg: K.wgrad_halo(a, c[0], c[1], c[2], s), "side"))
             w_at = len(self.launches) - 1
             sp = store.spec(cs.conv, "kernel")
             S, ld = cfg[2], g.NT * 16
@@ -986,10 +993,10 @@ class BatchPlan(GeometryMixin):
         if reducer is not None:
             bucket_groups = reducer.configure(groups)
             # one bucket at the end of the backward (the adaptive plan for gradients <= 16 MB):
-            # the groups final before a carrier launch (the first dual launch, the last wgrad
-            # launch -- the single-GPU step's carriers) are REDUCED early there (grad_only: no
-            # update), so the end-of-backward reduction ahead of the all-reduce only has the
-            # first layer's slabs left (the update stays behind the all-reduce)
+            # the groups final before the first dual launch (head, dense -- the single-GPU
+            # step's early bucket) are REDUCED early there (grad_only: no update), so the
+            # end-of-backward reduction ahead of the all-reduce only has the conv layers' slabs
+            # left (the update stays behind the all-reduce)
             if len(bucket_groups) == 1 and self.comm_in_graph and tune("dp_early", True):
                 dp_early = self._early_groups(grad_only=True)
         else:
@@ -1072,9 +1079,9 @@ class BatchPlan(GeometryMixin):
         """Single-GPU fused-optimizer step: slab groups whose gradients are final before a dual
         conv backward launch (the head and dense layers before the first one) are reduced and
         updated by extra workgroups OF that launch (DualExtra) instead of in the end-of-step
-        reduction -- their latency-bound reduce + update overlaps the conv backward; the groups
-        final before the last (first-layer) wgrad launch run in ITS workgroups' tails.  Only groups no later launch reads the weights of
-        (pack readers), each launch's as one contiguous parameter span.  Sets
+        reduction -- their latency-bound reduce + update overlaps the conv backward.  Only
+        groups no later launch reads the weights of (pack readers), as one contiguous
+        parameter span.  Sets
         self.early_red = {launch name: (RedTable, (lo, hi), grad_only)}; returns the groups
         assigned.  grad_only (data-parallel step): reduction only -- no update, no pack
         writes, so later pack readers do not matter."""
@@ -1089,13 +1096,9 @@ class BatchPlan(GeometryMixin):
         # layers' reductions as extra workgroups measured 2-3 us slower on RPV and MNIST:
         # profiles/r3_s2_early_wgrad_ab.txt)
         duals = [i for i, nm in enumerate(names) if nm.startswith("wgrad_dgrad_conv")][:1]
-        # Tail reduction: the step's LAST launch, when it is a halo wgrad (the first conv
-        # layer's), reduces + updates the earlier conv layers' slabs in its OWN workgroups after
-        # their wgrad work (wgrad_halo.hip) -- not as extra workgroups (measured slower, above):
-        # the early finishers absorb it while the stragglers run, and the separate end-of-step
-        # reduction is left with the first layer's slabs only
-        if tune("tail_reduce", True) and names and names[-1] in getattr(self, "tail_capable", ()):
-            duals.append(len(names) - 1)
+        # (the step's last launch -- the first conv layer's halo wgrad -- reducing + updating the
+        # earlier conv layers' slabs in its own workgroups' tails measured slower too: RPV
+        # 1.121M -> 1.071M img/s, legacy 103.4k -> 94.7k; profiles/r4_ab_rpv.txt)
         taken = []
         for t in duals:
             late_readers = [] if grad_only else [(rlo, rhi) for nm, rlo, rhi in self.pack_readers

@@ -61,8 +61,8 @@ class GeometryMixin:
         a.off_w, (a.off_codes, a.off_codes2), a.lds_bytes = off_w, off_codes, lds
         a.off_bias = off_bias
         a.dbg = tune("stack_dbg", 0)
-        a.k16 = int(tune("stack_k16", False))
-        a.wt = int(bool(int(tune("wt", 0)) & 1))      # write-through stage outputs / codes
+        a.k16 = int(tune("stack_k16", True))
+        a.wt = int(bool(int(tune("wt", 7)) & 1))      # write-through stage outputs / codes
         a.set_buf_offsets(off_b0, off_b1)
         a.splits = splits
         for l in range(n):
@@ -227,17 +227,6 @@ class GeometryMixin:
             if early is not None:
                 K.reduce_optim(ex.store.grad.data_ptr(), early[0], self._early_ro(early), s)
 
-    def _wgrad_h(self, wa, cfg, s, name=None):
-        """A halo wgrad launch; when _early_groups gave it a table, its workgroups then run that
-        table's reduction + optimizer (tail reduction, wgrad_halo.hip)."""
-        K, ex = self.ex.K, self.ex
-        early = (self.early_red or {}).get(name)
-        if early is None:
-            K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
-        else:
-            K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s, rt=early[0], ro=self._early_ro(early),
-                         rgrad=ex.store.grad.data_ptr())
-
     def _early_ro(self, early):
         """OptimArgs of an early reduction table: the Keras update, or (data-parallel step,
         early[2]) the reduction only -- the update follows the all-reduce."""
@@ -394,7 +383,7 @@ class GeometryMixin:
         a.slab = slab.data_ptr()
         a.bslab = bslab.data_ptr() if bslab is not None else 0
         # write-through slabs (16-byte sc1 stores, byte offsets < 2 GB)
-        a.wt = int(bool(int(tune("wt", 0)) & 4) and slab.numel() * 4 < (1 << 31))
+        a.wt = int(bool(int(tune("wt", 7)) & 4) and slab.numel() * 4 < (1 << 31))
         self.wgrad_slabs.append((slab, bslab))
         return a, (MT, NTT, S), slab, bslab
 

@@ -445,7 +445,7 @@ class NativeGradReducer:
             from . import xgmi as X
             self.xgmi = X.create(self.rank, self.size, n, self.device, allgather)
             if self.xgmi is not None:
-                self._xgmi_err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+                self._xgmi_err_host = torch.zeros(4, dtype=torch.int32).pin_memory()
         if self.xgmi is not None:
             self.xgmi_bucket = k
         elif self.comm is None:
@@ -495,7 +495,7 @@ class NativeGradReducer:
         if self.xgmi is not None:
             if int(self._xgmi_err_host[0]):
                 from . import xgmi as X
-                raise RuntimeError(X.describe_error(int(self._xgmi_err_host[0])))
+                raise RuntimeError(X.describe_error(*self._xgmi_err_host.tolist()))
             self._xgmi_err_host.copy_(self.xgmi.err, non_blocking=True)
 
     def reduce_all(self, grad: torch.Tensor, average: bool = True) -> None:

@@ -111,7 +111,7 @@ class XgmiAllreduce:
             except Exception as e:    # noqa: BLE001
                 err = "ipc: %s" % e
         self.ctr = torch.zeros(K.XGMI_MAX_WG, dtype=torch.int32, device=device)
-        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.err = torch.zeros(4, dtype=torch.int32, device=device)   # code, seq, seen, wg*64+peer
         a = K.XgmiArgs()
         a.rank, a.size, a.n, a.chunk, a.sub = rank, size, n, self.chunk, self.sub
         self.timeout_s = float(timeout_s or default_timeout_s())
@@ -138,9 +138,9 @@ class XgmiAllreduce:
 
     def check(self) -> None:
         """Raise if a wait in an earlier launch timed out (a peer died or hung)."""
-        e = int(self.err.item())
-        if e:
-            raise RuntimeError(describe_error(e))
+        e = self.err.tolist()
+        if e[0]:
+            raise RuntimeError(describe_error(*e))
 
     def selftest(self) -> Optional[str]:
         """Two launches on closed-form data (exact in fp32); None if correct on this rank."""
@@ -154,8 +154,8 @@ class XgmiAllreduce:
             g = pat * float(r + 1 + it)
             self.launch(g.data_ptr(), stream)
             torch.cuda.synchronize(self.device)
-            if int(self.err.item()):
-                return "selftest: wait timed out (phase %d)" % int(self.err.item())
+            if int(self.err[0].item()):
+                return "selftest: " + describe_error(*self.err.tolist())
             want = pat * float(sum(q + 1 + it for q in range(P)))
             if not torch.equal(g, want):
                 bad = int((g != want).sum())
@@ -175,10 +175,11 @@ class XgmiAllreduce:
             self.buf = 0
 
 
-def describe_error(e: int) -> str:
+def describe_error(e: int, seq: int = 0, seen: int = 0, where: int = 0) -> str:
     if e == 3:
         return "xgmi all-reduce: aborted (a peer rank timed out waiting; peer dead or hung)"
-    return "xgmi all-reduce: phase-%d wait timed out (peer rank dead or hung)" % e
+    return ("xgmi all-reduce: phase-%d wait timed out (peer rank dead or hung): workgroup %d waited for "
+            "rank %d's flag to reach %d, saw %d" % (e, where // 64, where % 64, seq, seen))
 
 
 def create(rank: int, size: int, n: int, device: torch.device, allgather,

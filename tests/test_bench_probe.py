@@ -29,7 +29,7 @@ def probe_env(monkeypatch):
         return "rccl_forked" if os.environ.get("INTML_BUCKET_BYTES") else "rccl"
 
     def build(args, size, dp, dev):
-        x = (types.SimpleNamespace(err=types.SimpleNamespace(item=lambda: 0)) if plane() in ("xgmi", "hybrid")
+        x = (types.SimpleNamespace(err=[types.SimpleNamespace(item=lambda: 0)]) if plane() in ("xgmi", "hybrid")
              else None)
         m = types.SimpleNamespace(_executor=types.SimpleNamespace(reducer=types.SimpleNamespace(xgmi=x)),
                                   plane=plane())

@@ -217,10 +217,10 @@ def test_xgmi_only_reducer_is_one_fused_bucket():
 def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
     """the 8-GPU data-parallel step end to end on one GPU.  P ranks (torchrun,
     all on GPU 0, so the RCCL-free plane is chosen on its own) train 24 captured steps (3
-    replays x 8) at per-rank batch 128/P through the fused xGMI all-reduce + Adam kernel:
-    no wait times out, every rank ends with bit-identical weights, and those match a
-    single-process run at global batch 128 from the same weights and permutation within the
-    bounds of the size-1 DP test (Adam amplifies last-ulp differences of near-zero grads)."""
+    replays x 8) at per-rank batch 128/P through the fused xGMI all-reduce + optimizer
+    kernel, with Adam and with SGD: no wait times out, every rank ends with bit-identical
+    weights, and those match a single-process run at global batch 128 from the same weights
+    and permutation (SGD within fp32 reordering; Adam within its sign-flip bound)."""
     env = dict(os.environ, PYTHONPATH=ROOT, INTML_DP_TIMEOUT="60")
     for k in ("WORLD_SIZE", "RANK", "INTML_DP_BACKEND", "INTML_COMM", "INTML_XGMI", "INTML_BUCKET_BYTES"):
         env.pop(k, None)
@@ -233,13 +233,26 @@ def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(ROOT, "tests", "dp_xgmi_worker_gpu.py"), str(tmp_path)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=420, cwd=ROOT)
+    if r.returncode != 0:
+        diag = [json.load(open(tmp_path / ("dpx%d.json" % i))) for i in range(P) if (tmp_path / ("dpx%d.json" % i)).exists()]
+        print(json.dumps(diag, indent=1))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     reps = [json.load(open(tmp_path / ("dpx%d.json" % i))) for i in range(P)]
-    for rep in reps:
-        assert rep["xgmi_only"] and not rep["rccl"] and rep["reducer"] == "NativeGradReducer", rep
-        assert rep["plane"] == "xgmi" and rep["comm_in_graph"] and len(rep["buckets"]) == 1, rep
-        assert rep["fused_launches"] == ["xgmi_allreduce_optim_b0"], rep
-        assert rep["err"] == 0 and rep["finite"] and rep["moved"] > 1e-4, rep
-    assert len({rep["digest"] for rep in reps}) == 1, [rep["digest"] for rep in reps]
-    vs = reps[0]["vs_single"]
-    assert vs["p999"] < 1e-5 and vs["max"] < 2e-3, vs
+    for top in reps:
+        assert top["xgmi_only"] and not top["rccl"], top
+        for opt in ("Adam", "SGD"):
+            rep = top[opt]
+            assert rep["reducer"] == "NativeGradReducer", rep
+            assert rep["plane"] == "xgmi" and rep["comm_in_graph"] and len(rep["buckets"]) == 1, rep
+            assert rep["fused_launches"] == ["xgmi_allreduce_optim_b0"], rep
+            assert rep["err"] == 0 and rep["finite"] and rep["moved"] > 1e-4, rep
+    for opt in ("Adam", "SGD"):
+        assert len({top[opt]["digest"] for top in reps}) == 1, [top[opt]["digest"] for top in reps]
+    # SGD: linear in the gradient -- only the all-reduce's summation order differs from the
+    # single-process step (p999 / max at fp32 reordering level)
+    vs = reps[0]["SGD"]["vs_single"]
+    assert vs["p999"] < 1e-5 and vs["max"] < 1e-4, vs
+    # Adam: a near-zero gradient element whose sign the reordering flips moves by up to a full
+    # lr (1e-3) per step: bound the tail by 2 lr and the worst element by 24 steps' worth
+    vs = reps[0]["Adam"]["vs_single"]
+    assert vs["p999"] < 2e-3 and vs["max"] < 2.4e-2, vs

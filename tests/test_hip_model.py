@@ -484,30 +484,6 @@ def test_head_fast_paths_bit_identical(kind, drop, cin, hw, opt, monkeypatch):
     assert m1 == m0 and i1 == i0 == 3
 
 
-@pytest.mark.parametrize("kind,drop,cin,hw,opt", [("rpv", 0.2, 3, 64, "Adam"), ("mnist", 0.4, 1, 28, "Adadelta")])
-def test_tail_reduction_bit_identical(kind, drop, cin, hw, opt, monkeypatch):
-    """The last (first-layer) wgrad launch reducing + updating the earlier conv layers' slabs
-    in its own workgroups' tails (wgrad_halo.hip) trains bit-identically to the end-of-step
-    reduction: the same table, the same fixed summation order, another launch."""
-    res = []
-    for tv in ("tail_reduce=1", "tail_reduce=0"):
-        monkeypatch.setenv("INTML_TUNE", tv)
-        set_random_seed(47)
-        m = _build(kind, "cuda", opt=opt, drop=drop, cin=cin, hw=hw)
-        x, y = _data(m, 512, seed=11)
-        ex = m._executor
-        d = ex.upload(x, y)
-        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(7)).to(ex.device)
-        ex.reset_metrics()
-        ex.train_steps(d, perm, 0, 128, 3)
-        torch.cuda.synchronize()
-        bp = ex._plans[(128, "train")]
-        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics(), sorted(bp.early_red)))
-    (w1, m1, e1), (w0, m0, e0) = res
-    assert "wgrad_conv0" in e1 and "wgrad_conv0" not in e0, (e1, e0)
-    assert torch.equal(w1, w0) and m1 == m0
-
-
 @pytest.mark.parametrize("kind,drop,cin,hw", [("rpv", 0.2, 3, 64), ("rpv", 0.0, 1, 16)])
 def test_stack_k16_tail_bit_identical(kind, drop, cin, hw, monkeypatch):
     """The conv stack's 4-channel first layer with its tap-8 k-step as a 16x16x16 MFMA

@@ -57,7 +57,7 @@ def full(r, P, dev, K, X, rep):
     m_ref = 0.1 * gm
     v_ref = 0.001 * gm * gm
     p_ref = p0 - lr_t * m_ref / (torch.sqrt(v_ref) + 1e-7)
-    rep["err"] = int(x.err.item())
+    rep["err"] = int(x.err[0].item())
     rep["grad_sum_ok"] = bool(torch.equal(g, pat * float(P * (P + 1) / 2)))
     rep["adam_maxdiff"] = float((p - p_ref).abs().max())
     rep["p_digest"] = [float(p.double().sum()), float(p.double().abs().sum())]
@@ -68,7 +68,7 @@ def full(r, P, dev, K, X, rep):
         x.launch(g2.data_ptr(), stream)
         torch.cuda.synchronize()
         ok = ok and bool(torch.equal(g2, pat * float(sum(q + 2 + it for q in range(P)))))
-    rep["repeat_ok"] = ok and int(x.err.item()) == 0
+    rep["repeat_ok"] = ok and int(x.err[0].item()) == 0
     x.close()
 
     # a bucket [lo, hi) of a larger flat gradient (hybrid plane: the conv bucket)
@@ -90,7 +90,7 @@ def full(r, P, dev, K, X, rep):
     torch.cuda.synchronize()
     gm = pat[lo:] * (P * (P + 1) / 2.0) / P
     p_ref = p0[lo:] - lr_t * (0.1 * gm) / (torch.sqrt(0.001 * gm * gm) + 1e-7)
-    rep["range_err"] = int(xb.err.item())
+    rep["range_err"] = int(xb.err[0].item())
     rep["range_sum_ok"] = bool(torch.equal(g[lo:], pat[lo:] * float(P * (P + 1) / 2)))
     rep["range_outside_untouched"] = bool(torch.equal(g[:lo], pat[:lo] * float(r + 1))
                                           and torch.equal(p[:lo], p0[:lo]) and not bool(m[:lo].any()))
@@ -114,14 +114,14 @@ def delay(r, P, dev, K, X, rep):
     x.launch(g.data_ptr(), stream)
     torch.cuda.synchronize()
     rep["first_launch_s"] = time.time() - t0
-    rep["err1"] = int(x.err.item())
+    rep["err1"] = int(x.err[0].item())
     # every later launch exits at once on both ranks and touches nothing
     g2 = torch.full((n,), 7.0, device=dev)
     t0 = time.time()
     x.launch(g2.data_ptr(), stream)
     torch.cuda.synchronize()
     rep["second_launch_s"] = time.time() - t0
-    rep["err2"] = int(x.err.item())
+    rep["err2"] = int(x.err[0].item())
     rep["second_untouched"] = bool((g2 == 7.0).all())
     try:
         x.check()
