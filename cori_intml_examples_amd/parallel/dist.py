@@ -26,6 +26,7 @@ import torch
 import torch.distributed as tdist
 
 from . import state as S
+from ..utils.env import tune
 
 
 # ------------------------------------------------------------------------------ bootstrap
@@ -443,7 +444,15 @@ class NativeGradReducer:
         self.xgmi_bucket = None
         if want and self.xgmi is None:
             from . import xgmi as X
-            self.xgmi = X.create(self.rank, self.size, n, self.device, allgather)
+            # ranks sharing a GPU (the one-GPU rehearsal of the multi-GPU step): a few
+            # workgroups only.  A rank's spinning all-reduce workgroups hold their CUs' register
+            # files; at one workgroup per CU they would leave no CU able to host a peer's conv
+            # stack workgroup (3 waves x 168 VGPRs per SIMD), and the peer never reaches its own
+            # all-reduce -- a deadlock that separate GPUs cannot have
+            st = _st()
+            shared = st.local_size > max(1, torch.cuda.device_count())
+            max_wg = int(tune("xgmi_shared_wg", 8)) if shared else None
+            self.xgmi = X.create(self.rank, self.size, n, self.device, allgather, max_wg=max_wg)
             if self.xgmi is not None:
                 self._xgmi_err_host = torch.zeros(4, dtype=torch.int32).pin_memory()
         if self.xgmi is not None:

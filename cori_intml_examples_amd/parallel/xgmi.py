@@ -73,12 +73,13 @@ class XgmiAllreduce:
     every rank must construct it, in the same order."""
 
     def __init__(self, rank: int, size: int, n: int, device: torch.device,
-                 allgather: Callable[[object], List[object]], timeout_s: Optional[float] = None):
+                 allgather: Callable[[object], List[object]], timeout_s: Optional[float] = None,
+                 max_wg: Optional[int] = None):
         K = kernels()
         self.K, self.rank, self.size, self.n, self.device = K, rank, size, n, device
         if size > K.XGMI_MAX_RANKS:
             raise ValueError("xgmi all-reduce supports at most %d ranks" % K.XGMI_MAX_RANKS)
-        self.chunk, self.sub, self.grid = geometry(n, size, K.XGMI_MAX_WG)
+        self.chunk, self.sub, self.grid = geometry(n, size, min(max_wg or K.XGMI_MAX_WG, K.XGMI_MAX_WG))
         words = self.chunk * size
         # layout (bytes): flag1 | flag2 | abort word | inbox [P][chunk] fp32 | outbox [P*chunk] fp32
         self.off_f1, self.off_f2 = 0, 4 * _FLAG_WORDS
@@ -183,12 +184,12 @@ def describe_error(e: int, seq: int = 0, seen: int = 0, where: int = 0) -> str:
 
 
 def create(rank: int, size: int, n: int, device: torch.device, allgather,
-           timeout_s: Optional[float] = None) -> Optional[XgmiAllreduce]:
+           timeout_s: Optional[float] = None, max_wg: Optional[int] = None) -> Optional[XgmiAllreduce]:
     """Build + self-test collectively; returns the object only if EVERY rank passed both
     the setup and the self-test (same decision on every rank: the votes are gathered)."""
     x, why = None, None
     try:
-        x = XgmiAllreduce(rank, size, n, device, allgather, timeout_s=timeout_s)
+        x = XgmiAllreduce(rank, size, n, device, allgather, timeout_s=timeout_s, max_wg=max_wg)
         why = x.setup_error
     except Exception as e:            # noqa: BLE001
         why = "error: %s" % e
