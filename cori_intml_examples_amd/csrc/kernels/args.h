@@ -102,7 +102,8 @@ struct ConvMMArgs {
   // conv_tile path (set => that path is used when there is no unpool-on-load input)
   const bf16* zero = nullptr;
   int dbg = 0;   // ablation (timing only, wrong results): 1 skip staging, 2 skip MFMA, 4 skip stores,
-                 // 8 skip the weight staging only; 16 = per-pixel unpool staging (A/B, exact)
+                 // 8 skip the weight staging only; 16 = per-pixel unpool staging (A/B, exact);
+                 // 32 = weights and pooled halo staged in two phases (A/B, exact)
   unsigned long long* ts = nullptr;   // diagnostics: [grid block][8] phase stamps, wave 0 lane 0 (null = off)
   // conv_halo LDS layout: input-halo pixel stride in elements (0 = Cs_in; padded strides
   // break the fragment reads' bank conflicts, models/lds_layout.py)

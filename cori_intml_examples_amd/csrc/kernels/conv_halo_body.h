@@ -2,6 +2,8 @@
 // as a device function of the block index so dual_halo.hip can co-schedule it with
 // the weight-gradient body in one launch.
 #pragma once
+#include <type_traits>
+
 #include "bwd_through.h"
 
 // NTC n-tiles of the weight slice, TM m-tiles per wave per pass (each A fragment feeds NTC
@@ -61,19 +63,16 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
     return load_bf16x8_if(ok, xbase + ((size_t)iy * a.W + ix) * Cs + c, xbase);
   };
   // weights -> LDS
-  if (dbg_stage && !(a.dbg & 8)) staged_copy<8, bf16x8>(
-      KS * NTC * 64, tid, 256,
-      [&](int i) {
-        const int ks = i / (NTC * 64);   // compile-time power of two
-        const int rem = i - ks * NTC * 64;
-        const int nt = nt0 + (rem >> 6);
-        const bool ok = nt < a.NT;
-        return load_bf16x8_if(ok, a.wpk + ((size_t)(ks * a.NT + nt) * 64 + (rem & 63)) * 8, a.wpk);
-      },
-      [&](int i, const bf16x8& v) { *reinterpret_cast<bf16x8*>(wl + (size_t)i * 8) = v; });
-  HALO_STAMP(1);
-  // k-chunk -> halo offset table
-  {
+  auto wload = [&](int i) {
+    const int ks = i / (NTC * 64);   // compile-time power of two
+    const int rem = i - ks * NTC * 64;
+    const int nt = nt0 + (rem >> 6);
+    const bool ok = nt < a.NT;
+    return load_bf16x8_if(ok, a.wpk + ((size_t)(ks * a.NT + nt) * 64 + (rem & 63)) * 8, a.wpk);
+  };
+  auto wstore = [&](int i, const bf16x8& v) { *reinterpret_cast<bf16x8*>(wl + (size_t)i * 8) = v; };
+  const int nw = KS * NTC * 64;
+  auto build_tab = [&]() {   // k-chunk -> halo offset table
     const int KHW = a.KH * a.KW;
     const int cw = CS4 ? 4 : 8;
     for (int c = tid; c < ntab; c += 256) {
@@ -86,107 +85,147 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
       }
       tab[c] = e;
     }
-  }
-  // input halo -> LDS
-  if (dbg_stage) {
-    if (CS4) {
-      staged_copy<8, bf16x4>(
-          nch, tid, 256,
-          [&](int i) {
-            int c, iy, ix;
-            const bool ok = coords(i, c, iy, ix);
-            return load_bf16x4_if(ok, xbase + ((size_t)iy * a.W + ix) * 4, xbase);
-          },
-          [&](int i, const bf16x4& v) { *reinterpret_cast<bf16x4*>(xl + (size_t)i * 4) = v; });
-    } else if (cbase && dil == 1 && !(a.dbg & 16)) {
-      // Pooled input (dY = unpool(dP, codes)): load each pooled chunk ONCE and expand it into
-      // the (up to) four full-resolution halo pixels of its window -- a quarter of the
-      // global loads of rebuilding every pixel from its window (unpool_load8 per pixel).
-      const int Ha = 2 * a.in_pH, Wa = 2 * a.in_pW;
-      const int y_lo = max(yb, 0), y_hi = min(yb + R_in, Ha);
-      const int x_lo = max(xb0, 0), x_hi = min(xb0 + W_in, Wa);
-      // halo pixels outside the pooled area (padding, odd edge) hold zeros: whole rows above
-      // / below it and the columns left / right of it -- enumerated directly (the border is
-      // a few hundred chunks; testing all R_in x W_in chunks cost two FastDivs each), and
-      // written while the first batch of pooled loads is in flight
-      auto zero_border = [&]() {
-        const int ntop = min(R_in, max(0, -yb));
-        const int nbot = min(R_in - ntop, max(0, yb + R_in - Ha));
-        const int lc = min(W_in, max(0, -xb0)), rc = min(W_in - lc, max(0, xb0 + W_in - Wa));
-        const int rowch = W_in * hcpp;
-        for (int rr = 0; rr < ntop + nbot; ++rr) {         // workgroup-uniform
-          const int r = rr < ntop ? rr : R_in - 1 - (rr - ntop);
-          for (int i = tid; i < rowch; i += 256) {
-            const int px = fcpp.div(i);
-            *reinterpret_cast<bf16x8*>(xl + (size_t)(r * W_in + px) * XP + (i - px * hcpp) * 8) = zero_bf16x8();
-          }
-        }
-        const int side = (lc + rc) * hcpp;
-        const int nside = (R_in - ntop - nbot) * side;
-        for (int i = tid; i < nside; i += 256) {
-          const int m = i / side, j = i - m * side;
-          const int cp = j / hcpp, ch = j - cp * hcpp;
-          const int px = cp < lc ? cp : W_in - rc + (cp - lc);
-          *reinterpret_cast<bf16x8*>(xl + (size_t)((ntop + m) * W_in + px) * XP + ch * 8) = zero_bf16x8();
-        }
-      };
-      if (!(y_lo < y_hi && x_lo < x_hi)) zero_border();
-      if (y_lo < y_hi && x_lo < x_hi) {
-        const int py0 = y_lo >> 1, npy = ((y_hi - 1) >> 1) - py0 + 1;
-        const int px0 = x_lo >> 1, npx = ((x_hi - 1) >> 1) - px0 + 1;
-        const int nq = npy * npx * hcpp;
-        const FastDiv fnpx(npx);
-        constexpr int UQ = 4;
-        for (int q0 = tid; q0 < nq; q0 += 256 * UQ) {
-          uint4 raw[UQ];
-          uint2 cw[UQ];
-          int qy[UQ], qx[UQ], qc[UQ];
-#pragma unroll
-          for (int u = 0; u < UQ; ++u) {   // branch-free: clamped index, always loaded
-            const int q = min(q0 + u * 256, nq - 1);
-            const int pp = fcpp.div(q);
-            qc[u] = (q - pp * hcpp) * 8;
-            const int ry = fnpx.div(pp);
-            qy[u] = py0 + ry;
-            qx[u] = px0 + (pp - ry * npx);
-            const size_t o = ((size_t)qy[u] * a.in_pW + qx[u]) * Cs + qc[u];
-            raw[u] = *reinterpret_cast<const uint4*>(xbase + o);
-            cw[u] = *reinterpret_cast<const uint2*>(cbase + o);
-          }
-          if (q0 == tid) zero_border();               // beside the first batch's loads
-                                                      // (threads past nq: after the loop)
-#pragma unroll
-          for (int u = 0; u < UQ; ++u) {
-            if (q0 + u * 256 >= nq) break;
-#pragma unroll
-            for (int pos = 0; pos < 4; ++pos) {
-              const int y = 2 * qy[u] + (pos >> 1), x = 2 * qx[u] + (pos & 1);
-              if (y < y_lo || y >= y_hi || x < x_lo || x >= x_hi) continue;
-              uint32_t m[4];
-#pragma unroll
-              for (int h = 0; h < 2; ++h) {
-                const uint32_t w = h ? cw[u].y : cw[u].x;
-                m[2 * h] = (((w & 0xFF) == (uint32_t)pos) ? 0x0000FFFFu : 0u) |
-                           ((((w >> 8) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
-                m[2 * h + 1] = ((((w >> 16) & 0xFF) == (uint32_t)pos) ? 0x0000FFFFu : 0u) |
-                               ((((w >> 24) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
-              }
-              const uint4 v = {raw[u].x & m[0], raw[u].y & m[1], raw[u].z & m[2], raw[u].w & m[3]};
-              *reinterpret_cast<uint4*>(xl + ((size_t)((y - yb) * W_in + (x - xb0)) * XP + qc[u])) = v;
-            }
-          }
-        }
-        if (tid >= nq) zero_border();
+  };
+  // Pooled input (dY = unpool(dP, codes)): load each pooled chunk ONCE and expand it into the
+  // (up to) four full-resolution halo pixels of its window -- a quarter of the global loads of
+  // rebuilding every pixel from its window (unpool_load8 per pixel).
+  const bool pooled_in = !CS4 && cbase && dil == 1 && !(a.dbg & 16);
+  const int Ha = 2 * a.in_pH, Wa = 2 * a.in_pW;
+  const int y_lo = max(yb, 0), y_hi = min(yb + R_in, Ha);
+  const int x_lo = max(xb0, 0), x_hi = min(xb0 + W_in, Wa);
+  const bool pin = y_lo < y_hi && x_lo < x_hi;
+  const int py0 = y_lo >> 1, npy = pin ? ((y_hi - 1) >> 1) - py0 + 1 : 0;
+  const int px0 = x_lo >> 1, npx = pin ? ((x_hi - 1) >> 1) - px0 + 1 : 1;
+  const int nq = npy * npx * hcpp;
+  const FastDiv fnpx(npx);
+  constexpr int UQ = 4;
+  // halo pixels outside the pooled area (padding, odd edge) hold zeros: whole rows above /
+  // below it and the columns left / right of it -- enumerated directly (the border is a few
+  // hundred chunks; testing all R_in x W_in chunks cost two FastDivs each)
+  auto zero_border = [&]() {
+    const int ntop = min(R_in, max(0, -yb));
+    const int nbot = min(R_in - ntop, max(0, yb + R_in - Ha));
+    const int lc = min(W_in, max(0, -xb0)), rc = min(W_in - lc, max(0, xb0 + W_in - Wa));
+    const int rowch = W_in * hcpp;
+    for (int rr = 0; rr < ntop + nbot; ++rr) {         // workgroup-uniform
+      const int r = rr < ntop ? rr : R_in - 1 - (rr - ntop);
+      for (int i = tid; i < rowch; i += 256) {
+        const int px = fcpp.div(i);
+        *reinterpret_cast<bf16x8*>(xl + (size_t)(r * W_in + px) * XP + (i - px * hcpp) * 8) = zero_bf16x8();
       }
-    } else {
-      staged_copy<8, bf16x8>(nch, tid, 256, halo8, [&](int i, const bf16x8& v) {
-        int o = i * 8;
-        if (XP != Cs) {
-          const int pix = fcpp.div(i);
-          o = pix * XP + (i - pix * hcpp) * 8;
+    }
+    const int side = (lc + rc) * hcpp;
+    const int nside = (R_in - ntop - nbot) * side;
+    for (int i = tid; i < nside; i += 256) {
+      const int m = i / side, j = i - m * side;
+      const int cp = j / hcpp, ch = j - cp * hcpp;
+      const int px = cp < lc ? cp : W_in - rc + (cp - lc);
+      *reinterpret_cast<bf16x8*>(xl + (size_t)((ntop + m) * W_in + px) * XP + ch * 8) = zero_bf16x8();
+    }
+  };
+  // one batch of UQ pooled chunks per thread: load (branch-free: clamped index, always loaded)
+  // ... and expand into the window's pixels
+  uint4 raw[UQ];
+  uint2 cwd[UQ];
+  int qy[UQ], qx[UQ], qc[UQ];
+  auto pq_load = [&](int q0) {
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      const int q = min(q0 + u * 256, nq - 1);
+      const int pp = fcpp.div(q);
+      qc[u] = (q - pp * hcpp) * 8;
+      const int ry = fnpx.div(pp);
+      qy[u] = py0 + ry;
+      qx[u] = px0 + (pp - ry * npx);
+      const size_t o = ((size_t)qy[u] * a.in_pW + qx[u]) * Cs + qc[u];
+      raw[u] = *reinterpret_cast<const uint4*>(xbase + o);
+      cwd[u] = *reinterpret_cast<const uint2*>(cbase + o);
+    }
+  };
+  auto pq_expand = [&](int q0) {
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      if (q0 + u * 256 >= nq) break;
+#pragma unroll
+      for (int pos = 0; pos < 4; ++pos) {
+        const int y = 2 * qy[u] + (pos >> 1), x = 2 * qx[u] + (pos & 1);
+        if (y < y_lo || y >= y_hi || x < x_lo || x >= x_hi) continue;
+        uint32_t m[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t w = h ? cwd[u].y : cwd[u].x;
+          m[2 * h] = (((w & 0xFF) == (uint32_t)pos) ? 0x0000FFFFu : 0u) |
+                     ((((w >> 8) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
+          m[2 * h + 1] = ((((w >> 16) & 0xFF) == (uint32_t)pos) ? 0x0000FFFFu : 0u) |
+                         ((((w >> 24) & 0xFF) == (uint32_t)pos) ? 0xFFFF0000u : 0u);
         }
-        *reinterpret_cast<bf16x8*>(xl + o) = v;
-      });
+        const uint4 v = {raw[u].x & m[0], raw[u].y & m[1], raw[u].z & m[2], raw[u].w & m[3]};
+        *reinterpret_cast<uint4*>(xl + ((size_t)((y - yb) * W_in + (x - xb0)) * XP + qc[u])) = v;
+      }
+    }
+  };
+  // One-batch prologue (the co-scheduled dgrad of the RPV / MNIST stacks: the pooled halo is
+  // one batch of chunks per thread): the weight vectors' loads go out first, the halo's right
+  // behind them, and only then are the weights stored -- their wait (in-order vmcnt) does not
+  // cover the halo loads, so the two global round trips overlap instead of running back to
+  // back.  (Halo loads issued BEFORE the weights' were measured 3 us slower: the weights'
+  // stores then wait behind them.)  dbg 32: the two-phase form (A/B, exact).
+  const bool onebatch = dbg_stage && pooled_in && pin && !(a.dbg & (8 | 32)) && nq <= 256 * UQ && nw <= 8 * 256;
+  if (onebatch) {
+    auto fused = [&](auto wu) {
+      constexpr int WU = decltype(wu)::value;
+      bf16x8 wv[WU];
+#pragma unroll
+      for (int u = 0; u < WU; ++u) wv[u] = wload(min(tid + u * 256, nw - 1));
+      pq_load(tid);
+#pragma unroll
+      for (int u = 0; u < WU; ++u)
+        if (tid + u * 256 < nw) wstore(tid + u * 256, wv[u]);
+      HALO_STAMP(1);
+      build_tab();
+      zero_border();
+      pq_expand(tid);
+    };
+    const int wit = (nw + 255) >> 8;
+    if (wit <= 2) fused(std::integral_constant<int, 2>{});
+    else if (wit <= 4) fused(std::integral_constant<int, 4>{});
+    else fused(std::integral_constant<int, 8>{});
+  } else {
+    if (dbg_stage && !(a.dbg & 8)) staged_copy<8, bf16x8>(nw, tid, 256, wload, wstore);
+    HALO_STAMP(1);
+    build_tab();
+    // input halo -> LDS
+    if (dbg_stage) {
+      if (CS4) {
+        staged_copy<8, bf16x4>(
+            nch, tid, 256,
+            [&](int i) {
+              int c, iy, ix;
+              const bool ok = coords(i, c, iy, ix);
+              return load_bf16x4_if(ok, xbase + ((size_t)iy * a.W + ix) * 4, xbase);
+            },
+            [&](int i, const bf16x4& v) { *reinterpret_cast<bf16x4*>(xl + (size_t)i * 4) = v; });
+      } else if (pooled_in) {
+        if (!pin) zero_border();
+        if (pin) {
+          for (int q0 = tid; q0 < nq; q0 += 256 * UQ) {
+            pq_load(q0);
+            if (q0 == tid) zero_border();               // beside the first batch's loads
+                                                        // (threads past nq: after the loop)
+            pq_expand(q0);
+          }
+          if (tid >= nq) zero_border();
+        }
+      } else {
+        staged_copy<8, bf16x8>(nch, tid, 256, halo8, [&](int i, const bf16x8& v) {
+          int o = i * 8;
+          if (XP != Cs) {
+            const int pix = fcpp.div(i);
+            o = pix * XP + (i - pix * hcpp) * 8;
+          }
+          *reinterpret_cast<bf16x8*>(xl + o) = v;
+        });
+      }
     }
   }
   HALO_STAMP(2);

@@ -962,6 +962,7 @@ class BatchPlan(GeometryMixin):
                 a.st = st_ptr
                 a.bt = self._bt_for(Src("conv", prev.i, prev.Cout, prev.Cs_out, prev.Hp, prev.Wp))
                 a.tm = tune("dgrad_tm%d" % g.i, 0)      # co-scheduled dgrad m-tiles per wave per pass
+                a.dbg = tune("dgrad_dbg", 0)            # A/B switches (ConvMMArgs::dbg; exact ones only)
                 dname = "dgrad_conv%d" % g.i
                 dual = (tune("dual_halo", True)
                         and not self._wide(g.Cs_in, g.KS, g.NT) and not self._wide(a.Cs_in, a.KS, g.NTd))

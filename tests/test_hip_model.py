@@ -546,3 +546,24 @@ def test_write_through_stores_bit_identical(kind, drop, cin, hw, monkeypatch):
         torch.cuda.synchronize()
         res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
     assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
+
+
+@pytest.mark.parametrize("kind,drop,cin,hw", [("rpv", 0.2, 3, 64), ("mnist", 0.3, 1, 28)])
+def test_dgrad_onebatch_prologue_bit_identical(kind, drop, cin, hw, monkeypatch):
+    """The co-scheduled dgrad's one-batch prologue (weight and pooled-halo loads in flight
+    together, conv_halo_body.h) stages exactly what the two-phase form (dgrad_dbg=32) does:
+    whole training steps bit-identical."""
+    res = []
+    for tv in ("dgrad_dbg=0", "dgrad_dbg=32"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(51)
+        m = _build(kind, "cuda", opt="Adam", drop=drop, cin=cin, hw=hw)
+        x, y = _data(m, 256, seed=15)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(12)).to(ex.device)
+        ex.reset_metrics()
+        ex.train_steps(d, perm, 0, 128, 2)
+        torch.cuda.synchronize()
+        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
+    assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
