@@ -287,6 +287,18 @@ struct HeadArgs {
   int generic = 0;
 };
 
+// The last hidden dense layer + the binary output head in one launch (dense_head.hip):
+// 16-row x 16-column output tiles over 1/kh of K per 16-wave workgroup, the last arriving
+// workgroup of each 16-row group finishing the layer and running the head for those rows.
+struct DenseHeadArgs {
+  DenseFwdArgs f;                // x, wpk, NT, KS, Ks, M; part: the fp32 tile partials
+                                 // [kh][M][NT*16]; book / sb: the step bookkeeping
+  HeadArgs h;                    // the head; h.epi: the dense layer's epilogue (bias, ReLU,
+                                 // dropout, out)
+  unsigned* ticket = nullptr;    // [row groups + 1] monotonic arrival counters (zeroed once)
+  int kh = 2;                    // workgroups along K per output tile
+};
+
 struct GatherArgs {
   const bf16* xs = nullptr;      // dataset [Nd][R] bf16
   const float* ys = nullptr;     // [Nd][C]

@@ -29,6 +29,8 @@ void launch_dense_epi(const DenseEpiArgs& a, hipStream_t s);
 int dense_groups(int M, int NT, int KS);
 bool dense_big(int NT, int KS);
 void launch_head(const HeadArgs& a, hipStream_t s);
+void launch_dense_head(const DenseHeadArgs& a, hipStream_t s);
+int dense_head_blocks(const DenseHeadArgs& a);
 bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits,
                       const DualExtra& x, hipStream_t s);
 bool launch_dense_bwd_dual(const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da,
@@ -126,6 +128,10 @@ PYBIND11_MODULE(_kernels, m) {
       RW(HeadArgs, act) RW(HeadArgs, training) RW(HeadArgs, inv_bs) PTR(HeadArgs, st) PTR(HeadArgs, probs)
       PTR(HeadArgs, wslab) PTR(HeadArgs, bslab) RW(HeadArgs, bt) RW(HeadArgs, epi) PTR(HeadArgs, ts)
       PTR(HeadArgs, yidx) RW(HeadArgs, generic);
+
+  py::class_<DenseHeadArgs>(m, "DenseHeadArgs")
+      .def(py::init<>())
+      RW(DenseHeadArgs, f) RW(DenseHeadArgs, h) PTR(DenseHeadArgs, ticket) RW(DenseHeadArgs, kh);
 
   py::class_<GatherArgs>(m, "GatherArgs")
       .def(py::init<>())
@@ -304,6 +310,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("dense_big", &dense_big, "dense_fwd uses the large-weight LDS path for (NT, KS)");
   m.def("dense_epi", [](const DenseEpiArgs& a, uintptr_t s) { launch_dense_epi(a, S(s)); check_last("dense_epi"); });
   m.def("head", [](const HeadArgs& a, uintptr_t s) { launch_head(a, S(s)); check_last("head"); });
+  m.def("dense_head", [](const DenseHeadArgs& a, uintptr_t s) { launch_dense_head(a, S(s)); check_last("dense_head"); },
+        "last hidden dense layer + binary head in one launch (dense_head.hip)");
+  m.def("dense_head_blocks", &dense_head_blocks);
   m.def("prologue", [](const PrologueArgs& a, const PackTable& t, uintptr_t s) {
     launch_prologue(a, t, S(s)); check_last("prologue"); });
   m.def("gather_gx", &gather_gx);

@@ -602,6 +602,29 @@ class BatchPlan(GeometryMixin):
         idx = self.srcidx.long()
         return d.x[idx], d.y[idx]
 
+    def _dense_head_args(self, h, epi, last_fwd, training):
+        """DenseHeadArgs for the fused dense layer + binary head launch when it applies: a
+        training step whose head (sigmoid, one output) reads the last hidden dense layer's
+        output (<= 256 columns), that layer on the small-weight path; else None."""
+        ex, K = self.ex, self.ex.K
+        if last_fwd is None or not training or not tune("dense_head", True):
+            return None
+        i, a, g = last_fwd
+        hd = ex.plan.head
+        kh = int(tune("dense_head_kh", 2))
+        splits = self.dense_splits[g.j][0]
+        if not (ex.head_act == 1 and hd.N == 1 and ex.head_src.kind == "dense" and g.Ns <= 256
+                and hd.K <= g.Ns and h.flat_C == h.flat_Cs and not K.dense_big(a.NT, a.KS)
+                and 1 <= kh <= splits and h.bt.dy and h.bt.prev_out == epi.out
+                and h.bt.pH == 1 and h.bt.pW == 1):
+            return None
+        d = K.DenseHeadArgs()
+        d.f, d.h, d.kh = a, h, kh
+        mgroups = cdiv(a.M, 16)
+        self.dense_head_ticket = torch.zeros(mgroups + 1, dtype=torch.int32, device=ex.device)
+        d.ticket = self.dense_head_ticket.data_ptr()
+        return d
+
     def _src_buf(self, src: Src):
         if src.kind == "input":
             return self.xb
@@ -743,6 +766,7 @@ class BatchPlan(GeometryMixin):
             if self.pro_free and g.j == 0 and training:
                 a.book, a.sb = 1, sb      # this step's bookkeeping (the stack read t + 1)
             self.launches.append(("dense_fwd%d" % g.j, lambda s, a=a: K.dense_fwd(a, s)))
+            last_fwd = (len(self.launches) - 1, a, g)
             e = K.DenseEpiArgs()
             e.part = a.part
             e.splits, e.M, e.N, e.Ns, e.ldp = splits, bs, g.N, g.Ns, g.NT * 16
@@ -789,7 +813,13 @@ class BatchPlan(GeometryMixin):
             bt = self._bt_for(src)
             if bt is not None:
                 h.bt = bt
-        self.launches.append(("head", lambda s, a=h: K.head(a, s)))
+        dh = self._dense_head_args(h, head_epi, last_fwd if head_epi is not None else None, training)
+        if dh is not None:
+            # the last dense layer and the head in ONE launch (dense_head.hip) in place of the
+            # split-K dense launch; no separate head launch
+            self.launches[last_fwd[0]] = ("dense_head", lambda s, a=dh: K.dense_head(a, s))
+        else:
+            self.launches.append(("head", lambda s, a=h: K.head(a, s)))
         if not training:
             return
 
