@@ -170,7 +170,8 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       const bool rowal = (a.Wo & 31) == 0 && (npix & 31) == 0 && !(a.kperm & 2);
       const int la0 = dP0 * s * XP, la1 = dP1 * s * XP;
       int y = 0, x0 = 0;
-      for (int ks = 0; ks < nks; ++ks) {
+      // k-step ks's fragments (the row-aligned path's scalar position (y, x0) advances)
+      auto frags = [&](const int ks, bf16x8 (&afr)[MTW], bf16x8 (&bfr)[NTT]) {
         // per-lane pixel rows of the two transposed reads (h = 0, 1).  MFMA k index 8g + j
         // stands for pixel 4g + j (j < 4) / 16 + 4g + j - 4 (j >= 4) of the k-step -- the same
         // bijection for both operands, so a 32-lane half reads 8 CONSECUTIVE pixels (the
@@ -189,7 +190,6 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
           off1 = ((y1 * s) * XR + (q1 - y1 * a.Wo) * s) * XP;
         }
         const bf16* pbrow = dyl + (size_t)P0 * ldb + 4 * (i & 3);
-        bf16x8 bfr[NTT], afr[MTW];
   #pragma unroll
         for (int v = 0; v < NTT; ++v) {
           const bf16* pb = pbrow + v * 16;
@@ -201,12 +201,40 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
           const bf16* pa1 = ko[u] >= 0 ? xl + off1 + ko[u] : zl;
           afr[u] = tbias[u] ? ones : __builtin_shufflevector(tr_read_h(pa0), tr_read_h(pa1), 0, 1, 2, 3, 4, 5, 6, 7);
         }
+      };
+      auto mmas = [&](const bf16x8 (&afr)[MTW], const bf16x8 (&bfr)[NTT]) {
   #pragma unroll
         for (int u = 0; u < MTW; ++u)
           if (tval[u]) {
   #pragma unroll
             for (int v = 0; v < NTT; ++v) acc[u][v] = mfma16(afr[u], bfr[v], acc[u][v]);
           }
+      };
+      if constexpr (!PIPE) {
+        // (the standalone launch's variant, registers to spare: the dual kernels sit at the
+        // 256-VGPR edge of two waves per SIMD) software-pipelined: k-step ks + 1's LDS reads
+        // are issued before k-step ks's MFMAs, so the transposed-read latency overlaps the
+        // matrix work instead of stalling every k-step (same k order: bit-identical)
+        if (!(a.dbg & 32)) {
+          bf16x8 a0[MTW], b0[NTT], a1[MTW], b1[NTT];
+          if (nks > 0) frags(0, a0, b0);
+          for (int ks = 0; ks < nks; ks += 2) {
+            if (ks + 1 < nks) frags(ks + 1, a1, b1);
+            __builtin_amdgcn_sched_barrier(0);
+            mmas(a0, b0);
+            if (ks + 1 < nks) {
+              if (ks + 2 < nks) frags(ks + 2, a0, b0);
+              __builtin_amdgcn_sched_barrier(0);
+              mmas(a1, b1);
+            }
+          }
+          return;
+        }
+      }
+      for (int ks = 0; ks < nks; ++ks) {
+        bf16x8 bfr[NTT], afr[MTW];
+        frags(ks, afr, bfr);
+        mmas(afr, bfr);
       }
   };
 

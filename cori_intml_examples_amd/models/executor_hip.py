@@ -844,11 +844,11 @@ class BatchPlan(GeometryMixin):
         # slower on RPV at batch 128: the 128 wgrad workgroups move the layer's 14 MB of optimizer
         # state at per-CU bandwidth (wgrad 6.1 -> 9.7 us) while the end-of-step reduction, which
         # spreads it over thousands of workgroups, only drops 10.8 -> 8.2 us
-        # dense_opt: "auto" = only layers whose gradient is written in place (> 16 MB, the legacy
-        # model's 33.5M-weight Dense(512)) -- measured slower there too (1.27 -> 1.35 ms/step:
-        # the wgrad's few workgroups move ~1 GB of optimizer state, and the layer's dX becomes a
-        # launch of its own); "1" = every one-split layer; default "0"
-        dense_opt = str(tune("dense_opt", "0")).lower()
+        # dense_opt: "auto" (default) = only layers whose gradient is written in place (> 16 MB,
+        # the legacy model's 33.5M-weight Dense(512)): their update moves ~1 GB either way, and
+        # fusing it saves the gradient's own write + re-read (legacy 1.269 -> 1.238 ms/step,
+        # profiles/r4c_ab_legacy.txt); "1" = every one-split layer; "0" = off
+        dense_opt = str(tune("dense_opt", "auto")).lower()
         self.dense_opt_ok = (ex.reducer is None and tune("fuse_optim", True)
                              and dense_opt not in ("0", "false", "off", "no"))
         self.dense_opt_all = dense_opt in ("1", "true", "on", "yes")

@@ -88,7 +88,7 @@ def test_dense_fused_optimizer_matches_reduction(monkeypatch):
 @gpu
 def test_dense_fused_optimizer_writes_packs_legacy(monkeypatch):
     """Legacy RPV (Dense(512) on a flattened 16384-wide input: its gradient is written in
-    place) with the optimizer fused into the dense wgrad (opt-in dense_opt=auto): the kernel
+    place) with the optimizer fused into the dense wgrad (dense_opt=auto, the default): the kernel
     also writes the layer's forward / backward bf16 packs from its updated-weight tile, and
     the layer's dX (the backward pack's reader) runs as a launch BEFORE it -- so after a few
     steps (a) the packs equal a full re-pack of the master bit for bit and (b) the weights
@@ -116,7 +116,7 @@ def test_dense_fused_optimizer_writes_packs_legacy(monkeypatch):
         names = [it[0] for it in plan.launches]
         out[flag] = (np.concatenate([w.ravel() for w in m.get_weights()]), len(plan.dense_fused_opt),
                      bool(plan.optim_fused), torch.equal(arena, ex.arena), names)
-    assert out["auto"][1] == 1 and out["0"][1] == 0, "fused path not taken with dense_opt=auto / taken with =0"
+    assert out["auto"][1] == 1 and out["0"][1] == 0, "fused path not taken by default / taken with dense_opt=0"
     assert out["auto"][3], "packs written by the fused dense optimizer differ from a re-pack"
     nm = out["auto"][4]
     assert "dense_dx0" in nm and nm.index("dense_dx0") < nm.index("wgrad_dense0"), nm
