@@ -6,13 +6,16 @@
 // Step bookkeeping (one thread): iteration counter, LR decay and the optimizer's
 // bias-correction scalars for this step.  (The data cursor is advanced by the head kernel,
 // after every prologue workgroup has read it.)
-__device__ __forceinline__ void step_bookkeeping(const StepBeginArgs& a) {
+// write_t false: every scalar of step st->t + 1 but the counter itself, which the caller
+// advances once no reader of the old count remains (dense_head.hip)
+__device__ __forceinline__ void step_bookkeeping(const StepBeginArgs& a, bool write_t = true) {
   StepState* st = a.st;
   if (!a.training) return;
-  st->t += 1;
-  const double t = (double)st->t;
+  const int t1 = st->t + 1;
+  if (write_t) st->t = t1;
+  const double t = (double)t1;
   double base = (double)st->lr;
-  const int g = st->t - st->warm_t0 - 1;
+  const int g = t1 - st->warm_t0 - 1;
   if (g >= 0 && g < st->warm_steps) {
     const double n = (double)st->warm_size;
     base = (double)st->warm_base / n * ((double)(g + 1) / st->warm_spe * (n - 1.0) / st->warm_epochs + 1.0);

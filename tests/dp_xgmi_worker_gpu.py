@@ -91,8 +91,9 @@ def run(opt, lr, outdir, r, P, dev):
         single.set_weights(w0)
         ws = train(single, data, perm.contiguous(), GLOBAL_B)
         d = np.abs(w - ws)
-        rep["vs_single"] = {"p999": float(np.quantile(d, 0.999)), "max": float(d.max()),
-                            "step_norm": float(np.linalg.norm(ws - np.concatenate([a.reshape(-1) for a in w0])))}
+        step = float(np.linalg.norm(ws - np.concatenate([a.reshape(-1) for a in w0])))
+        rep["vs_single"] = {"p999": float(np.quantile(d, 0.999)), "max": float(d.max()), "step_norm": step,
+                            "rel": float(np.linalg.norm(w - ws) / max(step, 1e-30))}
     return rep
 
 

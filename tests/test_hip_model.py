@@ -600,8 +600,8 @@ def test_dense_head_matches_split_launches(opt, lr, monkeypatch):
         assert float(d.max()) < 1e-4, float(d.max())
     else:
         assert float(torch.quantile(d[:1 << 20], 0.999)) < 2e-3 and float(d.max()) < 8e-3, float(d.max())
-    for k in m0:
-        assert abs(m1[k] - m0[k]) <= 1e-3 * max(1.0, abs(m0[k])), (k, m1[k], m0[k])
+    for v1, v0 in zip(m1, m0):
+        assert abs(v1 - v0) <= 1e-3 * max(1.0, abs(v0)), (m1, m0)
 
 
 @pytest.mark.parametrize("kind,drop,cin,hw", [("rpv", 0.2, 3, 64), ("mnist", 0.3, 1, 28)])
