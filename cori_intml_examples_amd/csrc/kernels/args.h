@@ -192,8 +192,7 @@ struct WgradArgs {
   // when it applies: 8 n-tiles per workgroup, unpooled dY)
   const bf16* zero = nullptr;
   int dbg = 0;   // ablation (timing only): 1 skip staging, 2 skip MFMA, 4 skip slab stores;
-                 // 16 = per-pixel unpool staging of pooled dY; 32 = the standalone halo
-                 // launch's k loop without its software pipeline (A/B, exact)
+                 // 16 = per-pixel unpool staging of pooled dY (A/B, exact)
   unsigned long long* ts = nullptr;   // diagnostics: per-workgroup [start, end] wall clock (null = off)
   unsigned long long* ts2 = nullptr;  // diagnostics: per-workgroup [16] phase stamps (null = off)
   // dense_wgrad with ONE split and the identity layout (slab == the Keras gradient): when
@@ -201,6 +200,9 @@ struct WgradArgs {
   // bias, opt_b + n) as soon as their gradient is final -- no slab reduction for the layer
   OptimArgs opt;
   int opt_w = -1, opt_b = -1;
+  // (with opt_w: opt_nograd = 1 skips storing the in-place gradient the update consumed --
+  // single-GPU step, nothing reads it; the data-parallel step never fuses the update here)
+  int opt_nograd = 0;
   // ... and (pk_fwd >= 0) the updated weights' bf16 copies written into the layer's forward /
   // backward fragment packs (element offsets in opt.arena, their n-tile counts) as whole
   // 16-byte vectors from an LDS tile -- the workgroup's 32 features x NTT*16 outputs are

@@ -105,7 +105,7 @@ PYBIND11_MODULE(_kernels, m) {
       RW(WgradArgs, dbg) PTR(WgradArgs, ts) PTR(WgradArgs, ts2) RW(WgradArgs, opt) RW(WgradArgs, opt_w)
       RW(WgradArgs, opt_b) RW(WgradArgs, xpix) RW(WgradArgs, xrow) RW(WgradArgs, dyld) RW(WgradArgs, kperm)
       PTR(WgradArgs, xidx) PTR(WgradArgs, xst) RW(WgradArgs, pk_fwd) RW(WgradArgs, pk_bwd) RW(WgradArgs, pk_NT)
-      RW(WgradArgs, pk_NTb) RW(WgradArgs, wt);
+      RW(WgradArgs, pk_NTb) RW(WgradArgs, wt) RW(WgradArgs, opt_nograd);
 
   py::class_<DenseFwdArgs>(m, "DenseFwdArgs")
       .def(py::init<>())

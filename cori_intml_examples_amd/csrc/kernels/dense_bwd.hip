@@ -234,7 +234,7 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
 #pragma unroll
       for (int w = 1; w < 4; ++w) s += *reinterpret_cast<const f32x4*>(red + (w * 16 + row) * G::LDR + c4 * 4);
       if (f < a.Ktiles * 16 && n < ld) {
-        *reinterpret_cast<f32x4*>(slab + (size_t)f * ld + n) = s;
+        if (!(OPT && a.opt_nograd)) *reinterpret_cast<f32x4*>(slab + (size_t)f * ld + n) = s;
         if constexpr (OPT) {
           const f32x4 pn = dw_opt4(a.opt, (size_t)a.opt_w + (size_t)f * ld + n, s, op[kt][q], om[kt][q], ov[kt][q]);
           if (packs) {

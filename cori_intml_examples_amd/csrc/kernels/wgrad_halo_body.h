@@ -210,27 +210,6 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
             for (int v = 0; v < NTT; ++v) acc[u][v] = mfma16(afr[u], bfr[v], acc[u][v]);
           }
       };
-      if constexpr (!PIPE) {
-        // (the standalone launch's variant, registers to spare: the dual kernels sit at the
-        // 256-VGPR edge of two waves per SIMD) software-pipelined: k-step ks + 1's LDS reads
-        // are issued before k-step ks's MFMAs, so the transposed-read latency overlaps the
-        // matrix work instead of stalling every k-step (same k order: bit-identical)
-        if (!(a.dbg & 32)) {
-          bf16x8 a0[MTW], b0[NTT], a1[MTW], b1[NTT];
-          if (nks > 0) frags(0, a0, b0);
-          for (int ks = 0; ks < nks; ks += 2) {
-            if (ks + 1 < nks) frags(ks + 1, a1, b1);
-            __builtin_amdgcn_sched_barrier(0);
-            mmas(a0, b0);
-            if (ks + 1 < nks) {
-              if (ks + 2 < nks) frags(ks + 2, a0, b0);
-              __builtin_amdgcn_sched_barrier(0);
-              mmas(a1, b1);
-            }
-          }
-          return;
-        }
-      }
       for (int ks = 0; ks < nks; ++ks) {
         bf16x8 bfr[NTT], afr[MTW];
         frags(ks, afr, bfr);

@@ -603,11 +603,14 @@ class BatchPlan(GeometryMixin):
         return d.x[idx], d.y[idx]
 
     def _dense_head_args(self, h, epi, last_fwd, training):
-        """DenseHeadArgs for the fused dense layer + binary head launch when it applies: a
+        """DenseHeadArgs for the fused dense layer + binary head launch (opt-in, dense_head=1:
+        measured 15.6 us for the launch against 13.3 us for the split-K dense launch + head
+        launch it replaces at RPV B=128 -- its 128 tile workgroups stream K at per-CU bandwidth
+        where the split-K launch spreads it over 512) when it applies: a
         training step whose head (sigmoid, one output) reads the last hidden dense layer's
         output (<= 256 columns), that layer on the small-weight path; else None."""
         ex, K = self.ex, self.ex.K
-        if last_fwd is None or not training or not tune("dense_head", True):
+        if last_fwd is None or not training or not tune("dense_head", False):
             return None
         i, a, g = last_fwd
         hd = ex.plan.head
@@ -884,6 +887,7 @@ class BatchPlan(GeometryMixin):
                     wa.slab = grad + 4 * sp.offset
                     wa.opt = ex._optim_args(False, defer_pack=True)
                     wa.opt_w = sp.offset
+                    wa.opt_nograd = int(tune("opt_nograd", True))   # the update is the gradient's only reader
                     if ex.routes_ok:
                         wa.pk_fwd, wa.pk_NT = g.pack_fwd, g.NT
                         wa.pk_bwd, wa.pk_NTb = (g.pack_bwd, g.NTb) if g.KSb else (-1, 0)

@@ -255,6 +255,7 @@ def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
     vs = reps[0]["SGD"]["vs_single"]
     assert vs["p999"] < 1e-4 and vs["max"] < 2e-3 and vs["rel"] < 0.05, vs
     # Adam: a near-zero gradient element whose sign the reordering flips moves by up to a full
-    # lr (1e-3) per step: bound the tail by 2 lr and the worst element by 24 steps' worth
+    # lr (1e-3) per step, in either direction: bound the worst weight by 24 steps' worth and
+    # the whole difference by a tenth of the step
     vs = reps[0]["Adam"]["vs_single"]
-    assert vs["p999"] < 2e-3 and vs["max"] < 2.4e-2, vs
+    assert vs["max"] < 2.4e-2 and vs["rel"] < 0.1, vs
