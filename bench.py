@@ -183,6 +183,9 @@ def probe_data_planes(args, size, dev, g, B, chunk):
             if not ok:
                 res[plane + "_rejected"] = "weights differ across ranks or a wait timed out"
             del model, data
+        except Exception as e:        # noqa: BLE001 -- a plane that cannot run is not chosen
+            res[plane] = None
+            res[plane + "_rejected"] = ("%s: %s" % (type(e).__name__, e))[:200]
         finally:
             for k in env:
                 os.environ.pop(k, None)

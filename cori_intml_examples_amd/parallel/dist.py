@@ -79,7 +79,25 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
         tdist.init_process_group(backend=be, rank=rank, world_size=world, timeout=timeout)
         owns = True
         if mode == "native":
-            comm = C.NativeComm(rank, world, torch.device("cuda", torch.cuda.current_device()), timeout_s)
+            # collective fallback: if the RCCL communicator fails to come up on ANY rank, every
+            # rank runs the RCCL-free plane (the fused xGMI kernel over IPC-mapped peer memory,
+            # gloo control plane) instead of one rank raising while the others wait
+            why = None
+            try:
+                comm = C.NativeComm(rank, world, torch.device("cuda", torch.cuda.current_device()), timeout_s)
+            except Exception as e:    # noqa: BLE001 -- reported through the vote below
+                comm, why = None, "%s: %s" % (type(e).__name__, e)
+            votes = [None] * world
+            tdist.all_gather_object(votes, why)
+            bad = [(i, v) for i, v in enumerate(votes) if v]
+            if bad:
+                if comm is not None:
+                    comm.close()
+                comm, xgmi_only = None, True
+                if rank == 0:
+                    import sys
+                    print("[dp] RCCL communicator unavailable %s: RCCL-free xGMI data plane" % bad,
+                          file=sys.stderr, flush=True)
     else:
         be = backend or "none"
         if force and use_gpu:

@@ -104,3 +104,12 @@ def test_shard_indices_disjoint_cover_and_reshard():
     assert np.array_equal(shard_indices(n, 2, size, True, 7, 5).numpy(), shard_indices(n, 2, size, True, 7, 5).numpy())
     # unshuffled: the contiguous fixed-shard layout
     assert np.array_equal(shard_indices(10, 1, 3, False, 0, 0).numpy(), np.arange(3, 6))
+
+
+def test_rccl_init_failure_falls_back_collectively(tmp_path):
+    """A multi-GPU job whose RCCL communicator cannot come up (any rank) moves EVERY rank onto
+    the RCCL-free xGMI data plane through a gloo vote in dist.init (2 ranks, gloo, CPU)."""
+    r = _torchrun(2, [os.path.join(ROOT, "tests", "comm_fallback_worker.py"), str(tmp_path)], timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    reps = [json.load(open(tmp_path / ("fb%d.json" % i))) for i in range(2)]
+    assert all(rep["xgmi_only"] and not rep["comm"] and rep["size"] == 2 for rep in reps), reps
