@@ -103,8 +103,7 @@ struct ConvMMArgs {
   const bf16* zero = nullptr;
   int dbg = 0;   // ablation (timing only, wrong results): 1 skip staging, 2 skip MFMA, 4 skip stores,
                  // 8 skip the weight staging only; 16 = per-pixel unpool staging (A/B, exact);
-                 // 32 = weights and pooled halo staged in two phases; 64 = dgrad ReLU masks loaded
-                 // in the epilogue instead of before the k loop (A/B, exact)
+                 // 32 = weights and pooled halo staged in two phases (A/B, exact)
   unsigned long long* ts = nullptr;   // diagnostics: [grid block][8] phase stamps, wave 0 lane 0 (null = off)
   // conv_halo LDS layout: input-halo pixel stride in elements (0 = Cs_in; padded strides
   // break the fragment reads' bank conflicts, models/lds_layout.py)

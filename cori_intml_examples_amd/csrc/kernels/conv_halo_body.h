@@ -272,33 +272,6 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
     for (int t = 0; t < TM; ++t)
 #pragma unroll
       for (int nt = 0; nt < NTC; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // epilogue geometry (8-channel chunks this workgroup owns per pixel)
-    const int LDC = NTC * 16;
-    const int csh = (a.mode == 1 ? a.bt.pCs : a.Cs_out) - nt0 * 16;   // channels this WG owns
-    const int C = csh < LDC ? csh : LDC;
-    const int cch = C >> 3;                                            // 8-channel chunks
-    const FastDiv fcch(cch > 0 ? cch : 1);
-    // dgrad: the saved activations (ReLU masks) of this pass's first epilogue chunks are
-    // requested now -- their global round trip runs under the k loop instead of stalling the
-    // epilogue after it (dbg 64: loaded in the epilogue, A/B, exact)
-    constexpr int NPRE = 2;
-    bf16x8 pre[NPRE];
-    const bool premask = a.mode == 1 && a.bt.prev_relu && !(a.dbg & 64) && dbg_store;
-    if (premask) {
-      const int np = max(0, min(TM * 16, npix - tb * 16));
-#pragma unroll
-      for (int u = 0; u < NPRE; ++u) {
-        const int c = lane + 64 * u;
-        const bool ok = c < np * cch;
-        const int cc = ok ? c : 0;
-        const int pr = fcch.div(cc), c8 = cc - pr * cch;
-        const int p = tb * 16 + pr;
-        const int pyl = fwo.div(p);
-        const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (p - pyl * a.Wo);
-        const int n0 = nt0 * 16 + c8 * 8;
-        pre[u] = load_bf16x8_if(ok && n0 < a.bt.pCs, a.bt.prev_out + m * a.bt.pCs + n0, a.bt.prev_out);
-      }
-    }
     // Fast k loop (kpipe; 8-channel-aligned input with Cs % 32 == 0, the co-scheduled dgrad
     // of the RPV / MNIST stacks): a k-step's tap is wave-uniform (k = 32 ks + 8 g lies in
     // one tap), so its halo offset is scalar arithmetic -- no per-step table lookup, whose
@@ -396,6 +369,11 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
     // re-read them as 8-channel vectors so every global store is 16 bytes.  The forward
     // epilogue stages all TM tiles of the pass first (final bf16 values + pool codes), so
     // one copy loop writes TM*16 pixels / TM*4 windows with all lanes busy.
+    const int LDC = NTC * 16;
+    const int csh = (a.mode == 1 ? a.bt.pCs : a.Cs_out) - nt0 * 16;   // channels this WG owns
+    const int C = csh < LDC ? csh : LDC;
+    const int cch = C >> 3;                                            // 8-channel chunks
+    const FastDiv fcch(cch > 0 ? cch : 1);
     if (a.mode == 0 && a.pool) {
       bf16* epb = reinterpret_cast<bf16*>(ep);                // [TM*4 windows][LDC]
       uint8_t* epc = reinterpret_cast<uint8_t*>(epb + TM * 4 * LDC);
@@ -477,13 +455,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
           float v[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] = bf2f(val[k]);
-          const int u = (c - lane) >> 6;                      // this lane's chunk number
-          if (premask && u < NPRE) {
-            const bf16x8 pv = u == 0 ? pre[0] : pre[1];
-            bwd_through_store8(a.bt, m, nt0 * 16 + c8 * 8, v, step, &pv);
-          } else {
-            bwd_through_store8(a.bt, m, nt0 * 16 + c8 * 8, v, step);
-          }
+          bwd_through_store8(a.bt, m, nt0 * 16 + c8 * 8, v, step);
         }
       }
       __builtin_amdgcn_wave_barrier();
