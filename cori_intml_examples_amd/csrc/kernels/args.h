@@ -148,7 +148,6 @@ struct ConvStackArgs {
   int dbg = 0;   // ablation (timing only, wrong results): 1 no MFMA loop, 2 no epilogue, 4 no global stores, 8 no staging;
                  // 16 = generic layer path only (A/B of the row-aligned path; results exact)
                  // 32 = all weight packs staged before layer 0 (no LDS-DMA prefetch; A/B, exact)
-                 // 256 = the later layers' weight DMA issued after the staging barrier (A/B, exact)
   int splits = 1;                     // workgroups (row bands) per image
   // per layer, per band: conv-output rows [c0, c1) computed, stage-output rows [own0, own1)
   // stored, input halo image = input rows [ib, ib + ih)

@@ -560,6 +560,9 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     }
   }
 
+  STACK_STAMP(1);
+  __syncthreads();                  // image, layer-0 weights, biases and tables staged
+
   // The later layers' weight packs -> their LDS slots by LDS-DMA, issued AFTER that barrier
   // so they land during layer 0's tiles: the slots (contiguous, layer 1 first) are not read
   // by layer 0; an explicit vmcnt(0) before layer 0's closing barrier publishes them to
@@ -570,7 +573,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   // (the DMA source addresses stay live until that wait: overwriting the VGPRs of an
   // outstanding load's address made the compiler wait for it right away)
   const bf16* dma_src[PF];
-  auto issue_dma = [&]() {
+  if (prefetch) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int ntot = nv1 + nv2 + nv3;                 // multiples of 64 vectors per layer
     LDS char* wdst = (LDS char*)(wlds + A.L[1].w_lds);
@@ -585,17 +588,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       dma_src[j] = src;
       dma16_untracked(src, wdst + (size_t)vb * 16);
     }
-  };
-  // (dbg 256: the DMA issued after the staging barrier -- the old order, A/B, exact.)  By
-  // default each wave issues its DMA as soon as its own staging stores are done: the slots
-  // are not touched by the staging, and a wave that finished early issues while the slowest
-  // wave's image loads are still arriving
-  const bool dma_early = prefetch && !(A.dbg & 256);
-  if (dma_early) issue_dma();
-  STACK_STAMP(1);
-  __syncthreads();                  // image, layer-0 weights, biases and tables staged
-
-  if (prefetch && !dma_early) issue_dma();
+  }
   for (int l = 0; l < A.n; ++l) {
     const StackLayer L = A.L[l];      // by value: one batch of scalar loads per layer instead of
     const bool last = l + 1 == A.n;   // a kernarg reload of every field after each barrier

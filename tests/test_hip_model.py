@@ -623,24 +623,3 @@ def test_wgrad_late_ktab_bit_identical(kind, drop, cin, hw, monkeypatch):
         torch.cuda.synchronize()
         res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
     assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
-
-
-@pytest.mark.parametrize("kind,drop,cin,hw", [("rpv", 0.2, 3, 64), ("mnist", 0.3, 1, 28)])
-def test_stack_early_dma_bit_identical(kind, drop, cin, hw, monkeypatch):
-    """The conv stack issuing its later layers' weight LDS-DMA before the staging barrier
-    stages exactly what the after-barrier order (stack_dbg=256) does: whole training steps
-    bit-identical."""
-    res = []
-    for tv in ("stack_dbg=0", "stack_dbg=256"):
-        monkeypatch.setenv("INTML_TUNE", tv)
-        set_random_seed(55)
-        m = _build(kind, "cuda", opt="Adam", drop=drop, cin=cin, hw=hw)
-        x, y = _data(m, 256, seed=19)
-        ex = m._executor
-        d = ex.upload(x, y)
-        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(16)).to(ex.device)
-        ex.reset_metrics()
-        ex.train_steps(d, perm, 0, 128, 2)
-        torch.cuda.synchronize()
-        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
-    assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
