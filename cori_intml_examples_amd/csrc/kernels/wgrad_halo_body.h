@@ -55,36 +55,30 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   const int MTb = MT + (do_bias ? 1 : 0);          // pseudo m-tile MT = bias (ones operand)
 
   WH_STAMP(0);
-  // k column block -> halo offset table in LDS, then the per-wave m-tile descriptors
-  // (constant over blocks and k-steps).  The pipelined path builds it AFTER issuing its first
-  // block's staging loads (their latency then covers the table and its barrier; dbg 32: the
-  // table first, A/B, exact).
+  if (tid < 32) reinterpret_cast<uint32_t*>(zl)[tid] = 0u;
+  for (int c = tid; c < MT * 4; c += 256) {
+    const int k = (mt0 + c / 4) * 16 + 4 * (c & 3);
+    const int tap = k / Cs;
+    int e = -1;
+    if (tap < KHW && mt0 + c / 4 < a.Ktiles) {
+      const int ky = tap / a.KW;
+      e = (ky * XR + (tap - ky * a.KW)) * XP + (k - tap * Cs);
+    }
+    ktab[c] = e;
+  }
+  __syncthreads();
+  WH_STAMP(8);
+
+  // per-wave m-tile descriptors (constant over blocks and k-steps)
   int ko[MTW];
   bool tbias[MTW], tval[MTW];
-  auto build_ktab = [&]() {
-    if (tid < 32) reinterpret_cast<uint32_t*>(zl)[tid] = 0u;
-    for (int c = tid; c < MT * 4; c += 256) {
-      const int k = (mt0 + c / 4) * 16 + 4 * (c & 3);
-      const int tap = k / Cs;
-      int e = -1;
-      if (tap < KHW && mt0 + c / 4 < a.Ktiles) {
-        const int ky = tap / a.KW;
-        e = (ky * XR + (tap - ky * a.KW)) * XP + (k - tap * Cs);
-      }
-      ktab[c] = e;
-    }
-    __syncthreads();
-    WH_STAMP(8);
 #pragma unroll
-    for (int u = 0; u < MTW; ++u) {
-      const int mt = wave + 4 * u;
-      tval[u] = mt < MTb;
-      tbias[u] = mt == MT && do_bias;
-      ko[u] = (mt < MT) ? ktab[mt * 4 + (i & 3)] : -1;
-    }
-  };
-  const bool late_tab = PIPE && !(a.dbg & 32);
-  if (!late_tab) build_ktab();
+  for (int u = 0; u < MTW; ++u) {
+    const int mt = wave + 4 * u;
+    tval[u] = mt < MTb;
+    tbias[u] = mt == MT && do_bias;
+    ko[u] = (mt < MT) ? ktab[mt * 4 + (i & 3)] : -1;
+  }
   bf16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = f2bf(1.f);
@@ -354,7 +348,6 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
     };
     WH_STAMP(9);
     fetch(blk0);
-    if (late_tab) build_ktab();
     WH_STAMP(1);
     for (int blk = blk0; blk < blk1; ++blk) {
       const int b = blk / nrb, oy0 = (blk - b * nrb) * R;
@@ -369,7 +362,6 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       WH_STAMP(3 + 2 * (blk - blk0));
     }
   } else {
-    if (late_tab) build_ktab();
     for (int blk = blk0; blk < blk1; ++blk) {
       const int b = blk / nrb;
       const int oy0 = (blk - b * nrb) * R;
