@@ -245,7 +245,6 @@ struct DenseFwdArgs {
   // the iteration count as t + 1, see ConvStackArgs::step_inc)
   int book = 0;
   StepBeginArgs sb;
-  int dbg = 0;                   // A/B (exact): 1 = dX's ReLU masks loaded in its epilogue
 };
 
 // Split-K reduction + bias + activation + dropout -> bf16 [M][Ns]

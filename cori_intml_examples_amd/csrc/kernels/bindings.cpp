@@ -112,7 +112,7 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(DenseFwdArgs, x) RW(DenseFwdArgs, M) RW(DenseFwdArgs, Ks) PTR(DenseFwdArgs, wpk)
       RW(DenseFwdArgs, NT) RW(DenseFwdArgs, KS) RW(DenseFwdArgs, splits) RW(DenseFwdArgs, ks_per_split)
       PTR(DenseFwdArgs, part) RW(DenseFwdArgs, mode) PTR(DenseFwdArgs, st) RW(DenseFwdArgs, bt)
-      RW(DenseFwdArgs, book) RW(DenseFwdArgs, sb) RW(DenseFwdArgs, dbg);
+      RW(DenseFwdArgs, book) RW(DenseFwdArgs, sb);
 
   py::class_<DenseEpiArgs>(m, "DenseEpiArgs")
       .def(py::init<>())

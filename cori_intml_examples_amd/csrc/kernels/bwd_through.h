@@ -29,13 +29,12 @@ __device__ __forceinline__ void bwd_through_store(const BwdThrough& t, int b, in
 
 // Vectorised form: 8 consecutive channels [c0, c0+8) of output pixel qi (flat index over
 // the previous stage's output grid); one 16-byte load of the saved output, one 16-byte store.
-// (pre: that saved-output vector, loaded by the caller ahead of time)
 __device__ __forceinline__ void bwd_through_store8(const BwdThrough& t, size_t qi, int c0, const float* g,
-                                                   uint32_t step, const bf16x8* pre = nullptr) {
+                                                   uint32_t step) {
   if (c0 >= t.pCs) return;
   const size_t o = qi * t.pCs + c0;
   bf16x8 prev = zero_bf16x8();
-  if (t.prev_relu) prev = pre ? *pre : load_bf16x8(t.prev_out + o);
+  if (t.prev_relu) prev = load_bf16x8(t.prev_out + o);
   bf16x8 outv;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {

@@ -305,22 +305,6 @@ __device__ __forceinline__ void dense_dx_body(const DenseFwdArgs& a, const int b
   f32x4 acc[NTC];
 #pragma unroll
   for (int nt = 0; nt < NTC; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // the saved activation (ReLU mask) of this lane's first epilogue chunk, requested with the
-  // k loop's loads instead of after them: one memory round trip fewer in the epilogue's chain
-  // (dbg 1: loaded in the epilogue, A/B, exact)
-  const BwdThrough& t = a.bt;
-  const int width = t.pH * t.pW * t.pCs;
-  const int pix = t.pH * t.pW;
-  constexpr int C8 = NTC * 2;
-  const bool premask = t.prev_relu && !(a.dbg & 1);
-  bf16x8 pre = zero_bf16x8();
-  if (premask) {
-    const int e = lane, rr = e / C8, c8 = e - rr * C8;
-    const int m = mt * 16 + rr, n = nt0 * 16 + c8 * 8;
-    const bool ok = e < 16 * C8 && m < a.M && n < width;
-    const int px = ok ? n / t.pCs : 0;
-    pre = load_bf16x8_if(ok, t.prev_out + ((size_t)m * pix + px) * t.pCs + (n - px * t.pCs), t.prev_out);
-  }
   for (int kb = 0; kb < a.KS; kb += 4) {
     bf16x8 af[4], bfr[4][NTC];
 #pragma unroll
@@ -345,7 +329,11 @@ __device__ __forceinline__ void dense_dx_body(const DenseFwdArgs& a, const int b
 #pragma unroll
     for (int j = 0; j < 4; ++j) ep[(4 * g + j) * LDE + nt * 16 + r] = acc[nt][j];
   __builtin_amdgcn_wave_barrier();
+  const BwdThrough& t = a.bt;
   const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
+  const int width = t.pH * t.pW * t.pCs;
+  const int pix = t.pH * t.pW;
+  constexpr int C8 = NTC * 2;
   for (int e = lane; e < 16 * C8; e += 64) {
     const int rr = e / C8, c8 = e - rr * C8;
     const int m = mt * 16 + rr, n = nt0 * 16 + c8 * 8;
@@ -356,7 +344,7 @@ __device__ __forceinline__ void dense_dx_body(const DenseFwdArgs& a, const int b
 #pragma unroll
     for (int k = 0; k < 4; ++k) { v[k] = lo[k]; v[4 + k] = hi[k]; }
     const int px = n / t.pCs;
-    bwd_through_store8(t, (size_t)m * pix + px, n - px * t.pCs, v, step, (premask && e == lane) ? &pre : nullptr);
+    bwd_through_store8(t, (size_t)m * pix + px, n - px * t.pCs, v, step);
   }
 }
 

@@ -925,7 +925,6 @@ class BatchPlan(GeometryMixin):
                 a.mode = 1
                 a.st = st_ptr
                 a.bt = self._bt_for(g.src)
-                a.dbg = tune("dense_dbg", 0)            # A/B switches (DenseFwdArgs::dbg; exact)
                 dname = "dense_dx%d" % g.j
                 ntc = self._dense_dx_ntc(a) if (bwd2 and a.bt.pCs % 8 == 0 and a.Ks % 8 == 0
                                                and not K.dense_big(a.NT, a.KS)) else 0

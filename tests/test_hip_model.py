@@ -602,23 +602,3 @@ def test_dense_head_matches_split_launches(opt, lr, monkeypatch):
         assert float(torch.quantile(d[:1 << 20], 0.999)) < 2e-3 and float(d.max()) < 8e-3, float(d.max())
     for v1, v0 in zip(m1, m0):
         assert abs(v1 - v0) <= 1e-3 * max(1.0, abs(v0)), (m1, m0)
-
-
-@pytest.mark.parametrize("kind,drop,cin,hw", [("rpv", 0.2, 3, 64), ("mnist", 0.3, 1, 28)])
-def test_dense_dx_mask_prefetch_bit_identical(kind, drop, cin, hw, monkeypatch):
-    """The dense dX epilogue's ReLU masks requested with the k loop's loads compute exactly
-    what epilogue-time loads (dense_dbg=1) do: whole training steps bit-identical."""
-    res = []
-    for tv in ("dense_dbg=0", "dense_dbg=1"):
-        monkeypatch.setenv("INTML_TUNE", tv)
-        set_random_seed(56)
-        m = _build(kind, "cuda", opt="Adam", drop=drop, cin=cin, hw=hw)
-        x, y = _data(m, 256, seed=20)
-        ex = m._executor
-        d = ex.upload(x, y)
-        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(17)).to(ex.device)
-        ex.reset_metrics()
-        ex.train_steps(d, perm, 0, 128, 2)
-        torch.cuda.synchronize()
-        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
-    assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
