@@ -887,7 +887,10 @@ class BatchPlan(GeometryMixin):
                     wa.slab = grad + 4 * sp.offset
                     wa.opt = ex._optim_args(False, defer_pack=True)
                     wa.opt_w = sp.offset
-                    wa.opt_nograd = int(tune("opt_nograd", True))   # the update is the gradient's only reader
+                    # opt_nograd=1: skip storing the gradient the update consumed (legacy 1.231 ->
+                    # 1.218 ms/step, profiles/r4g_ab_legacy.txt) -- opt-in: the layer's gradient
+                    # is then not readable through the store (store.view(..., grad=True))
+                    wa.opt_nograd = int(tune("opt_nograd", False))
                     if ex.routes_ok:
                         wa.pk_fwd, wa.pk_NT = g.pack_fwd, g.NT
                         wa.pk_bwd, wa.pk_NTb = (g.pack_bwd, g.NTb) if g.KSb else (-1, 0)
