@@ -112,11 +112,11 @@ def test_inline_hpo_record_on_cpu(monkeypatch):
         recs = h.run()
     finally:
         h.stop()
-    assert h.engines == 3               # max(engines_per_gpu, concurrent RPV trials) per GPU
+    assert h.engines == 2 and h.rpv_engines == 3   # the search's farm; the RPV record's own farm
     rec = recs["hpo"]
     assert rec["trials_done"] == 3 and not rec["capped"], rec
     assert rec["trials_per_hour"] > 0 and rec["wall_s"] >= rec["startup_s"] > 0
-    assert rec["epochs"] == 1 and rec["samples"] == 600 and rec["engines_per_gpu"] == 3   # all engines search
+    assert rec["epochs"] == 1 and rec["samples"] == 600 and rec["engines_per_gpu"] == 2
     assert rec["label_noise"] == 0.1
     rr = recs["hpo_rpv"]
     assert rr["trials_done"] == 3 and not rr["capped"] and rr["concurrent"] == 3, rr
