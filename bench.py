@@ -316,7 +316,7 @@ class InlineHpo:
         cloudpickle.register_pickle_by_value(hpo_throughput)
         t1 = time.time()
         g = max(1, self.n_gpu)
-        view = c.load_balanced_view(targets=list(range(self.epg * g)))
+        view = c.load_balanced_view()           # the search's own farm: every engine
         trials = rs.mnist_trials(self.TRIALS)
         ars = rs.submit_trials(view, hpo_throughput.trial_mnist, trials, n_train=self.SAMPLES,
                                batch_size=self.BATCH, n_epochs=self.EPOCHS, valid_frac=self.VALID_FRAC)
@@ -354,7 +354,7 @@ class InlineHpo:
         params = {k: [t[k] for t in trials] for k in ("conv_sizes", "fc_sizes", "dropout", "optimizer", "lr")}
         fn = functools.partial(hpo_throughput.trial_rpv_widget, n_train=self.RPV_TRAIN, n_valid=self.RPV_VALID,
                                batch_size=self.RPV_BATCH, n_epochs=self.RPV_EPOCHS)
-        ctl = ModelController(client=c, view=c.load_balanced_view(targets=list(range(self.RPV_TRIALS))))
+        ctl = ModelController(client=c, view=c.load_balanced_view())   # its own farm: 8 engines
         psm = ParamSpanModel(fn, params, controller=ctl)
         seen = {}                                           # (row, epoch) -> first time on the dashboard
 

@@ -216,6 +216,7 @@ class LoadBalancedView(_View):
     def __init__(self, client, targets=None):
         super().__init__(client)
         self.targets = targets
+        self._next = 0                 # round-robin position over an explicit target list
 
     def _target_for(self, i):
         if self.targets is None:
@@ -224,8 +225,13 @@ class LoadBalancedView(_View):
         return t[i % len(t)]
 
     def _submit_apply(self, f, args, kwargs):
-        mid = self.client._submit(self._target_for(0) if self.targets is not None else None, "apply",
-                                  (f, tuple(args), dict(kwargs)))
+        # no targets: the controller's shared queue (whichever engine is idle first); an
+        # explicit target list: round-robin over it (the controller queues per engine)
+        target = None
+        if self.targets is not None:
+            target = self._target_for(self._next)
+            self._next += 1
+        mid = self.client._submit(target, "apply", (f, tuple(args), dict(kwargs)))
         return AsyncResult(self.client, [mid], single=True)
 
     def __repr__(self):

@@ -55,6 +55,19 @@ def test_ids_and_load_balanced(cluster):
     assert lv.map_sync(_square, [1, 2, 3]) == [1, 4, 9]
 
 
+def test_load_balanced_over_target_list(cluster):
+    """A view restricted to an explicit target list spreads its tasks over every listed
+    engine (it once sent all of them to the first one, serialising a whole search)."""
+    _, c = cluster
+    lv = c.load_balanced_view(targets=[0, 1])
+    ars = [lv.apply(_square, i, 0.2) for i in range(4)]
+    assert [a.get(30) for a in ars] == [i * i for i in range(4)]
+    assert sorted(a.engine_id for a in ars) == [0, 0, 1, 1]
+    one = c.load_balanced_view(targets=[1])
+    ars = [one.apply(_square, i) for i in range(3)]
+    assert [a.get(30) for a in ars] == [0, 1, 4] and {a.engine_id for a in ars} == {1}
+
+
 _SHIPPED_GLOBAL = {}
 
 
