@@ -192,8 +192,7 @@ struct WgradArgs {
   // when it applies: 8 n-tiles per workgroup, unpooled dY)
   const bf16* zero = nullptr;
   int dbg = 0;   // ablation (timing only): 1 skip staging, 2 skip MFMA, 4 skip slab stores;
-                 // 16 = per-pixel unpool staging of pooled dY; 64 = no 3-m-tile dual instance
-                 // (A/B, exact)
+                 // 16 = per-pixel unpool staging of pooled dY (A/B, exact)
   unsigned long long* ts = nullptr;   // diagnostics: per-workgroup [start, end] wall clock (null = off)
   unsigned long long* ts2 = nullptr;  // diagnostics: per-workgroup [16] phase stamps (null = off)
   // dense_wgrad with ONE split and the identity layout (slab == the Keras gradient): when

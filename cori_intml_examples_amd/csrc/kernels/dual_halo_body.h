@@ -59,11 +59,7 @@ static bool dual_w(const ConvMMArgs& ca, const WgradArgs& wa, int MT, int NTT, i
     dual_t<NTC, M_, N_, TMD>(ca, wa, MT, wg, cgx, cgy, lds, x, s);            \
     return true;                                                           \
   }
-  C(1, 1) C(2, 1) C(4, 1) C(1, 2) C(2, 2) C(4, 2) C(1, 4) C(2, 4)
-  // three m-tiles per wave with four n-tiles (the RPV conv2 wgrad: 9 k-tiles + bias): 48
-  // accumulator VGPRs instead of the 4-tile form's 64 (wa.dbg 64: the 4-tile form, A/B)
-  if (!(wa.dbg & 64)) { C(3, 4) }
-  C(4, 4) C(1, 8) C(2, 8)
+  C(1, 1) C(2, 1) C(4, 1) C(1, 2) C(2, 2) C(4, 2) C(1, 4) C(2, 4) C(4, 4) C(1, 8) C(2, 8)
 #undef C
   return false;
 }

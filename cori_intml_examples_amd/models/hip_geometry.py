@@ -356,7 +356,6 @@ class GeometryMixin:
                 break
         # LDS layout from the bank-conflict model (pixel / row strides of the X halo, dY rows)
         a.kperm = int(tune("wgrad_perm", True)) | (0 if tune("wgrad_fast", True) else 2)
-        a.dbg = tune("wgrad_dbg", 0)            # A/B switches (WgradArgs::dbg; exact ones only)
         if tune("lds_layout", True):
             a.xpix, a.xrow, a.dyld = lds_layout.wgrad_layout(g.Cs_in, W_in, g.Wo, NTT, g.KH, g.KW, g.stride,
                                                              a.Ktiles, bool(a.kperm & 1))
