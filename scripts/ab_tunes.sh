@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of INTML_TUNE variants on the 1-GPU bench (no HPO): interleaved rounds,
-#   bash scripts/ab_tunes.sh "" "tail_reduce=0" "head_generic=1"      (ROUNDS, STEPS, BENCH_ARGS)
+#   bash scripts/ab_tunes.sh "" "wt=0" "head_generic=1"      (ROUNDS, STEPS, BENCH_ARGS)
 cd $GRAFT_REPO_ROOT
 for i in $(seq 1 ${ROUNDS:-3}); do
   for v in "$@"; do
