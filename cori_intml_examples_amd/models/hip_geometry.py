@@ -336,10 +336,11 @@ class GeometryMixin:
         mt_cap = (8 if NTT == 8 else 16) - (1 if bias else 0)
         MT = max(1, min(a.Ktiles, mt_cap))
         MT = cdiv(a.Ktiles, cdiv(a.Ktiles, MT))        # balance the m-groups
-        # rows per block: ~256 pixels, at most 8 rows (measured best at batch 128 for the
-        # RPV and MNIST stacks), bounded LDS
+        # rows per block: ~256 pixels (the first layer, a standalone launch: ~512), at most 8
+        # rows (measured best at batch 128 for the RPV and MNIST stacks; RPV first layer
+        # 512 px = 8 rows: +0.2-0.5 %, profiles/r4m_ab_rpv.txt, r4n_ab_rpv.txt), bounded LDS
         W_in = (g.Wo - 1) * g.stride + g.KW
-        px = tune("wgrad_block_px%d" % g.i, tune("wgrad_block_px", 256))
+        px = tune("wgrad_block_px%d" % g.i, tune("wgrad_block_px", 512 if g.i == 0 else 256))
         R = max(1, min(g.Ho, px // max(1, g.Wo), tune("wgrad_max_rows%d" % g.i, tune("wgrad_max_rows", 8))))
         # prefer the largest R whose block staging fits the kernel's register pipeline
         # (<= 4 X-halo and 4 dY chunks per thread, wgrad_halo_body.h WH_PX / WH_PY)
