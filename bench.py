@@ -436,8 +436,9 @@ def main():
     ap.add_argument("--samples", type=int, default=32768, help="resident synthetic samples per rank")
     ap.add_argument("--model", default="rpv", choices=["rpv", "mnist", "rpv_legacy"])
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--steps-per-graph", type=int, default=int(os.environ.get("INTML_STEPS_PER_GRAPH", 8)),
-                    help="full training steps per HIP-graph replay (the fit() loop's default)")
+    ap.add_argument("--steps-per-graph", type=int, default=int(os.environ.get("INTML_STEPS_PER_GRAPH", 32)),
+                    help="full training steps per HIP-graph replay (32: +0.7 %% over 8, profiles/r4q_spg.txt; "
+                         "fit() replays INTML_STEPS_PER_GRAPH, default 8, between its callbacks)")
     ap.add_argument("--no-dp-delta", action="store_true",
                     help="skip the DP-off re-run that measures the exposed communication time")
     ap.add_argument("--via-fit", action="store_true", help="time apps.rpv.train_model epochs (Keras fit path)")

@@ -464,7 +464,9 @@ class GeometryMixin:
         >= tune dx_min_wgs workgroups (4 waves x 16 rows each)."""
         if tune("dx_ntc", 0):
             return tune("dx_ntc", 0)
-        want = tune("dx_min_wgs", 512)
+        # (256: the RPV dense dX at 2 n-tiles per wave, 256 workgroups -- 3 us faster than
+        # 512 one-tile workgroups, profiles/r4p_ab_rpv.txt)
+        want = tune("dx_min_wgs", 256)
         for ntc in (4, 2):
             if cdiv(a.M, 64) * cdiv(a.NT, ntc) >= want:
                 return ntc

@@ -569,6 +569,27 @@ def test_dgrad_onebatch_prologue_bit_identical(kind, drop, cin, hw, monkeypatch)
     assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
 
 
+def test_dense_dx_tiles_agree(monkeypatch):
+    """The dense layer's dX at 1, 2 and 4 n-tiles per wave (dense_bwd_pair / dense_dx: the
+    tile only changes which wave computes an output, not its k order) trains the same: SGD
+    weights after 2 steps agree to fp32 reordering level."""
+    res = []
+    for tv in ("dx_ntc=1", "dx_ntc=2", "dx_ntc=4"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(53)
+        m = _build("rpv_bench", "cuda", opt="SGD", drop=0.0, cin=3, hw=64)
+        x, y = _data(m, 256, seed=17)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(14)).to(ex.device)
+        ex.reset_metrics()
+        ex.train_steps(d, perm, 0, 128, 2)
+        torch.cuda.synchronize()
+        res.append(m.store.master[:m.store.numel].clone())
+    for r in res[1:]:
+        assert (r - res[0]).abs().max().item() < 1e-5
+
+
 @pytest.mark.parametrize("opt,lr", [("SGD", 0.05), ("Adam", 1e-3)])
 def test_dense_head_matches_split_launches(opt, lr, monkeypatch):
     """The fused dense layer + binary head launch (dense_head.hip: 16-wave K-slice tiles, the
