@@ -441,7 +441,7 @@ class GeometryMixin:
         NT = cdiv(N, 16)
         a.NT = NT
         a.P = bs
-        ntt = _pow2_le(NT, 8)
+        ntt = _pow2_le(NT, min(8, tune("dw_ntt", 8)))
         kg = 2
         groups = cdiv(a.Ktiles, kg) * cdiv(NT, ntt)
         per_split_bytes = a.Ktiles * 16 * NT * 16 * 4
