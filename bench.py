@@ -94,10 +94,18 @@ def synthetic(n, shape, ncls, ex, dev, g):
     return synth.synth_device("rpv" if ncls == 1 else "mnist", n, shape, ncls, ex.in_Cs, seed, dev)
 
 
-def time_steps(model, data, B, steps, warmup, chunk, g, dev):
+def time_steps(model, data, B, steps, warmup, chunk, g, dev, settle_ms=0.0, info=None):
     """Warmup (captures every graph the timed loop replays), then time `steps` full training
     steps as graph replays of `chunk` steps.  Returns (elapsed seconds on this rank, per-step
-    ms of each replay from HIP events)."""
+    ms of each replay from HIP events).
+
+    settle_ms > 0: before the timed region, replay the timed graph back to back (no host sync
+    between replays) until the GPU has run it for ~settle_ms.  The chip's power management
+    holds a lower clock until it has been under sustained load for ~10-15 ms; the driver's
+    short command (--steps 20 --warmup 5: ~3 ms of work before its timed region) otherwise
+    times the ramp, not the step -- every kernel of the step runs 3-5 % slower in it and an
+    idle gap of 200 ms puts it back (profiles/r5_driver_gap.txt).  The settle steps are
+    reported on the JSON line (``settle_steps`` / ``settle_ms``), never folded into ``warmup``."""
     import torch
     from cori_intml_examples_amd.parallel import hvd
     ex = model._executor
@@ -118,6 +126,21 @@ def time_steps(model, data, B, steps, warmup, chunk, g, dev):
     timed = chunks(steps)
     for k in chunks(warmup) + sorted(set(timed)):
         run(k)
+    if settle_ms > 0 and timed:
+        k = max(timed)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        run(k)
+        e1.record()
+        torch.cuda.synchronize()
+        reps = max(1, int(-(-settle_ms // max(e0.elapsed_time(e1), 1e-3))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run(k)
+        torch.cuda.synchronize()
+        if info is not None:
+            info["settle_steps"] = (reps + 1) * k
+            info["settle_ms"] = round((time.perf_counter() - t0) * 1e3 + e0.elapsed_time(e1), 2)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(timed) + 1)]
     hvd.barrier()
     torch.cuda.synchronize()
@@ -169,7 +192,8 @@ def probe_data_planes(args, size, dev, g, B, chunk):
             model, shape, ncls, *_ = build(args, size, True, dev)
             hvd.broadcast_global_variables(0, model=model)
             data = synthetic(max(args.samples, B * 4), shape, ncls, model._executor, dev, g)
-            e, _ = time_steps(model, data, B, probe, min(args.warmup, 16), chunk, g, dev)
+            e, _ = time_steps(model, data, B, probe, min(args.warmup, 16), chunk, g, dev,
+                              settle_ms=min(getattr(args, "settle_ms", 0.0), 20.0))
             # the reducer sets the xGMI plane up at its first step (collective self-test + vote)
             x = getattr(model._executor.reducer, "xgmi", None)
             on = plane not in ("xgmi", "hybrid") or x is not None
@@ -439,6 +463,10 @@ def main():
     ap.add_argument("--steps-per-graph", type=int, default=int(os.environ.get("INTML_STEPS_PER_GRAPH", 32)),
                     help="full training steps per HIP-graph replay (32: +0.7 %% over 8, profiles/r4q_spg.txt; "
                          "fit() replays INTML_STEPS_PER_GRAPH, default 8, between its callbacks)")
+    ap.add_argument("--settle-ms", type=float, default=60.0,
+                    help="before the timed steps, replay the timed graph back to back for ~this long so the "
+                         "GPU clock has left its power-management ramp (reported as settle_steps / settle_ms; "
+                         "0 = off; profiles/r5_driver_gap.txt)")
     ap.add_argument("--no-dp-delta", action="store_true",
                     help="skip the DP-off re-run that measures the exposed communication time")
     ap.add_argument("--via-fit", action="store_true", help="time apps.rpv.train_model epochs (Keras fit path)")
@@ -495,7 +523,9 @@ def main():
     else:
         data = synthetic(max(args.samples, B * 4), shape, ncls, ex, dev, g)
         hvd.broadcast_global_variables(0, model=model)
-        elapsed, per_step = time_steps(model, data, B, args.steps, args.warmup, chunk, g, dev)
+        settle = {}
+        elapsed, per_step = time_steps(model, data, B, args.steps, args.warmup, chunk, g, dev,
+                                       settle_ms=args.settle_ms, info=settle)
         steps = args.steps
         warmup_note = args.warmup
     loss = ex.read_metrics()[0]
@@ -535,7 +565,7 @@ def main():
             # the same step without the data-parallel machinery, same N, right after
             ref, *_ = build(args, size, False, dev)
             data2 = synthetic(max(args.samples, B * 4), shape, ncls, ref._executor, dev, g)
-            e2, _ = time_steps(ref, data2, B, args.steps, args.warmup, chunk, g, dev)
+            e2, _ = time_steps(ref, data2, B, args.steps, args.warmup, chunk, g, dev, settle_ms=args.settle_ms)
             if size > 1:
                 e2 = max(hvd.allgather(e2))
             selfcheck["nodp_ms_per_step"] = round(e2 / args.steps * 1e3, 4)
@@ -549,7 +579,8 @@ def main():
                     alt, *_ = build(args, size, True, dev)
                     hvd.broadcast_global_variables(0, model=alt)
                     data3 = synthetic(max(args.samples, B * 4), shape, ncls, alt._executor, dev, g)
-                    e3, _ = time_steps(alt, data3, B, args.steps, args.warmup, chunk, g, dev)
+                    e3, _ = time_steps(alt, data3, B, args.steps, args.warmup, chunk, g, dev,
+                                       settle_ms=args.settle_ms)
                 finally:
                     if old is None:
                         os.environ.pop("INTML_XGMI", None)
@@ -583,6 +614,11 @@ def main():
                           "path": "fit" if args.via_fit else "train_steps",
                           "step_ms_p50": round(stats["p50"], 4), "step_ms_max": round(stats["max"], 4),
                           "train_loss": round(loss, 5)}}
+        if not args.via_fit:
+            # untimed back-to-back replays of the timed graph after the warmup (clock settle,
+            # see time_steps) -- reported, not counted as warmup
+            out["settle_steps"] = settle.get("settle_steps", 0)
+            out["settle_ms"] = settle.get("settle_ms", 0.0)
         if args.via_fit:
             out["data"] = "synthetic (host numpy uploaded by fit(), random-init weights)"
             out["config"]["lr_warmup_epochs"] = args.lr_warmup_epochs

@@ -60,7 +60,7 @@ def main(argv=None):
     st = hvd.init(shard_data=args.shard)
     print("[train_rpv] rank %d/%d (local %d) on %s, data plane %s" % (
         hvd.rank(), hvd.size(), hvd.local_rank(), socket.gethostname(),
-        "rccl" if st.comm is not None else st.backend))
+        st.plane or ("rccl" if st.comm is not None else st.backend)))
     if args.seed is not None:
         set_random_seed(args.seed + hvd.rank())
 
@@ -87,6 +87,8 @@ def main(argv=None):
     history = train_model(model, train_input=train_input, train_labels=train_labels, valid_input=valid_input,
                           valid_labels=valid_labels, batch_size=args.batch_size, n_epochs=args.n_epochs,
                           verbose=args.verbose, use_horovod=True)
+    if hvd.rank() == 0 and getattr(history, "data_plane", None):
+        print("[train_rpv] gradient reducer %s" % history.data_plane)
     if args.fom in ("best", "last"):
         from ..hpo.evaluator import figure_of_merit
         print("FoM:", figure_of_merit(history.history["val_loss"], args.fom))

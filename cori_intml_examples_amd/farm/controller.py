@@ -89,6 +89,11 @@ class Controller:
                     "LOCAL_WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(self.dp_port),
                     "INTML_FARM_ENGINE": str(eid), "INTML_FARM_CLUSTER": self.info["cluster_id"]})
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if self.gpus is not None and len(set(self.gpus[e % len(self.gpus)] for e in range(self.n))) < self.n:
+            # engines share a GPU: RCCL refuses two ranks on one device, so a %%px data-parallel
+            # job over these engines runs the RCCL-free xGMI plane -- on EVERY engine (every rank
+            # must pick the same plane)
+            env.setdefault("INTML_COMM", "xgmi")
         return env
 
     def _spawn(self, eid: int):

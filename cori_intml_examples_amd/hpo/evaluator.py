@@ -13,8 +13,9 @@ on 127.0.0.1:<own port>) -- nested HPO x DP.  Slots run con
 ``slots`` gives the slot list explicitly instead (one list of GPU ids per slot).  A slot
 that names one GPU more than once runs that many ranks on it (oversubscription: a 1-GPU
 box can still run a 2-rank nested evaluation); RCCL needs distinct devices per rank, so
-such a slot's ranks exchange gradients over gloo (``INTML_DP_BACKEND=gloo``) while the
-compute stays on the GPU.  ``slots_per_gpu`` > 1 repeats every slot that many times
+such a slot's ranks select the RCCL-free xGMI data plane on their own (``dist.init``: more
+local ranks than visible GPUs) -- the same fused all-reduce + optimizer kernel over
+IPC-mapped peer memory that a multi-GPU job uses, captured into the step graph.  ``slots_per_gpu`` > 1 repeats every slot that many times
 (several small evaluations share a GPU concurrently, as the farm's engines-per-GPU do).
 
 An evaluation whose command fails or prints no ``FoM:`` line scores ``inf`` (worst);
@@ -173,8 +174,8 @@ class Evaluator:
         if slot is not None:
             uniq = list(dict.fromkeys(slot))
             env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in uniq)
-            if len(uniq) < len(slot):      # ranks share a GPU (LOCAL_RANK % visible devices)
-                env.setdefault("INTML_DP_BACKEND", "gloo")
+            # (ranks sharing a GPU -- LOCAL_RANK % visible devices -- take the RCCL-free xGMI
+            # plane: dist.init sees more local ranks than devices)
         else:
             env.setdefault("INTML_DEVICE", "cpu")
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

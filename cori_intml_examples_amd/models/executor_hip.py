@@ -1041,7 +1041,7 @@ class BatchPlan(GeometryMixin):
             # single stream, no all-reduce to overlap: ONE reduction launch at the end of the
             # backward (each launch boundary costs ~5 us here), if the descriptors fit a table
             ndesc = sum(len(d) for _, _, d in self.red_groups)
-            one = ndesc <= 16
+            one = ndesc <= tune("red_desc_max", 16)       # (RedTable capacity, MAX_RED)
             limit = 1 << 62 if one else int(os.environ.get("INTML_BUCKET_BYTES", 1 << 20))
             # ... with the optimizer fused into it when its table covers every parameter
             covered = sum(d[5] for _, _, ds in self.red_groups for d in ds)
@@ -1049,9 +1049,12 @@ class BatchPlan(GeometryMixin):
             self.optim_fused = one and covered == ex.store.numel and tune("fuse_optim", True)
             if not self.optim_fused:
                 # the step ends with a full optimizer launch after all: the dense layers keep
-                # writing their gradient in place, but leave the update to it
+                # writing their gradient in place, but leave the update -- and the bf16 pack
+                # writes that go with it -- to it, so they also store the gradient it reads
                 for wa, _ in self.dense_fused_opt:
                     wa.opt_w, wa.opt_b = -1, -1
+                    wa.pk_fwd, wa.pk_bwd = -1, -1
+                    wa.opt_nograd = 0
                 self.dense_fused_opt = []
             early = self._early_groups() if self.optim_fused else []
             bucket_groups, cur, nb = [], [], 0

@@ -14,6 +14,7 @@ all-reduce (rpv.py:65), ``BroadcastGlobalVariablesCallback`` (rpv.py:85),
 from __future__ import annotations
 
 import os
+import time
 from typing import Optional
 
 import torch
@@ -148,6 +149,136 @@ class NativeComm:
         if self._c is not None:
             self._c.stop_watchdog()
             self._c = None
+
+    # ------------------------------------------------------------------ admission
+    def self_test(self, timeout_s: float = 60.0) -> Optional[str]:
+        """Closed-form numeric all-reduce, eager AND captured into a HIP graph (the way the
+        training step issues it): rank r contributes (r + 1) * (i % 13 + 1), so every element
+        of the sum is the exact integer size (size + 1) / 2 * (i % 13 + 1) in fp32.  Bounded
+        in time: a collective that does not complete within ``timeout_s`` aborts the
+        communicator.  Returns None on success, else what went wrong (for the init vote)."""
+        dev = self.device
+        n = 4099                                   # odd: not a multiple of any RCCL chunking
+        base = (torch.arange(n, device=dev, dtype=torch.float32) % 13) + 1
+        want = base * (self.size * (self.size + 1) / 2)
+        mine = base * (self.rank + 1)
+
+        def wait(what: str) -> Optional[str]:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            deadline = time.monotonic() + timeout_s
+            while not ev.query():
+                if time.monotonic() > deadline:
+                    self.abort("self-test %s did not complete within %.0f s" % (what, timeout_s))
+                    return "%s all-reduce timed out after %.0f s" % (what, timeout_s)
+                time.sleep(1e-3)
+            return None
+
+        try:
+            with torch.cuda.device(dev):
+                t = mine.clone()
+                self.all_reduce(t)
+                err = wait("eager")
+                if err:
+                    return err
+                if not torch.equal(t, want):
+                    return "eager all-reduce wrong: max |err| %.3g" % float((t - want).abs().max())
+                t2 = torch.zeros_like(mine)
+                s = torch.cuda.Stream(device=dev)
+                s.wait_stream(torch.cuda.current_stream(dev))
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    self.all_reduce(t2, stream=s)
+                t2.copy_(mine)
+                g.replay()
+                err = wait("captured")
+                if err:
+                    return err
+                if not torch.equal(t2, want):
+                    return "captured all-reduce wrong: max |err| %.3g" % float((t2 - want).abs().max())
+                del g
+        except Exception as e:   # noqa: BLE001 -- reported through the vote
+            return "%s: %s" % (type(e).__name__, e)
+        return None
+
+
+def establish(rank: int, size: int, device: torch.device, timeout_s: float = 600.0,
+              init_timeout_s: Optional[float] = None, factory=None):
+    """Bring up the RCCL data plane for a job of ``size`` ranks, with the SAME outcome on every
+    rank: returns ``(comm, None)`` or ``(None, [(rank, why), ...])``, in which case every rank
+    runs the RCCL-free xGMI plane.  Each phase ends in a collective step of the gloo control
+    plane, so an asymmetric failure -- one rank's only -- still reaches every rank:
+
+      1. rank 0 creates the unique id (or reports why it could not) and broadcasts THAT, so a
+         rank-0 failure does not leave the others inside a broadcast that never matches;
+      2. every rank builds its communicator in a worker thread with a deadline
+         (``INTML_RCCL_INIT_TIMEOUT``, default 120 s): a rank that never joins (it failed
+         before ``ncclCommInitRank``) leaves its peers blocked inside RCCL, but their main
+         threads give up waiting and go on to the vote (the blocked thread is abandoned);
+      3. the numeric self-test (``NativeComm.self_test``: eager + graph-captured, closed-form);
+      4. ONE all_gather of every rank's verdict; any failure anywhere -> every rank aborts its
+         communicator and falls back.
+
+    ``factory(rank, size, device, timeout_s, uid)`` builds a communicator (tests inject
+    failing ones)."""
+    import threading
+
+    import torch.distributed as tdist
+    factory = factory or (lambda r, n, d, t, u: NativeComm(r, n, d, t, uid=u))
+    if init_timeout_s is None:
+        init_timeout_s = float(os.environ.get("INTML_RCCL_INIT_TIMEOUT", 120))
+    why = None
+    # phase 1: the unique id, or rank 0's reason for not having one
+    box = [None]
+    if rank == 0:
+        try:
+            box = [("ok", _module().unique_id())]
+        except Exception as e:   # noqa: BLE001
+            box = [("err", "unique id: %s: %s" % (type(e).__name__, e))]
+    if size > 1:
+        tdist.broadcast_object_list(box, src=0)
+    kind, val = box[0]
+    comm = None
+    if kind != "ok":
+        why = val if rank == 0 else None
+    else:
+        # phase 2: communicator construction with a deadline
+        res = {}
+
+        def work():
+            try:
+                if device.type == "cuda":
+                    torch.cuda.set_device(device)
+                res["comm"] = factory(rank, size, device, timeout_s, val)
+            except BaseException as e:   # noqa: BLE001
+                res["err"] = "%s: %s" % (type(e).__name__, e)
+
+        th = threading.Thread(target=work, name="rccl-init", daemon=True)
+        th.start()
+        th.join(init_timeout_s)
+        if th.is_alive():
+            why = "communicator not up within %.0f s (a peer never joined)" % init_timeout_s
+        elif "err" in res:
+            why = res["err"]
+        else:
+            comm = res["comm"]
+            # phase 3: numeric self-test, eager and captured
+            why = comm.self_test(min(timeout_s, 60.0))
+    # phase 4: one vote
+    votes = [why]
+    if size > 1:
+        votes = [None] * size
+        tdist.all_gather_object(votes, why)
+    bad = [(i, v) for i, v in enumerate(votes) if v]
+    if bad:
+        if comm is not None:
+            try:
+                comm.abort("data-plane vote failed: %s" % bad)
+            except Exception:   # noqa: BLE001
+                pass
+            comm.close()
+        return None, bad
+    return comm, None
 
 
 def comm_mode(use_gpu: bool, backend: Optional[str], local_size: Optional[int] = None,

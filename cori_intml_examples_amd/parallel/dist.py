@@ -59,9 +59,11 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
     use_gpu = torch.cuda.is_available() and os.environ.get("INTML_DEVICE", "cuda").startswith("cuda")
     timeout_s = float(os.environ.get("INTML_DP_TIMEOUT", 600))
     owns, comm, xgmi_only = False, None, False
+    plane_note = None
     if tdist.is_available() and tdist.is_initialized():
         world, rank = tdist.get_world_size(), tdist.get_rank()
         be = tdist.get_backend()
+        plane_note = "torch.distributed %s (process group created by the caller)" % be
     elif world > 1:
         from . import comm as C
         mode = C.comm_mode(use_gpu, backend, local_size, torch.cuda.device_count() if use_gpu else 0)
@@ -79,25 +81,23 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
         tdist.init_process_group(backend=be, rank=rank, world_size=world, timeout=timeout)
         owns = True
         if mode == "native":
-            # collective fallback: if the RCCL communicator fails to come up on ANY rank, every
-            # rank runs the RCCL-free plane (the fused xGMI kernel over IPC-mapped peer memory,
-            # gloo control plane) instead of one rank raising while the others wait
-            why = None
-            try:
-                comm = C.NativeComm(rank, world, torch.device("cuda", torch.cuda.current_device()), timeout_s)
-            except Exception as e:    # noqa: BLE001 -- reported through the vote below
-                comm, why = None, "%s: %s" % (type(e).__name__, e)
-            votes = [None] * world
-            tdist.all_gather_object(votes, why)
-            bad = [(i, v) for i, v in enumerate(votes) if v]
+            # collective fallback: if the RCCL communicator fails to come up -- or fails its
+            # closed-form numeric self-test, eager or graph-captured -- on ANY rank, every rank
+            # runs the RCCL-free plane (the fused xGMI kernel over IPC-mapped peer memory, gloo
+            # control plane) instead of one rank raising while the others wait
+            # (comm.establish: phased, every phase ends in a control-plane collective)
+            dev = torch.device("cuda", torch.cuda.current_device()) if use_gpu else torch.device("cpu")
+            comm, bad = C.establish(rank, world, dev, timeout_s)
             if bad:
-                if comm is not None:
-                    comm.close()
-                comm, xgmi_only = None, True
-                if rank == 0:
-                    import sys
-                    print("[dp] RCCL communicator unavailable %s: RCCL-free xGMI data plane" % bad,
-                          file=sys.stderr, flush=True)
+                xgmi_only = True
+                plane_note = "xgmi (RCCL unavailable: %s)" % "; ".join("rank %d: %s" % b for b in bad)[:400]
+            else:
+                plane_note = "rccl (communicator up on %d ranks, numeric self-test passed eager + captured)" % world
+        elif mode == "xgmi":
+            plane_note = "xgmi (RCCL-free: %s)" % ("INTML_COMM=xgmi" if os.environ.get("INTML_COMM", "").lower()
+                                                   == "xgmi" else "ranks share a GPU")
+        else:
+            plane_note = "torch.distributed %s" % be
     else:
         be = backend or "none"
         if force and use_gpu:
@@ -105,10 +105,14 @@ def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
             if C.comm_mode(use_gpu, backend) == "native":
                 comm = C.NativeComm(0, 1, torch.device("cuda", torch.cuda.current_device()), timeout_s)
                 be = "rccl"
+                plane_note = "rccl (size 1, INTML_DP_FORCE)"
     st = S.DPState(rank=rank, size=world, local_rank=local_rank, local_size=local_size,
                    backend=be, shard_data=shard_data, bucket_bytes=bucket_bytes, owns_pg=owns,
-                   comm=comm, xgmi_only=xgmi_only)
+                   comm=comm, xgmi_only=xgmi_only, plane=plane_note)
     S.set_state(st)
+    if plane_note and rank == 0 and world > 1:
+        import sys
+        print("[dp] %d ranks, gradient data plane: %s" % (world, plane_note), file=sys.stderr, flush=True)
     return st
 
 

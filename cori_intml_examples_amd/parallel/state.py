@@ -17,6 +17,7 @@ class DPState:
     owns_pg: bool = False
     comm: Any = None              # parallel.comm.NativeComm (RCCL data plane) or None
     xgmi_only: bool = False       # no RCCL communicator: the fused xGMI kernel is the data plane
+    plane: Optional[str] = None   # how init chose the data plane (reported on stderr / History)
 
 
 _STATE: Optional[DPState] = None

@@ -15,6 +15,7 @@ History keys ``loss, acc, val_loss, val_acc`` (+ ``lr`` from ReduceLROnPlateau).
 from __future__ import annotations
 
 import os
+from typing import Optional
 
 import numpy as np
 import torch
@@ -165,4 +166,21 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
         if model.stop_training:
             break
     cb.on_train_end()
+    model.history.data_plane = data_plane_of(ex, dp)
     return model.history
+
+
+def data_plane_of(ex, dp) -> Optional[str]:
+    """Which gradient data plane a distributed fit() ran on (recorded on its History):
+    "rccl" / "xgmi" / "hybrid" for the native captured reducer (NativeGradReducer), "gloo" /
+    "nccl" for the torch.distributed reducer, None without data parallelism; plus how
+    dist.init chose it."""
+    red = getattr(ex, "reducer", None)
+    if red is None or dp is None:
+        return None
+    if type(red).__name__ == "NativeGradReducer":
+        plane = "xgmi" if (red.xgmi is not None and len(red.buckets) == 1) else red.plane
+        kind = "NativeGradReducer:%s" % plane
+    else:
+        kind = "GradReducer:%s" % dp.backend
+    return kind + (" [%s]" % dp.plane if dp.plane else "")

@@ -28,7 +28,10 @@ def main(kind, d):
     h = m.fit(data["x"], data["y"], batch_size=64, epochs=2, validation_data=(data["xv"], data["yv"]),
               verbose=0, callbacks=cbs)
     with open(os.path.join(d, "dp%d.json" % hvd.rank()), "w") as f:
-        json.dump({k: [float(v) for v in vals] for k, vals in h.history.items()}, f)
+        rec = {k: [float(v) for v in vals] for k, vals in h.history.items()}
+        rec["reducer"] = type(m._executor.reducer).__name__
+        rec["data_plane"] = getattr(h, "data_plane", None)
+        json.dump(rec, f)
     hvd.shutdown()
 
 

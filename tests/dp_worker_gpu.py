@@ -1,7 +1,8 @@
-"""GPU worker for tests/test_gpu_integration.py: 2 ranks on ONE MI355X (gloo carries the
-gradients, since RCCL needs one GPU per rank).  Exercises the HIP executor's data-parallel
-path -- graph split before/after the gradient all-reduce, grad_scale folded into the
-fused optimizer -- and checks lockstep + equivalence with a single-process global batch."""
+"""GPU worker for tests/test_gpu_integration.py: 2 ranks on ONE MI355X.  RCCL needs one GPU
+per rank, so dist.init selects the RCCL-free xGMI data plane on its own (more local ranks than
+GPUs): NativeGradReducer with the fused all-reduce + optimizer kernel captured into the step
+graph -- the reducer an 8-GPU job runs when the probe picks xGMI.  Checks lockstep and
+equivalence with a single-process global batch, through train_on_batch AND fit()."""
 import json
 import os
 import sys
@@ -47,6 +48,8 @@ def main(out_dir):
     wf = flat(m)
     rep["wf"] = [float(wf.sum()), float(np.abs(wf).sum())]
     rep["val_loss"] = h.history["val_loss"]
+    rep["reducer"] = type(m._executor.reducer).__name__
+    rep["data_plane"] = getattr(h, "data_plane", None)
     with open(os.path.join(out_dir, "rank%d.json" % r), "w") as f:
         json.dump(rep, f)
     hvd.shutdown()

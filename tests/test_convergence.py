@@ -107,7 +107,8 @@ def test_bf16_step_converges_like_fp32_reference(kind, tmp_path):
     assert vr < 0.75 * chance and vh < 0.75 * chance, rec      # both learned (noise floor ~0.5 chance)
     assert abs(vh - vr) <= 0.05 * vr, rec                       # same training, within 5 %
     assert abs(h_hip["val_acc"][-1] - h_ref["val_acc"][-1]) < 0.02, rec
-    # DP: 2 ranks x 64 = the same global batch of 128 (gloo data plane, both on GPU 0)
+    # DP: 2 ranks x 64 = the same global batch of 128, both on GPU 0: the RCCL-free xGMI plane
+    # (NativeGradReducer, fused all-reduce + optimizer kernel in the step graph)
     np.savez(tmp_path / "data.npz", x=x, y=y, xv=xv, yv=yv)
     np.savez(tmp_path / "w0.npz", *w0)
     import socket
@@ -115,8 +116,8 @@ def test_bf16_step_converges_like_fp32_reference(kind, tmp_path):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    env = dict(os.environ, PYTHONPATH=ROOT, INTML_DP_BACKEND="gloo", INTML_DEVICE="cuda:0")
-    for k in ("WORLD_SIZE", "RANK", "INTML_COMM"):
+    env = dict(os.environ, PYTHONPATH=ROOT, INTML_DEVICE="cuda:0")
+    for k in ("WORLD_SIZE", "RANK", "INTML_COMM", "INTML_DP_BACKEND"):
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
@@ -128,5 +129,6 @@ def test_bf16_step_converges_like_fp32_reference(kind, tmp_path):
     if os.path.isdir(out):
         with open(os.path.join(out, "convergence_%s.json" % kind), "w") as f:
             json.dump(rec, f)
+    assert dp["reducer"] == "NativeGradReducer" and "xgmi" in dp["data_plane"], dp
     assert dp["val_loss"][-1] < 0.75 * chance, rec
     assert abs(dp["val_loss"][-1] - vr) <= 0.10 * vr, rec       # different sampling: wider band

@@ -106,10 +106,22 @@ def test_shard_indices_disjoint_cover_and_reshard():
     assert np.array_equal(shard_indices(10, 1, 3, False, 0, 0).numpy(), np.arange(3, 6))
 
 
-def test_rccl_init_failure_falls_back_collectively(tmp_path):
-    """A multi-GPU job whose RCCL communicator cannot come up (any rank) moves EVERY rank onto
-    the RCCL-free xGMI data plane through a gloo vote in dist.init (2 ranks, gloo, CPU)."""
-    r = _torchrun(2, [os.path.join(ROOT, "tests", "comm_fallback_worker.py"), str(tmp_path)], timeout=120)
+@pytest.mark.parametrize("scenario", ["all_init", "one_init", "uid", "hang", "selftest", "ok"])
+def test_rccl_failure_falls_back_collectively(tmp_path, scenario):
+    """A multi-GPU job whose RCCL data plane fails to come up -- in any phase (unique id,
+    communicator construction, a rank that never joins, the numeric self-test), on every rank
+    or on ONE rank only -- moves EVERY rank onto the RCCL-free xGMI data plane through the
+    phased votes of comm.establish: no rank raises, no rank hangs (2 ranks, gloo, CPU)."""
+    r = _torchrun(2, [os.path.join(ROOT, "tests", "comm_fallback_worker.py"), str(tmp_path), scenario],
+                  timeout=120, extra_env={"INTML_RCCL_INIT_TIMEOUT": "4"})
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     reps = [json.load(open(tmp_path / ("fb%d.json" % i))) for i in range(2)]
-    assert all(rep["xgmi_only"] and not rep["comm"] and rep["size"] == 2 for rep in reps), reps
+    assert all(rep["size"] == 2 for rep in reps), reps
+    if scenario == "ok":
+        assert all(rep["comm"] and not rep["xgmi_only"] and rep["plane"].startswith("rccl") for rep in reps), reps
+        return
+    assert all(rep["xgmi_only"] and not rep["comm"] and rep["plane"].startswith("xgmi") for rep in reps), reps
+    if scenario in ("one_init", "hang", "selftest"):
+        assert reps[0]["aborted"] == 1, reps        # rank 0's healthy communicator was aborted
+    if scenario == "hang":
+        assert all(rep["init_s"] < 60 for rep in reps), reps

@@ -90,8 +90,11 @@ def _free_port():
 
 
 def test_hip_data_parallel_two_ranks(tmp_path):
-    env = dict(os.environ, PYTHONPATH=ROOT, INTML_DP_BACKEND="gloo")
-    env.pop("INTML_DEVICE", None)
+    """2 ranks on GPU 0 through train_on_batch and fit() on the native reducer (ranks sharing
+    a GPU select the RCCL-free xGMI plane themselves; no gloo override)."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("INTML_DEVICE", "INTML_DP_BACKEND", "INTML_COMM"):
+        env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "tests", "dp_worker_gpu.py"), str(tmp_path)]
@@ -101,13 +104,16 @@ def test_hip_data_parallel_two_ranks(tmp_path):
     assert reps[0]["w1"] == reps[1]["w1"] and reps[0]["wf"] == reps[1]["wf"]       # lockstep
     assert reps[0]["val_loss"] == reps[1]["val_loss"]
     assert reps[0]["rel_diff"] < 0.05, reps[0]["rel_diff"]      # bf16 half-batches vs one global batch
+    for rep in reps:
+        assert rep["reducer"] == "NativeGradReducer" and "xgmi" in rep["data_plane"], rep
 
 
 def test_nested_hpo_dp_evaluation_gpu(tmp_path):
     """Nested HPO x DP (CrayHPO_rpv.ipynb:62-64,145-151): one Evaluator evaluation that is a
-    2-rank torch.distributed.run train_rpv job on GPU.  With >= 2 GPUs the slot is two
-    distinct GPUs and gradients go over RCCL; on a 1-GPU box both ranks share GPU 0 (the
-    slot names it twice) and exchange gradients over gloo -- said in the assert message."""
+    2-rank torch.distributed.run train_rpv job on GPU through fit().  With >= 2 GPUs the slot
+    is two distinct GPUs and the job votes on RCCL (numeric self-test); on a 1-GPU box both
+    ranks share GPU 0 (the slot names it twice) and run the RCCL-free xGMI plane.  Either way
+    the gradients go through the native captured reducer (NativeGradReducer)."""
     import torch
     from cori_intml_examples_amd import hpo
     n = torch.cuda.device_count()
@@ -118,20 +124,41 @@ def test_nested_hpo_dp_evaluation_gpu(tmp_path):
     foms = ev.evaluate([["--lr", "0.001"]])
     rec = ev.history[0]
     out = open(sorted(tmp_path.glob("eval*.out"))[0]).read()
-    plane = "gloo, ranks share GPU 0" if n < 2 else "rccl over 2 GPUs"
+    plane = "xgmi, ranks share GPU 0" if n < 2 else "rccl over 2 GPUs"
     assert rec["ok"] and np.isfinite(foms[0]), "%s: rc %s\n%s" % (plane, rec["rc"], out[-3000:])
     assert "rank 0/2" in out, out[-2000:]
+    assert "gradient reducer NativeGradReducer:%s" % ("xgmi" if n < 2 else "rccl") in out, out[-2000:]
+
+
+def test_train_rpv_cli_four_ranks_one_gpu(tmp_path):
+    """The train_rpv CLI (train_rpv.py:37,55-79) as a 4-rank torchrun job through fit() on ONE
+    GPU: the ranks select the RCCL-free xGMI plane (the fused all-reduce + Adam kernel, captured
+    into the step graph), linear LR scaling, Horovod callbacks; every rank prints the same FoM."""
+    env = dict(os.environ, PYTHONPATH=ROOT, HIP_VISIBLE_DEVICES="0")
+    for k in ("INTML_DEVICE", "INTML_DP_BACKEND", "INTML_COMM", "WORLD_SIZE", "RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "cori_intml_examples_amd.apps.train_rpv", "--synthetic", "--n-epochs", "2",
+           "--n-train", "4096", "--n-valid", "1024", "--lr-scaling", "linear", "--fom", "best"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400, cwd=ROOT)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    foms = [float(l.split()[-1]) for l in r.stdout.splitlines() if l.startswith("FoM:")]
+    assert len(foms) == 4 and len(set(foms)) == 1 and np.isfinite(foms[0]), out[-3000:]
+    assert "gradient reducer NativeGradReducer:xgmi" in out, out[-3000:]
+    assert "rank 3/4" in out, out[-2000:]
 
 
 def test_dist_train_px_engines_gpu():
     """DistTrain_rpv through %%px on farm engines (DistTrain_mnist.ipynb:148,294-317,494):
     two engines pinned to GPU 0, hvd.init() inside the engines turns them into one 2-rank
-    data-parallel job (gloo data plane: RCCL needs distinct GPUs per rank), the HIP
-    executor trains on the GPU and both engines end in lockstep."""
+    data-parallel job (engines sharing a GPU run the RCCL-free xGMI plane: the controller
+    says so in their environment, so every rank picks the same plane), the HIP executor
+    trains on the GPU through the native reducer and both engines end in lockstep."""
     from cori_intml_examples_amd import farm
     from cori_intml_examples_amd.farm import magics
-    cl = farm.start_cluster(2, cluster_id="gpu_px_%d" % os.getpid(), gpus=[0, 0], timeout=300,
-                            env={"INTML_DP_BACKEND": "gloo"})
+    cl = farm.start_cluster(2, cluster_id="gpu_px_%d" % os.getpid(), gpus=[0, 0], timeout=300)
     try:
         with cl.client() as c:
             ar = magics.px(
@@ -146,10 +173,13 @@ def test_dist_train_px_engines_gpu():
                 "                    optimizer='Adam', lr=0.001 * hvd.size(), use_horovod=True)\n"
                 "history = train_model(model, x, y, xv, yv, batch_size=128, n_epochs=2, use_horovod=True, verbose=0)\n"
                 "wsum = float(sum(np.abs(w).sum() for w in model.get_weights()))\n"
-                "dev = str(model.device); ex = type(model._executor).__name__; world = hvd.size()\n",
+                "dev = str(model.device); ex = type(model._executor).__name__; world = hvd.size()\n"
+                "red = type(model._executor.reducer).__name__; plane = history.data_plane\n",
                 client=c, verbose=False, block=True)
             dv = c[:]
             assert dv.pull("world") == [2, 2]
+            assert dv.pull("red") == ["NativeGradReducer"] * 2, dv.pull("plane")
+            assert all("xgmi" in p for p in dv.pull("plane")), dv.pull("plane")
             assert dv.pull("ex") == ["HipExecutor"] * 2 and all(d.startswith("cuda") for d in dv.pull("dev"))
             ws = dv.pull("wsum")
             assert ws[0] == ws[1], ws                                   # lockstep weights

@@ -569,6 +569,35 @@ def test_dgrad_onebatch_prologue_bit_identical(kind, drop, cin, hw, monkeypatch)
     assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
 
 
+def test_fused_dense_optimizer_falls_back(monkeypatch):
+    """A dense layer that took the in-wgrad optimizer path (dense_opt=1: every one-split layer)
+    in a step whose end-of-step reduction cannot fuse the optimizer (more slab descriptors than
+    the table holds; forced here with red_desc_max=1) falls back to the full optimizer launch:
+    its wgrad then stores the gradient and writes no packs, and the step trains exactly like
+    the same fallback step without the dense fusion (it used to throw 'fused pack
+    writes need the fused optimizer' on every launch)."""
+    res = []
+    for tv in ("dense_opt=1,red_desc_max=1", "dense_opt=0,red_desc_max=1"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(54)
+        m = _build("rpv_bench", "cuda", opt="Adam", drop=0.2, cin=3, hw=64)
+        x, y = _data(m, 256, seed=18)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(15)).to(ex.device)
+        ex.reset_metrics()
+        ex.train_steps(d, perm, 0, 128, 2)
+        torch.cuda.synchronize()
+        plan = ex._plans[(128, "train")]
+        assert not plan.optim_fused and not plan.dense_fused_opt
+        arena = ex.arena.clone()
+        ex.params_changed()                      # full re-pack from the master
+        torch.cuda.synchronize()
+        assert torch.equal(arena, ex.arena), "packs differ from a re-pack of the master"
+        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
+    assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
+
+
 def test_dense_dx_tiles_agree(monkeypatch):
     """The dense layer's dX at 1, 2 and 4 n-tiles per wave (dense_bwd_pair / dense_dx: the
     tile only changes which wave computes an output, not its k order) trains the same: SGD

@@ -181,14 +181,15 @@ def test_evaluator_timeout_kills_whole_process_group(tmp_path):
 
 
 def test_evaluator_explicit_and_shared_gpu_slots(monkeypatch):
-    """Explicit slots; a slot naming one GPU twice runs 2 ranks on it with the gloo data plane;
+    """Explicit slots; a slot naming one GPU twice runs 2 ranks on it (they select the RCCL-free
+    xGMI data plane themselves: more local ranks than visible GPUs -- no gloo override);
     slots_per_gpu repeats slots (several evaluations per GPU)."""
     monkeypatch.delenv("INTML_DP_BACKEND", raising=False)
     ev = hpo.Evaluator("python -c pass", gpus_per_eval=2, slots=[[0, 0]], slots_per_gpu=3)
     assert ev.num_slots == 3 and ev.gpus == [0]
     assert ev.oversubscribed([0, 0]) and not ev.oversubscribed([0, 1])
     env = ev._env_for([0, 0])
-    assert env["HIP_VISIBLE_DEVICES"] == "0" and env["INTML_DP_BACKEND"] == "gloo"
+    assert env["HIP_VISIBLE_DEVICES"] == "0" and "INTML_DP_BACKEND" not in env
     env = hpo.Evaluator("python -c pass", gpus_per_eval=2, slots=[[2, 3]])._env_for([2, 3])
     assert env["HIP_VISIBLE_DEVICES"] == "2,3" and "INTML_DP_BACKEND" not in env
     cmd = ev.command_for(["--lr", "0.1"], [0, 0])
