@@ -167,6 +167,9 @@ struct ConvStackArgs {
   int k16 = 0;
   // wt: stage outputs and argmax codes stored write-through (16-byte sc1 buffer stores)
   int wt = 0;
+  // spec: run a specialised (layer-signature) instance when one matches (conv_stack_variant);
+  // 0 = always the generic kernel (A/B and the bit-identity tests)
+  int spec = 1;
 };
 
 // Weight gradient: dW[k][n] = sum_pixels im2col(x)[p][k] * dY[p][n]  (split over pixels)
@@ -384,7 +387,7 @@ struct XgmiArgs {
   int sub = 0;                   // elements per workgroup slice of a chunk (multiple of 4)
   long long timeout_ticks = 0;   // bounded waits: give up after this many wall_clock64 ticks (100 MHz)
   int mode = 1;                  // 0: sum only (reduced gradient -> grad); 1: + optimizer
-  int fence = 1;                 // system-scope release/acquire fences around the flags
+  int fence = 2;                 // fences around the flags: 2 agent acquire, 1 system release + acquire, 0 none
   float* grad = nullptr;         // local bucket gradient (read in 1, reduced sum written in 2/3)
   float* inbox[XGMI_MAX_RANKS] = {};     // rank j's inbox [P][chunk] (as mapped here)
   float* outbox[XGMI_MAX_RANKS] = {};    // rank j's outbox [P * chunk] = reduced gradient

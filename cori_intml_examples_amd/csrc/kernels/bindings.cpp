@@ -44,6 +44,7 @@ void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s);
 void launch_init_params(const InitArgs& a, hipStream_t s);
 void launch_synth(const SynthArgs& a, hipStream_t s);
 int conv_stack_threads();
+int conv_stack_variant(const ConvStackArgs& a);
 int conv_stack_tabn();
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
 int gather_gx(int R);
@@ -160,7 +161,7 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(ConvStackArgs, st) RW(ConvStackArgs, dbg) RW(ConvStackArgs, off_w) RW(ConvStackArgs, off_codes) RW(ConvStackArgs, off_codes2) RW(ConvStackArgs, lds_bytes)
       .def("set_buf_offsets", [](ConvStackArgs& a, int b0, int b1) { a.off_buf[0] = b0; a.off_buf[1] = b1; })
       RW(ConvStackArgs, splits) PTR(ConvStackArgs, ts) RW(ConvStackArgs, off_bias)
-      RW(ConvStackArgs, from_data) RW(ConvStackArgs, training) RW(ConvStackArgs, step_inc) PTR(ConvStackArgs, srcidx) RW(ConvStackArgs, k16) RW(ConvStackArgs, wt)
+      RW(ConvStackArgs, from_data) RW(ConvStackArgs, training) RW(ConvStackArgs, step_inc) PTR(ConvStackArgs, srcidx) RW(ConvStackArgs, k16) RW(ConvStackArgs, wt) RW(ConvStackArgs, spec)
       .def("set_rows", [](ConvStackArgs& a, int l, int sp, int c0, int c1, int o0, int o1, int ib, int ih) {
         if (l < 0 || l >= MAX_STACK || sp < 0 || sp >= MAX_STACK_SPLIT) throw std::out_of_range("conv stack rows");
         const int v[6] = {c0, c1, o0, o1, ib, ih};
@@ -352,6 +353,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("MAX_STACK_SPLIT") = MAX_STACK_SPLIT;
   m.attr("STACK_THREADS") = conv_stack_threads();
   m.attr("STACK_TABN") = conv_stack_tabn();
+  m.def("conv_stack_variant", &conv_stack_variant);
   m.def("conv_stack_fwd", [](const ConvStackArgs& a, uintptr_t s) {
     launch_conv_stack_fwd(a, S(s)); check_last("conv_stack_fwd"); });
   m.def("slab_reduce", [](uintptr_t grad, int lo, int hi, const RedTable& t, uintptr_t s) {

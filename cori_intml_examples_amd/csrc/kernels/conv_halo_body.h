@@ -9,10 +9,16 @@
 // NTC n-tiles of the weight slice, TM m-tiles per wave per pass (each A fragment feeds NTC
 // MFMAs and each weight fragment TM), KCH k-steps per batch of independent reads.
 #define HALO_STAMP(i)                                                                \
-  if (a.ts && threadIdx.x == 0) a.ts[(size_t)blockIdx.x * 8 + (i)] = wall_clock64();
+  if (INSTR && a.ts && threadIdx.x == 0) a.ts[(size_t)blockIdx.x * 8 + (i)] = wall_clock64();
 
-template <int NTC, int TM, int KCH, bool CS4>
+// MODE: 0 forward / 1 backward-through epilogue fixed at compile time, -1 = a.mode at run time;
+// INSTR: the ablation switches (dbg) and diagnostics stamps (a.ts) are compiled in.  The
+// co-scheduled dual launch instantiates <.., 1, false>: none of that code (nor the forward
+// epilogue) is in its instruction stream or its register allocation.
+template <int NTC, int TM, int KCH, bool CS4, int MODE = -1, bool INSTR = true>
 __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx, const int by, char* smem) {
+  const int dbg = INSTR ? a.dbg : 0;
+  const int mode = MODE >= 0 ? MODE : a.mode;
   const int KS = a.KS, R = a.R, s = a.stride, dil = a.in_dil, Cs = a.Cs_in;
   // halo pixel stride (elements): padded by the host's bank-conflict model (lds_layout.py)
   const int XP = (CS4 || !a.xpix) ? Cs : a.xpix;
@@ -32,7 +38,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
 
   HALO_STAMP(0);
   if (tid < 8) reinterpret_cast<uint32_t*>(zl)[tid] = 0u;
-  const bool dbg_stage = !(a.dbg & 1), dbg_mfma = !(a.dbg & 2), dbg_store = !(a.dbg & 4);
+  const bool dbg_stage = !(dbg & 1), dbg_mfma = !(dbg & 2), dbg_store = !(dbg & 4);
   // input halo geometry (staged after the weights: issuing the halo's HBM loads first was
   // measured 3 us slower -- the weights' LDS stores then wait behind them)
   const int hcw = CS4 ? 4 : 8;
@@ -89,7 +95,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
   // Pooled input (dY = unpool(dP, codes)): load each pooled chunk ONCE and expand it into the
   // (up to) four full-resolution halo pixels of its window -- a quarter of the global loads of
   // rebuilding every pixel from its window (unpool_load8 per pixel).
-  const bool pooled_in = !CS4 && cbase && dil == 1 && !(a.dbg & 16);
+  const bool pooled_in = !CS4 && cbase && dil == 1 && !(dbg & 16);
   const int Ha = 2 * a.in_pH, Wa = 2 * a.in_pW;
   const int y_lo = max(yb, 0), y_hi = min(yb + R_in, Ha);
   const int x_lo = max(xb0, 0), x_hi = min(xb0 + W_in, Wa);
@@ -170,7 +176,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
   // cover the halo loads, so the two global round trips overlap instead of running back to
   // back.  (Halo loads issued BEFORE the weights' were measured 3 us slower: the weights'
   // stores then wait behind them.)  dbg 32: the two-phase form (A/B, exact).
-  const bool onebatch = dbg_stage && pooled_in && pin && !(a.dbg & (8 | 32)) && nq <= 256 * UQ && nw <= 8 * 256;
+  const bool onebatch = dbg_stage && pooled_in && pin && !(dbg & (8 | 32)) && nq <= 256 * UQ && nw <= 8 * 256;
   if (onebatch) {
     auto fused = [&](auto wu) {
       constexpr int WU = decltype(wu)::value;
@@ -191,7 +197,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
     else if (wit <= 4) fused(std::integral_constant<int, 4>{});
     else fused(std::integral_constant<int, 8>{});
   } else {
-    if (dbg_stage && !(a.dbg & 8)) staged_copy<8, bf16x8>(nw, tid, 256, wload, wstore);
+    if (dbg_stage && !(dbg & 8)) staged_copy<8, bf16x8>(nw, tid, 256, wload, wstore);
     HALO_STAMP(1);
     build_tab();
     // input halo -> LDS
@@ -370,11 +376,11 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
     // epilogue stages all TM tiles of the pass first (final bf16 values + pool codes), so
     // one copy loop writes TM*16 pixels / TM*4 windows with all lanes busy.
     const int LDC = NTC * 16;
-    const int csh = (a.mode == 1 ? a.bt.pCs : a.Cs_out) - nt0 * 16;   // channels this WG owns
+    const int csh = (mode == 1 ? a.bt.pCs : a.Cs_out) - nt0 * 16;   // channels this WG owns
     const int C = csh < LDC ? csh : LDC;
     const int cch = C >> 3;                                            // 8-channel chunks
     const FastDiv fcch(cch > 0 ? cch : 1);
-    if (a.mode == 0 && a.pool) {
+    if (mode == 0 && a.pool) {
       bf16* epb = reinterpret_cast<bf16*>(ep);                // [TM*4 windows][LDC]
       uint8_t* epc = reinterpret_cast<uint8_t*>(epb + TM * 4 * LDC);
 #pragma unroll
@@ -414,7 +420,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
     } else {
       // unpooled forward and dgrad (mode 1): stage the TM tiles as bf16, then one copy loop
       bf16* epb = reinterpret_cast<bf16*>(ep);                // [TM*16 pixels][LDC]
-      const bool fwd = a.mode == 0;
+      const bool fwd = mode == 0;
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
 #pragma unroll

@@ -39,11 +39,11 @@
 
 typedef LDS bf16 lbf16;
 
-__device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // phase stamp (diagnostics only: A.ts null in production): wall clock per wave, lane 0
 #define STACK_STAMP(i)                                                                                   \
-  if (A.ts && (threadIdx.x & 63) == 0) {                                                                 \
+  if (TS && A.ts && (threadIdx.x & 63) == 0) {                                                                 \
     unsigned long long* ts_ = A.ts + ((size_t)blockIdx.x * STACK_WAVES + (threadIdx.x >> 6)) * 32 + (i);  \
     ts_[0] = wall_clock64();                                                                             \
     ts_[16] = clock64();                                                                                 \
@@ -57,7 +57,7 @@ template <int NT, int TM, bool CS4>
 __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                             int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
                                             int OW, int XPo, LDS uint8_t* codes, const lbf16* wl, const LDS int* tab,
-                                            const lbf16* zl, uint32_t step, const LDS float* lb) {
+                                            const lbf16* zl, uint32_t step, const LDS float* lb, const int dbg) {
   // OW / XPo: row stride (pixels) / pixel stride (elements) of the output image
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
   const int XR = L.xrow, XP = L.xpix;           // input image layout
@@ -108,7 +108,7 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
     for (int t = 0; t < TM; ++t)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int KSr = (A.dbg & 1) ? 0 : KS;
+    const int KSr = (dbg & 1) ? 0 : KS;
 #pragma unroll 3
     for (int ks = 0; ks < KSr; ++ks) {
       bf16x8 af[TM];
@@ -133,7 +133,7 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
         for (int t = 0; t < TM; ++t) acc[t][nt] = mfma16(af[t], bfr, acc[t][nt]);
       }
     }
-    if (A.dbg & 2) {
+    if (dbg & 2) {
 #pragma unroll
       for (int t = 0; t < TM; ++t)
 #pragma unroll
@@ -208,7 +208,9 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
 // beyond the last tap points at the pixel itself -- finite activations times the pack's
 // zero rows -- instead of a zero buffer behind a select.  Same k order, rounding points,
 // argmax codes and dropout counters as stack_layer (bit-identical).
-template <int NT, int TM, bool CS4, int KS, bool FULL>
+// K16: 1 = the k16 tail (below) always, 0 = never, -1 = as A.k16 says (generic kernel);
+// TS: the diagnostics stamps are compiled in (timeline builds; A.ts may still be null)
+template <int NT, int TM, bool CS4, int KS, bool FULL, int K16 = -1, bool TS = true>
 __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                                  int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
                                                  int OW, int XPo, LDS uint8_t* codes, const lbf16* wl, uint32_t step,
@@ -285,8 +287,8 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) bv[nt] = *reinterpret_cast<const LDS bf16x8*>(wl + ((ks * NT + nt) * 64 + lane) * 8);
     };
-    if constexpr (CS4 && KS == 2) {
-      if (A.k16) {
+    if constexpr (CS4 && KS == 2 && K16 != 0) {
+      if (K16 == 1 || A.k16) {
         // k-step 1 holds only tap 8 (k 32..35): one 16x16x16 MFMA (lane group g holds k
         // 4g..4g+3 of the 16-wide step) on the lane's 8-byte tap-8 read; B = the 32-wide pack
         // vector's first four k of lane (r, 0), zero for g > 0 (k >= 36: no tap)
@@ -325,9 +327,11 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
       __builtin_amdgcn_sched_barrier(0);
     }
   k_done:
-    if (stamp && tb == wave * TM) {
-      asm volatile("" ::"v"(acc[0][0][0]));
-      STACK_STAMP(14);
+    if constexpr (TS) {
+      if (stamp && tb == wave * TM) {
+        asm volatile("" ::"v"(acc[0][0][0]));
+        STACK_STAMP(14);
+      }
     }
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
@@ -341,14 +345,16 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
         const uint32_t qt = (qb + (uint32_t)(pyl * Wp + wx0)) * (uint32_t)Cout + qlane;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
-          float best = -3.4e38f;
-          int code = 0;
+          // 2x2 max-pool + first-index argmax as a max tree and three equality tests (the
+          // serial compare-and-select chain was 3 compares + 6 selects per element)
+          float v[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float v = acc[t][nt][j] + bias[nt];
-            if (L.relu) v = fmaxf(v, 0.f);
-            if (v > best) { best = v; code = j; }
+            v[j] = acc[t][nt][j] + bias[nt];
+            if (L.relu) v[j] = fmaxf(v[j], 0.f);
           }
+          float best = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+          const int code = v[0] == best ? 0 : v[1] == best ? 1 : v[2] == best ? 2 : 3;
           if (thr) best = dropout_keep(qt + (uint32_t)(nt * 16), seed, sid, step, thr) ? best * dscale : 0.f;
           if (keep) outimg[ob + nt * 16] = f2bf(best);
           codes[cb + nt * 16] = (uint8_t)code;
@@ -378,7 +384,9 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
         codes[co + n] = (uint8_t)code;
       }
     }
-    if (stamp && tb == wave * TM) STACK_STAMP(15);
+    if constexpr (TS) {
+      if (stamp && tb == wave * TM) STACK_STAMP(15);
+    }
   }
 }
 
@@ -386,9 +394,10 @@ template <int NT, bool CS4>
 __device__ __forceinline__ void stack_layer_tm(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                                int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
                                                int OW, int XPo, LDS uint8_t* codes, const lbf16* wl, const LDS int* tab,
-                                               const lbf16* zl, uint32_t step, const LDS float* lb) {
+                                               const lbf16* zl, uint32_t step, const LDS float* lb, const int dbg) {
   constexpr int TM = NT >= 2 ? 2 : 4;
-  stack_layer<NT, TM, CS4>(A, L, b, c0, c1, roff, in, outimg, obase, OH, ol, OW, XPo, codes, wl, tab, zl, step, lb);
+  stack_layer<NT, TM, CS4>(A, L, b, c0, c1, roff, in, outimg, obase, OH, ol, OW, XPo, codes, wl, tab, zl, step, lb,
+                           dbg);
 }
 
 // the row-aligned fast path applies (pooled, pooled width % 4 == 0, 3x3; ablations off)
@@ -405,9 +414,57 @@ __device__ __forceinline__ void dma16_untracked(const bf16* gsrc, LDS char* ldst
                :: "s"(m0v), "v"(gsrc) : "memory", "m0");
 }
 
-__global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const ConvStackArgs A) {
+// ---------------------------------------------------------------------------------------
+// Layer signatures.  The generic kernel picks each layer's body at run time from a table of
+// 7 row-aligned and 8 generic instances, keeps every ablation branch (A.dbg) and the k16
+// switch live, and carries all of that code's register pressure into every launch (96 SGPRs
+// spilled to VGPR lanes).  A SPECIALISED instance is compiled per layer signature of the
+// networks that matter (the DistTrain_rpv / DistTrain_mnist stacks): the layer sequence,
+// each layer's body and tile shape are template constants, there is no ablation code and
+// no generic fallback inside it -- the launcher (launch_conv_stack_fwd) matches the args to
+// an instantiated signature on the host and falls back to the generic kernel otherwise.
+// A layer code packs:  kind (1 row-aligned, 2 generic) | CS4 << 2 | KS << 3 | NT << 8 |
+// TM << 11 | FULL << 14  (stack_code() computes it on the host from the same rules the
+// generic kernel applies per band).
+constexpr unsigned stack_lc(int kind, bool cs4, int ks, int nt, int tm, bool full) {
+  return (unsigned)kind | (cs4 ? 4u : 0u) | ((unsigned)ks << 3) | ((unsigned)nt << 8) | ((unsigned)tm << 11) |
+         (full ? (1u << 14) : 0u);
+}
+template <unsigned C> struct StackLC {
+  static constexpr int kind = C & 3;
+  static constexpr bool cs4 = (C >> 2) & 1;
+  static constexpr int KS = (C >> 3) & 31, NT = (C >> 8) & 7, TM = (C >> 11) & 7;
+  static constexpr bool full = (C >> 14) & 1;
+};
+
+// one layer of a specialised stack: code C's body, no run-time dispatch
+template <unsigned C, bool TS>
+__device__ __forceinline__ void stack_run_code(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
+                                               int roff, const lbf16* in, lbf16* out, int obase, int OH, int ol,
+                                               int ORS, int OPS, LDS uint8_t* codes, const lbf16* wl,
+                                               const LDS int* tab, const lbf16* zl, uint32_t step,
+                                               const LDS float* lb, bool last) {
+  using D = StackLC<C>;
+  if constexpr (D::kind == 1) {
+    stack_layer_rows<D::NT, D::TM, D::cs4, D::KS, D::full, 1, TS>(A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS,
+                                                                    OPS, codes, wl, step, lb, last);
+  } else if constexpr (D::kind == 2) {
+    stack_layer<D::NT, D::TM, D::cs4>(A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, tab, zl,
+                                      step, lb, 0);
+  }
+}
+
+// SPEC: a specialised instance for the layer codes C0..C3 (0 = no layer); TS: stamps compiled in
+template <bool SPEC, bool TS, unsigned C0, unsigned C1, unsigned C2, unsigned C3>
+__global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvStackArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem_[];
   LDS char* smem = (LDS char*)smem_;
+  constexpr int NL = SPEC ? (C0 != 0) + (C1 != 0) + (C2 != 0) + (C3 != 0) : 0;
+  // every layer row-aligned: no k-offset tables (only the generic body reads them)
+  constexpr bool no_tab = SPEC && StackLC<C0>::kind != 2 && StackLC<C1>::kind != 2 && StackLC<C2>::kind != 2 &&
+                          StackLC<C3>::kind != 2;
+  const int dbg = SPEC ? 0 : A.dbg;               // ablations: generic kernel only
+  const int nlayers = SPEC ? NL : A.n;
   const int tid = threadIdx.x;
   const int b = blockIdx.x / A.splits, sp = blockIdx.x - b * A.splits;
   lbf16* zl = (lbf16*)smem;                                      // 32 B of zeros
@@ -424,10 +481,11 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   // and written to LDS only before layer 1 -- their latency hides behind layer 0.
   constexpr int PF = (4096 + STACK_THREADS - 1) / STACK_THREADS;
   // vectors of layers 1, 2, 3 (static indices: the kernarg loads hoist out of the loops)
-  const int nv1 = A.n > 1 ? A.L[1].KS * A.L[1].NT * 64 : 0;
-  const int nv2 = A.n > 2 ? A.L[2].KS * A.L[2].NT * 64 : 0;
-  const int nv3 = A.n > 3 ? A.L[3].KS * A.L[3].NT * 64 : 0;
-  const bool prefetch = !(A.dbg & 40) && A.n > 1 && nv1 + nv2 + nv3 <= PF * STACK_THREADS;   // (32: A/B, exact)
+  const int nv1 = nlayers > 1 ? A.L[1].KS * A.L[1].NT * 64 : 0;
+  const int nv2 = nlayers > 2 ? A.L[2].KS * A.L[2].NT * 64 : 0;
+  const int nv3 = nlayers > 3 ? A.L[3].KS * A.L[3].NT * 64 : 0;
+  // (specialised instances: the launcher checked these geometry conditions on the host)
+  const bool prefetch = SPEC ? NL > 1 : !(dbg & 40) && nlayers > 1 && nv1 + nv2 + nv3 <= PF * STACK_THREADS;
   // Fast prologue (the RPV / MNIST stacks: 4-channel input, one batch of image loads per
   // thread): every global round trip of the staging in ONE batch -- the biases and layer 0's
   // weight pack are loaded first (independent of the image), then the image's dataset row
@@ -437,13 +495,13 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   LDS float* lbias = (LDS float*)(smem + A.off_bias);
   const int nv0 = A.L[0].KS * A.L[0].NT * 64;
   const int hiwi0 = A.rows[0][sp][5] * (A.L[0].Wo + A.L[0].KW - 1);
-  const bool fastpro = !(A.dbg & (8 | 128)) && prefetch && A.L[0].Cs_in == 4 && nv0 <= STACK_THREADS &&
-                       A.n * 64 <= STACK_THREADS && hiwi0 <= 4 * STACK_THREADS;
+  const bool fastpro = SPEC || (!(dbg & (8 | 128)) && prefetch && A.L[0].Cs_in == 4 && nv0 <= STACK_THREADS &&
+                                nlayers * 64 <= STACK_THREADS && hiwi0 <= 4 * STACK_THREADS);
   if (fastpro) {
     const StackLayer& L = A.L[0];
-    const int bl = min(tid, A.n * 64 - 1), bc = bl & 63;
+    const int bl = min(tid, nlayers * 64 - 1), bc = bl & 63;
     const StackLayer& LB = A.L[bl >> 6];
-    const bool bok = tid < A.n * 64 && LB.bias != nullptr && bc < LB.Cout;
+    const bool bok = tid < nlayers * 64 && LB.bias != nullptr && bc < LB.Cout;
     const float braw = *(bok ? LB.bias + bc : reinterpret_cast<const float*>(L.wpk));
     const bf16x8 wv = load_bf16x8(L.wpk + (size_t)min(tid, nv0 - 1) * 8);
     lbf16* img = (lbf16*)(smem + A.off_buf[0]);
@@ -464,7 +522,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       const bool ok = iy >= 0 && ix >= 0 && iy < L.H && ix < L.W;
       iv[u] = load_bf16x4_if(ok, x + (iy * L.W + ix) * 4, x);
     }
-    if (tid < A.n * 64) lbias[tid] = bok ? braw : 0.f;
+    if (tid < nlayers * 64) lbias[tid] = bok ? braw : 0.f;
     if (tid < nv0) *reinterpret_cast<LDS bf16x8*>(wlds + L.w_lds + tid * 8) = wv;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -477,13 +535,13 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   } else {
     // biases -> LDS [layer][64] (read by the epilogues: no global load after the prefetch
     // below, which would otherwise make its first use wait for every prefetched vector)
-    for (int i = tid; i < A.n * 64; i += STACK_THREADS) {
+    for (int i = tid; i < nlayers * 64; i += STACK_THREADS) {
       const StackLayer& L = A.L[i >> 6];
       const int c = i & 63;
       lbias[i] = (L.bias && c < L.Cout) ? L.bias[c] : 0.f;
     }
 
-    for (int l = 0; l < ((A.dbg & 8) ? 0 : (prefetch ? 1 : A.n)); ++l) {
+    for (int l = 0; l < ((dbg & 8) ? 0 : (prefetch ? 1 : nlayers)); ++l) {
       const StackLayer& L = A.L[l];
       const int nv = L.KS * L.NT * 64;
       const bf16* src = L.wpk;
@@ -493,7 +551,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
           [&](int i, const bf16x8& v) { *reinterpret_cast<LDS bf16x8*>(dst + i * 8) = v; });
     }
     // the image rows layer 0 needs -> its zero-padded halo image
-    if (!(A.dbg & 8)) {
+    if (!(dbg & 8)) {
       const StackLayer& L = A.L[0];
       lbf16* img = (lbf16*)(smem + A.off_buf[0]);
       const int Hi = A.rows[0][sp][5], Wi = L.Wo + L.KW - 1, Cs = L.Cs_in;
@@ -545,7 +603,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
   // row-aligned path keeps its tap offsets in registers, but a rows_ok layer without an
   // instantiated (KS, NT) falls back to the generic path), all computed once here: the
   // per-layer table phase and its barrier are gone
-  for (int l = 0; l < A.n; ++l) {
+  for (int l = 0; l < (no_tab ? 0 : nlayers); ++l) {
     const StackLayer& L = A.L[l];
     const int Wi = L.xrow, KHW = L.KH * L.KW, cw = L.Cs_in == 4 ? 4 : 8;
     const int ntab = L.Cs_in == 4 ? L.KS * 8 : L.KS * 4;
@@ -589,9 +647,9 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       dma16_untracked(src, wdst + (size_t)vb * 16);
     }
   }
-  for (int l = 0; l < A.n; ++l) {
+  for (int l = 0; l < nlayers; ++l) {
     const StackLayer L = A.L[l];      // by value: one batch of scalar loads per layer instead of
-    const bool last = l + 1 == A.n;   // a kernarg reload of every field after each barrier
+    const bool last = l + 1 == nlayers;   // a kernarg reload of every field after each barrier
     const int c0 = A.rows[l][sp][0], c1 = A.rows[l][sp][1];
     const int own0 = A.rows[l][sp][2], own1 = A.rows[l][sp][3];
     const int p0 = L.pool ? c0 >> 1 : c0;
@@ -625,7 +683,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
       // row padding past OW is never read)
       const int vpp = OPS >> 3;                             // vectors per pixel (Cs_out % 8 == 0)
       const int nrow = ORS * vpp;                           // vectors per image row
-      if (L.Cs_out == L.Cout && wr0 < wr1 && !(A.dbg & 3)) {
+      if (L.Cs_out == L.Cout && wr0 < wr1 && !(dbg & 3)) {
         const int ntop = wr0 * nrow, nbot = (OH - wr1) * nrow;
         const int nside = (OW - L.Wp) * vpp;                // border vectors per written row
         for (int i = tid; i < ntop + nbot; i += STACK_THREADS) z[i < ntop ? i : wr1 * nrow + (i - ntop)] = zero8;
@@ -645,7 +703,16 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     STACK_STAMP(2 + 4 * l);
     const lbf16* wl = wlds + L.w_lds;
 #define STACK_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, tab + l * STACK_TABN, zl, step, lbias + l * 64
-#define ROWS_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, step, lbias + l * 64, l == A.n - 1
+#define ROWS_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, step, lbias + l * 64, l == nlayers - 1
+    if constexpr (SPEC) {
+#define CODE_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, tab + l * STACK_TABN, zl, step, \
+                  lbias + l * 64, l == nlayers - 1
+      if (l == 0) stack_run_code<C0, TS>(CODE_ARGS);
+      else if (l == 1) stack_run_code<C1, TS>(CODE_ARGS);
+      else if (l == 2) stack_run_code<C2, TS>(CODE_ARGS);
+      else stack_run_code<C3, TS>(CODE_ARGS);
+#undef CODE_ARGS
+    } else {
     // row-aligned fast path (pooled, pooled width % 4 == 0, 3x3, instantiated KS), else generic
     const bool rows_ok = stack_rows_ok(A, L);
     // TM = 1 when it evens out the waves' tile counts (few tiles per workgroup)
@@ -667,18 +734,19 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
 #undef ROWS
     else if (L.Cs_in == 4) {
       switch (L.NT) {
-        case 1: stack_layer_tm<1, true>(STACK_ARGS); break;
-        case 2: stack_layer_tm<2, true>(STACK_ARGS); break;
-        case 3: stack_layer_tm<3, true>(STACK_ARGS); break;
-        default: stack_layer_tm<4, true>(STACK_ARGS); break;
+        case 1: stack_layer_tm<1, true>(STACK_ARGS, dbg); break;
+        case 2: stack_layer_tm<2, true>(STACK_ARGS, dbg); break;
+        case 3: stack_layer_tm<3, true>(STACK_ARGS, dbg); break;
+        default: stack_layer_tm<4, true>(STACK_ARGS, dbg); break;
       }
     } else {
       switch (L.NT) {
-        case 1: stack_layer_tm<1, false>(STACK_ARGS); break;
-        case 2: stack_layer_tm<2, false>(STACK_ARGS); break;
-        case 3: stack_layer_tm<3, false>(STACK_ARGS); break;
-        default: stack_layer_tm<4, false>(STACK_ARGS); break;
+        case 1: stack_layer_tm<1, false>(STACK_ARGS, dbg); break;
+        case 2: stack_layer_tm<2, false>(STACK_ARGS, dbg); break;
+        case 3: stack_layer_tm<3, false>(STACK_ARGS, dbg); break;
+        default: stack_layer_tm<4, false>(STACK_ARGS, dbg); break;
       }
+    }
     }
 #undef STACK_ARGS
 #undef ROWS_ARGS
@@ -691,7 +759,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
     __syncthreads();
     STACK_STAMP(4 + 4 * l);
     // owned stage rows (+ argmax codes) -> global, 16-byte stores
-    if (!(A.dbg & 4)) {
+    if (!(dbg & 4)) {
       const int cch = L.Cs_out >> 3;
       const int n = (own1 - own0) * L.Wp * cch;
       const FastDiv fc(cch), fw(L.Wp);
@@ -727,8 +795,77 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_fwd_kernel(const Con
 int conv_stack_threads() { return STACK_THREADS; }
 int conv_stack_tabn() { return STACK_TABN; }
 
+// ----------------------------------------------------------------------- host-side dispatch
+// Layer l's code as the generic kernel would pick its body (stack_rows_ok, the TM rule per
+// band, FULL); 0 if the bands disagree on TM (no specialised instance can serve them).
+static unsigned host_layer_code(const ConvStackArgs& a, int l) {
+  const StackLayer& L = a.L[l];
+  const bool rows_ok = !(a.dbg & 19) && L.pool && (L.Wp & 3) == 0 && L.KH == 3 && L.KW == 3;
+  const bool full = L.Cs_out == L.Cout && L.Cout == L.NT * 16;
+  int tm = 0;
+  for (int sp = 0; sp < a.splits; ++sp) {
+    const int ntl = ((a.rows[l][sp][1] - a.rows[l][sp][0]) >> 1) * (L.Wp >> 2);
+    const bool tm1 = ntl <= STACK_WAVES || cdiv(ntl, STACK_WAVES) < 2 * cdiv(ntl, 2 * STACK_WAVES);
+    const int t = tm1 ? 1 : 2;
+    if (tm && t != tm) return 0;
+    tm = t;
+  }
+  const bool c4 = L.Cs_in == 4;
+  if (rows_ok && c4 && L.KS == 2 && L.NT == 1) return stack_lc(1, true, 2, 1, 4, full);
+  if (rows_ok && c4 && L.KS == 2 && L.NT == 2) return stack_lc(1, true, 2, 2, 2, full);
+  if (rows_ok && !c4 && L.KS == 5 && L.NT == 2) return stack_lc(1, false, 5, 2, tm, full);
+  if (rows_ok && !c4 && L.KS == 9 && L.NT == 4) return stack_lc(1, false, 9, 4, tm, full);
+  if (rows_ok && !c4 && L.KS == 9 && L.NT == 2) return stack_lc(1, false, 9, 2, 2, full);
+  const int nt = L.NT < 1 ? 1 : (L.NT > 4 ? 4 : L.NT);
+  return stack_lc(2, c4, 0, nt, nt >= 2 ? 2 : 4, false);
+}
+
+// the specialised instances: the DistTrain_rpv stack (64x64x{1,3} -> conv 16 / 32 / 64, each
+// + ReLU + 2x2 pool; the TM of layers 1 and 2 depends on the row bands) and the
+// DistTrain_mnist stack (28x28x1 -> conv 32 'valid' unpooled, conv 64 + pool)
+#define RPV_L0 stack_lc(1, true, 2, 1, 4, true)
+#define RPV_L1(tm) stack_lc(1, false, 5, 2, tm, true)
+#define RPV_L2(tm) stack_lc(1, false, 9, 4, tm, true)
+#define MN_L0 stack_lc(2, true, 0, 2, 2, false)
+#define MN_L1(tm) stack_lc(1, false, 9, 4, tm, true)
+typedef void (*StackKernel)(const ConvStackArgs);
+struct StackSig { unsigned c[MAX_STACK]; StackKernel k[2]; };   // k[TS]
+#define SIG(c0, c1, c2, c3) \
+  {{c0, c1, c2, c3}, {conv_stack_kernel<true, false, c0, c1, c2, c3>, conv_stack_kernel<true, true, c0, c1, c2, c3>}}
+static const StackSig kStackSigs[] = {
+    SIG(RPV_L0, RPV_L1(2), RPV_L2(1), 0u), SIG(RPV_L0, RPV_L1(2), RPV_L2(2), 0u),
+    SIG(RPV_L0, RPV_L1(1), RPV_L2(1), 0u), SIG(RPV_L0, RPV_L1(1), RPV_L2(2), 0u),
+    SIG(MN_L0, MN_L1(1), 0u, 0u), SIG(MN_L0, MN_L1(2), 0u, 0u),
+};
+#undef SIG
+
+// 1 + index of the specialised instance serving these args, or 0 (generic kernel)
+int conv_stack_variant(const ConvStackArgs& a) {
+  if (!a.spec || a.dbg || a.n < 2 || a.n > MAX_STACK) return 0;
+  unsigned code[MAX_STACK] = {0u, 0u, 0u, 0u};
+  for (int l = 0; l < a.n; ++l)
+    if (!(code[l] = host_layer_code(a, l))) return 0;
+  // the specialised prologue's geometry conditions (the generic kernel tests them per launch)
+  constexpr int PF = (4096 + STACK_THREADS - 1) / STACK_THREADS;
+  int nv_later = 0;
+  for (int l = 1; l < a.n; ++l) nv_later += a.L[l].KS * a.L[l].NT * 64;
+  const StackLayer& L0 = a.L[0];
+  if (L0.Cs_in != 4 || L0.KS * L0.NT * 64 > STACK_THREADS || a.n * 64 > STACK_THREADS ||
+      nv_later > PF * STACK_THREADS)
+    return 0;
+  for (int sp = 0; sp < a.splits; ++sp)
+    if (a.rows[0][sp][5] * (L0.Wo + L0.KW - 1) > 4 * STACK_THREADS) return 0;
+  for (int i = 0; i < (int)(sizeof(kStackSigs) / sizeof(kStackSigs[0])); ++i) {
+    bool same = true;
+    for (int l = 0; l < MAX_STACK; ++l) same = same && kStackSigs[i].c[l] == code[l];
+    if (same) return i + 1;
+  }
+  return 0;
+}
+
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s) {
-  auto k = conv_stack_fwd_kernel;
+  const int v = conv_stack_variant(a);
+  StackKernel k = v ? kStackSigs[v - 1].k[a.ts ? 1 : 0] : conv_stack_kernel<false, true, 0u, 0u, 0u, 0u>;
   if (a.lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, a.lds_bytes);
   hipLaunchKernelGGL(k, dim3(a.B * a.splits), dim3(STACK_THREADS), a.lds_bytes, s, a);

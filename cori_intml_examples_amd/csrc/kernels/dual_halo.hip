@@ -21,6 +21,9 @@ size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT);
 bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits,
                       const DualExtra& x, hipStream_t s) {
   if (ca.Cs_in == 4 || wa.Cs_in == 4 || ca.KS <= 2) return false;   // 4-channel / tiny-K variants
+  // the dual kernel is built without ablation / diagnostics code and with the dgrad's
+  // backward-through epilogue only: anything else runs as two standalone launches
+  if (ca.mode != 1 || ca.dbg || wa.dbg || ca.ts || wa.ts || wa.ts2) return false;
   const int cgy = (ca.NT + ntc - 1) / ntc;
   const int cgx = ca.B * ((ca.Ho + ca.R - 1) / ca.R);
   const dim3 wg(splits, (wa.NT + NTT - 1) / NTT, (wa.Ktiles + MT - 1) / MT);

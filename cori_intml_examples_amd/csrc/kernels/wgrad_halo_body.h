@@ -16,7 +16,7 @@ __device__ __forceinline__ bf16x4 tr_read_h(const bf16* p) {
 // PIPE: software-pipelined block loop (more VGPRs; pays off for workgroups that stream many
 // blocks, not for grids that already hide the latency with many resident workgroups).
 #define WH_STAMP(i)                                                                     \
-  if (a.ts2 && threadIdx.x == 0 && (i) < 16) a.ts2[(size_t)blockIdx.x * 16 + (i)] = wall_clock64();
+  if (INSTR && a.ts2 && threadIdx.x == 0 && (i) < 16) a.ts2[(size_t)blockIdx.x * 16 + (i)] = wall_clock64();
 
 // image b of the wgrad input: the activation buffer, or (prologue-free step, first layer)
 // dataset row xidx[b] of the bound dataset
@@ -29,9 +29,12 @@ __device__ __forceinline__ const bf16* wg_xbase(const WgradArgs& a, int b) {
 // 16 banks apart (conflict-free lane writes), rows stay 16-byte aligned for the vector read
 #define WH_SQ 20
 
-template <int MTW, int NTT, bool CS4, bool PIPE>
+// INSTR: the ablation switches (dbg) and diagnostics stamps (a.ts2) are compiled in (the
+// co-scheduled dual launch instantiates false)
+template <int MTW, int NTT, bool CS4, bool PIPE, bool INSTR = true>
 __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT, const int bx, const int by,
                                                 const int bz, char* smem) {
+  const int dbg = INSTR ? a.dbg : 0;
   const int R = a.R, s = a.stride, Cs = a.Cs_in;
   const int W_in = (a.Wo - 1) * s + a.KW;
   const int R_in = (R - 1) * s + a.KH;
@@ -100,13 +103,13 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   const int nch_y = npb32 * cpr;                    // dY chunks per block
   const FastDiv fcpp(cpp), fwin(W_in), fcpr(cpr), fwo(a.Wo);
 
-  const bool dbg_stage = !(a.dbg & 1);
+  const bool dbg_stage = !(dbg & 1);
   // Pooled dY (dP + argmax codes) over whole even blocks: stage each pooled chunk ONCE and
   // expand it into its 2x2 window's pixel rows in LDS (a quarter of the global loads of a
   // per-pixel unpool; every LDS dY element of the block is written, zeros included).
   const int hw = a.Wo >> 1;
   // (pipelined path only: in the plain path its extra registers cost occupancy -- measured)
-  const bool pexp = PIPE && a.dy_code && !(a.dbg & 16) && (R & 1) == 0 && a.Ho % R == 0 && (a.Wo & 1) == 0 &&
+  const bool pexp = PIPE && a.dy_code && !(dbg & 16) && (R & 1) == 0 && a.Ho % R == 0 && (a.Wo & 1) == 0 &&
                     npb32 == npb && a.NT % NTT == 0 && a.NT * 16 <= a.Cs_dy && 2 * a.dHp >= a.Ho &&
                     2 * a.dWp >= a.Wo;
   const int nq = (R >> 1) * hw * cpr;               // pooled dY chunks per block
@@ -161,7 +164,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   // per-lane pixel offsets within a 32-pixel k-step (the kperm bijection, see below)
   const int dP0 = ((a.kperm & 1) ? 4 * g : 8 * g) + (i >> 2), dP1 = dP0 + ((a.kperm & 1) ? 16 : 4);
   auto mma_block = [&](const int npix) {
-      const int nks = (a.dbg & 2) ? 0 : (npix + 31) >> 5;
+      const int nks = (dbg & 2) ? 0 : (npix + 31) >> 5;
       // Row-aligned fast path (output width % 32 == 0, whole k-steps): a k-step's 32 pixels
       // lie in ONE output row, so the halo offset is a scalar per k-step plus a per-lane
       // constant -- no per-step division or clamping (same pixels, same k order).  One MFMA
@@ -358,7 +361,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       WH_STAMP(2 + 2 * (blk - blk0));
       fetch(min(blk + 1, blk1 - 1));      // next block's loads fly during this block's MFMAs
       mma_block(npix);
-      if (a.ts2) asm volatile("" ::"v"(acc[0][0][0]));
+      if (INSTR && a.ts2) asm volatile("" ::"v"(acc[0][0][0]));
       WH_STAMP(3 + 2 * (blk - blk0));
     }
   } else {
@@ -440,14 +443,14 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       __syncthreads();
       WH_STAMP(2 + 2 * (blk - blk0));
       mma_block(npix);
-      if (a.ts2) asm volatile("" ::"v"(acc[0][0][0]));
+      if (INSTR && a.ts2) asm volatile("" ::"v"(acc[0][0][0]));
       WH_STAMP(3 + 2 * (blk - blk0));
     }
   }
 
   const int ld = a.NT * 16;
   float* slab = a.slab + (size_t)bx * a.Ktiles * 16 * ld;
-  if (a.dbg & 4) {
+  if (dbg & 4) {
 #pragma unroll
     for (int u = 0; u < MTW; ++u)
 #pragma unroll

@@ -5,11 +5,16 @@
 // optimizer launch (a linear HIP graph: no cross-queue edges).  See XgmiArgs (args.h).
 //
 // Memory model (MI355X_MICROARCH.md "inter-workgroup visibility", cdna_hip_programming.md
-// Guideline 16, at system scope across GPUs):
+// Guideline 16, across GPUs).  The inbox / outbox / flags are UNCACHED device memory (MTYPE UC):
+// payload stores go straight to the owning GPU's memory and are acknowledged from there, so
 //   producer: payload stores -> every wave s_waitcnt vmcnt(0) -> workgroup barrier ->
-//             release fence (system) -> s_waitcnt vmcnt(0) -> relaxed system-scope flag store;
-//   consumer: relaxed system-scope poll (bounded) -> acquire fence (system) -> barrier -> loads.
-// The inbox/outbox/flags are uncached device memory, so neither side's L2 holds a stale copy.
+//             relaxed system-scope flag store (the drained stores are complete: nothing is left
+//             in any cache to write back -- the write-through publish of Guideline 16 R1);
+//   consumer: relaxed system-scope poll (bounded) -> acquire -> barrier -> loads.
+// a.fence selects the fences around the flags: 2 (default) = an agent-scope acquire only (drops
+// this CU's L1 lines of the reused inbox / outbox addresses; no L2 writeback, no L2
+// invalidate); 1 = system-scope release + acquire (the original form: every workgroup's
+// release writes back its XCD's whole L2 and every acquire invalidates it); 0 = none.
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -41,7 +46,7 @@ __device__ __forceinline__ void signal_all(unsigned* const* flags, int slot, int
   __syncthreads();
   const int t = threadIdx.x;
   if (t < P) {
-    if (fence) {     // payload in uncached memory is not in any cache: drained stores suffice
+    if (fence == 1) {   // (payload in uncached memory is not in any cache: drained stores suffice)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       drain_stores();
     }
@@ -81,8 +86,11 @@ __device__ __forceinline__ bool wait_all(const XgmiArgs& a, const unsigned* flag
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (a.fence) {
+    if (a.fence == 1) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      drain_stores();
+    } else if (a.fence == 2) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       drain_stores();
     }
   }

@@ -63,6 +63,8 @@ class GeometryMixin:
         a.dbg = tune("stack_dbg", 0)
         a.k16 = int(tune("stack_k16", True))
         a.wt = int(bool(int(tune("wt", 7)) & 1))      # write-through stage outputs / codes
+        # a layer-signature-specialised instance when one matches (conv_stack.hip kStackSigs)
+        a.spec = int(tune("stack_spec", True))
         a.set_buf_offsets(off_b0, off_b1)
         a.splits = splits
         for l in range(n):

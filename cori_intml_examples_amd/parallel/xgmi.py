@@ -118,7 +118,9 @@ class XgmiAllreduce:
         self.timeout_s = float(timeout_s or default_timeout_s())
         a.timeout_ticks = int(self.timeout_s * _TICKS_PER_S)
         a.ctr, a.err = self.ctr.data_ptr(), self.err.data_ptr()
-        a.fence = int(tune("xgmi_fence", 1))
+        # 2: agent-scope acquire only (uncached payload needs no release: xgmi.hip header);
+        # 1: the system-scope release + acquire form; 0: none
+        a.fence = int(tune("xgmi_fence", 2))
         if err is None:
             for j, b in enumerate(bases):
                 a.set_peer(j, b + self.off_in, b + self.off_out, b + self.off_f1, b + self.off_f2, b + self.off_ab)

@@ -526,6 +526,34 @@ def test_stack_fast_prologue_bit_identical(kind, drop, cin, hw, monkeypatch):
     assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
 
 
+@pytest.mark.parametrize("kind,drop,cin,hw", [("rpv_bench", 0.2, 3, 64), ("rpv_bench", 0.0, 1, 64),
+                                               ("mnist_bench", 0.3, 1, 28)])
+def test_conv_stack_specialised_bit_identical(kind, drop, cin, hw, monkeypatch):
+    """The layer-signature-specialised conv stack instances (compile-time layer bodies and
+    tile shapes, no ablation code: conv_stack.hip kStackSigs) train exactly like the generic
+    kernel on the DistTrain_rpv / DistTrain_mnist stacks -- and the launcher really picks a
+    specialised instance for them (conv_stack_variant > 0)."""
+    res = []
+    for tv in ("stack_spec=1", "stack_spec=0"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(55)
+        m = _build(kind, "cuda", opt="Adam", drop=drop, cin=cin, hw=hw)
+        x, y = _data(m, 256, seed=19)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(16)).to(ex.device)
+        ex.reset_metrics()
+        ex.train_steps(d, perm, 0, 128, 2)
+        torch.cuda.synchronize()
+        plan = ex._plans[(128, "train")]
+        stack = [f for it in plan.launches if it[0] == "conv_stack_fwd" for f in (it[1].__defaults__ or ())
+                 if hasattr(f, "spec")]
+        assert len(stack) == 1
+        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics(), ex.K.conv_stack_variant(stack[0])))
+    assert res[0][2] > 0 and res[1][2] == 0, (res[0][2], res[1][2])
+    assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
+
+
 @pytest.mark.parametrize("kind,drop,cin,hw", [("rpv", 0.2, 3, 64), ("mnist", 0.3, 1, 28)])
 def test_write_through_stores_bit_identical(kind, drop, cin, hw, monkeypatch):
     """Write-through (16-byte sc1) stores of the stage outputs / argmax codes (wt & 1), the
@@ -550,11 +578,12 @@ def test_write_through_stores_bit_identical(kind, drop, cin, hw, monkeypatch):
 
 @pytest.mark.parametrize("kind,drop,cin,hw", [("rpv", 0.2, 3, 64), ("mnist", 0.3, 1, 28)])
 def test_dgrad_onebatch_prologue_bit_identical(kind, drop, cin, hw, monkeypatch):
-    """The co-scheduled dgrad's one-batch prologue (weight and pooled-halo loads in flight
-    together, conv_halo_body.h) stages exactly what the two-phase form (dgrad_dbg=32) does:
-    whole training steps bit-identical."""
+    """The dgrad's one-batch prologue (weight and pooled-halo loads in flight together,
+    conv_halo_body.h) stages exactly what the two-phase form (dgrad_dbg=32) does: whole training
+    steps bit-identical.  (The A/B switch lives in the standalone dgrad kernel only -- the
+    co-scheduled dual kernel is built without it -- so both arms run standalone launches.)"""
     res = []
-    for tv in ("dgrad_dbg=0", "dgrad_dbg=32"):
+    for tv in ("dual_halo=0,dgrad_dbg=0", "dual_halo=0,dgrad_dbg=32"):
         monkeypatch.setenv("INTML_TUNE", tv)
         set_random_seed(51)
         m = _build(kind, "cuda", opt="Adam", drop=drop, cin=cin, hw=hw)
@@ -596,6 +625,54 @@ def test_fused_dense_optimizer_falls_back(monkeypatch):
         assert torch.equal(arena, ex.arena), "packs differ from a re-pack of the master"
         res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
     assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
+
+
+@pytest.mark.parametrize("kind,drop,cin,hw", [("rpv_bench", 0.2, 3, 64), ("mnist_bench", 0.3, 1, 28)])
+def test_dual_launch_matches_standalone(kind, drop, cin, hw, monkeypatch):
+    """The co-scheduled wgrad || dgrad launch (production bodies only: dgrad epilogue fixed to
+    backward-through, no ablation / stamp code) computes exactly what the two standalone kernels
+    it fuses compute: with the head / dense layers' reduction + update at the end of the step in
+    both arms (early_reduce=0), whole training steps are bit-identical.  (With the default early
+    reduction riding in the dual launch, the update of those layers runs in a different kernel
+    instance -- fp32 last-bit differences, test_dual_launch_early_reduce_close.)"""
+    res = []
+    for tv in ("dual_halo=1,early_reduce=0", "dual_halo=0,early_reduce=0"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(56)
+        m = _build(kind, "cuda", opt="Adam", drop=drop, cin=cin, hw=hw)
+        x, y = _data(m, 256, seed=20)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(17)).to(ex.device)
+        ex.reset_metrics()
+        ex.train_steps(d, perm, 0, 128, 2)
+        torch.cuda.synchronize()
+        names = [it[0] for it in ex._plans[(128, "train")].launches]
+        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics(), names))
+    assert any(n.startswith("wgrad_dgrad_conv") for n in res[0][2])
+    d = (res[0][0] - res[1][0]).abs()
+    assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1], (float(d.max()), int((d > 0).sum()),
+                                                                           res[0][1], res[1][1])
+
+
+def test_dual_launch_early_reduce_close(monkeypatch):
+    """Default step (dual launches carrying the head / dense reduction + Adam in extra
+    workgroups) vs standalone launches with one end-of-step reduction: the same training to
+    fp32 last-bit level (measured max |dw| ~4e-9), identical metrics."""
+    res = []
+    for tv in ("dual_halo=1", "dual_halo=0"):
+        monkeypatch.setenv("INTML_TUNE", tv)
+        set_random_seed(57)
+        m = _build("rpv_bench", "cuda", opt="Adam", drop=0.2, cin=3, hw=64)
+        x, y = _data(m, 256, seed=21)
+        ex = m._executor
+        d = ex.upload(x, y)
+        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(18)).to(ex.device)
+        ex.reset_metrics()
+        ex.train_steps(d, perm, 0, 128, 2)
+        torch.cuda.synchronize()
+        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics()))
+    assert float((res[0][0] - res[1][0]).abs().max()) < 1e-6 and res[0][1] == res[1][1]
 
 
 def test_dense_dx_tiles_agree(monkeypatch):
