@@ -167,8 +167,12 @@ def probe_data_planes(args, size, dev, g, B, chunk):
     here; SURVEY.md §5.1 item 3 "benchmark it against RCCL and keep the winner"): unless
     ``INTML_XGMI`` / ``INTML_BUCKET_BYTES`` pin it, time a short probe of the full DP step on
     each candidate data plane --
-      xgmi         the fused two-shot xGMI all-reduce + optimizer kernel (one bucket),
-      rccl         one RCCL all-reduce of the whole gradient at the end of the backward,
+      xgmi         the fused two-shot xGMI all-reduce + optimizer kernel (one bucket; the
+                   head / dense part pushed to its owners from inside the backward),
+      rccl         the default plane of fit(): at N > 1 the head / dense bucket's RCCL
+                   all-reduce + update forked onto the comm stream (overlapping the conv
+                   backward), then the small conv bucket (dist.adaptive_bucket_bytes),
+      rccl_single  one RCCL all-reduce of the whole gradient at the end of the backward,
       rccl_forked  1 MiB buckets in backward order, each all-reduce forked onto the comm
                    stream as soon as its gradients are reduced (overlaps the conv backward),
       hybrid       the dense bucket's RCCL all-reduce forked onto the comm stream (overlaps the
@@ -182,6 +186,7 @@ def probe_data_planes(args, size, dev, g, B, chunk):
             or "INTML_BUCKET_BYTES" in os.environ):
         return None
     cands = (("xgmi", {"INTML_XGMI": "xgmi"}), ("rccl", {"INTML_XGMI": "rccl"}),
+             ("rccl_single", {"INTML_XGMI": "rccl", "INTML_BUCKET_BYTES": str(1 << 40)}),
              ("rccl_forked", {"INTML_XGMI": "rccl", "INTML_BUCKET_BYTES": str(1 << 20)}),
              ("hybrid", {"INTML_XGMI": "hybrid", "INTML_BUCKET_BYTES": str(1 << 20)}))
     probe = max(chunk * 6, 48)

@@ -357,6 +357,17 @@ struct RedTable {
   RedDesc d[MAX_RED];
 };
 
+// Producer push (xGMI data plane, P > 1): the thread that finalises an element of the early
+// (head / dense) bucket's reduced gradient also stores it straight into its owner's inbox row
+// -- phase 1 of the step's fused all-reduce (xgmi.hip) happens inside the backward, behind
+// the conv layers still running, and the all-reduce kernel skips those elements.
+#define XGMI_MAX_RANKS 8
+struct XgmiPush {
+  int on = 0, rank = 0, size = 1, chunk = 0;
+  long long lo = 0;                      // first flat element of the all-reduce bucket
+  float* inbox[XGMI_MAX_RANKS] = {};     // rank j's inbox [P][chunk] (as mapped here)
+};
+
 // Optional extra workgroups of the dual conv backward launch: the fused reduction + optimizer
 // of an EARLY bucket (gradients final before that launch, weights no later kernel of the step
 // reads), run in n_r workgroups of the same grid (after the conv ones, or before: rfirst).
@@ -365,6 +376,7 @@ struct DualExtra {
   OptimArgs ro;
   float* grad = nullptr;
   int n_r = 0, rfirst = 0;
+  XgmiPush xp;                   // (ro.grad_only tables) push the reduced elements to their owners
 };
 
 // Fused data-parallel all-reduce + optimizer over xGMI peer memory (xgmi.hip).  Every rank
@@ -378,7 +390,6 @@ struct DualExtra {
 // Flags carry a per-workgroup sequence number (ctr[w] + 1), so they never need resetting.
 // Communication memory is uncached device memory shared by IPC handles; every wait is
 // bounded in time (timeout_ticks) and sets *err instead of hanging.
-#define XGMI_MAX_RANKS 8
 #define XGMI_MAX_WG 256
 struct XgmiArgs {
   int rank = 0, size = 1;
@@ -387,7 +398,11 @@ struct XgmiArgs {
   int sub = 0;                   // elements per workgroup slice of a chunk (multiple of 4)
   long long timeout_ticks = 0;   // bounded waits: give up after this many wall_clock64 ticks (100 MHz)
   int mode = 1;                  // 0: sum only (reduced gradient -> grad); 1: + optimizer
-  int fence = 2;                 // fences around the flags: 2 agent acquire, 1 system release + acquire, 0 none
+  int fence = 3;                 // fences around the flags: 3 none + sc1 payload loads, 2 agent acquire,
+                                 // 1 system release + acquire, 0 none (xgmi.hip)
+  // bucket elements [skip_lo, skip_hi) were pushed to their owners already (XgmiPush, in the
+  // backward): phase 1 skips every float4 wholly inside
+  long long skip_lo = 0, skip_hi = 0;
   float* grad = nullptr;         // local bucket gradient (read in 1, reduced sum written in 2/3)
   float* inbox[XGMI_MAX_RANKS] = {};     // rank j's inbox [P][chunk] (as mapped here)
   float* outbox[XGMI_MAX_RANKS] = {};    // rank j's outbox [P * chunk] = reduced gradient

@@ -49,7 +49,8 @@ int conv_stack_tabn();
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
 int gather_gx(int R);
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s);
-void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, hipStream_t s);
+void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, hipStream_t s,
+                         const XgmiPush* xp = nullptr);
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s);
 void launch_pack(const float* master, bf16* arena, const PackTable& tab, hipStream_t s);
 int xgmi_grid(const XgmiArgs& a);
@@ -318,8 +319,10 @@ PYBIND11_MODULE(_kernels, m) {
     launch_prologue(a, t, S(s)); check_last("prologue"); });
   m.def("gather_gx", &gather_gx);
   m.def("head_epi_max", &head_epi_max);
-  m.def("reduce_optim", [](uintptr_t grad, const RedTable& t, const OptimArgs& a, uintptr_t s) {
-    launch_reduce_optim(reinterpret_cast<float*>(grad), t, a, S(s)); check_last("reduce_optim"); });
+  m.def("reduce_optim", [](uintptr_t grad, const RedTable& t, const OptimArgs& a, uintptr_t s, const XgmiPush* xp) {
+    if (xp && xp->on && !a.grad_only) throw std::invalid_argument("producer push needs a grad_only table");
+    launch_reduce_optim(reinterpret_cast<float*>(grad), t, a, S(s), xp); check_last("reduce_optim"); },
+    py::arg("grad"), py::arg("t"), py::arg("a"), py::arg("s"), py::arg("xp") = nullptr);
   m.def("dense_bwd_dual", [](const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da, uintptr_t s) {
     const bool ok = launch_dense_bwd_dual(wa, ktw, ntt, splits, da, S(s));
     check_last("dense_bwd_dual");
@@ -336,11 +339,15 @@ PYBIND11_MODULE(_kernels, m) {
   m.def(
       "dual_halo",
       [](const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits, uintptr_t s,
-         const RedTable* rt, const OptimArgs* ro, uintptr_t rgrad, int rfirst) {
+         const RedTable* rt, const OptimArgs* ro, uintptr_t rgrad, int rfirst, const XgmiPush* xp) {
         DualExtra x;
         if (rt && ro && rt->nblocks > 0) {
           x.rt = *rt, x.ro = *ro, x.grad = reinterpret_cast<float*>(rgrad);
           x.n_r = rt->nblocks, x.rfirst = rfirst;
+          if (xp && xp->on) {
+            if (!ro->grad_only) throw std::invalid_argument("producer push needs a grad_only table");
+            x.xp = *xp;
+          }
         }
         const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, x, S(s));
         check_last("dual_halo");
@@ -348,6 +355,7 @@ PYBIND11_MODULE(_kernels, m) {
       },
       py::arg("ca"), py::arg("ntc"), py::arg("wa"), py::arg("MT"), py::arg("NTT"), py::arg("splits"), py::arg("s"),
       py::arg("rt") = nullptr, py::arg("ro") = nullptr, py::arg("rgrad") = 0, py::arg("rfirst") = 0,
+      py::arg("xp") = nullptr,
       "dual wgrad + dgrad launch; with (rt, ro, rgrad) it also runs that table's reduction + optimizer");
   m.attr("MAX_STACK") = MAX_STACK;
   m.attr("MAX_STACK_SPLIT") = MAX_STACK_SPLIT;
@@ -365,8 +373,16 @@ PYBIND11_MODULE(_kernels, m) {
   // fused xGMI all-reduce + optimizer (xgmi.hip)
   m.attr("XGMI_MAX_RANKS") = XGMI_MAX_RANKS;
   m.attr("XGMI_MAX_WG") = XGMI_MAX_WG;
+  py::class_<XgmiPush>(m, "XgmiPush")
+      .def(py::init<>())
+      RW(XgmiPush, on) RW(XgmiPush, rank) RW(XgmiPush, size) RW(XgmiPush, chunk) RW(XgmiPush, lo)
+      .def("set_inbox", [](XgmiPush& x, int j, uintptr_t p) {
+        if (j < 0 || j >= XGMI_MAX_RANKS) throw std::out_of_range("peer index");
+        x.inbox[j] = reinterpret_cast<float*>(p);
+      });
   py::class_<XgmiArgs>(m, "XgmiArgs")
       .def(py::init<>())
+      RW(XgmiArgs, skip_lo) RW(XgmiArgs, skip_hi)
       RW(XgmiArgs, rank) RW(XgmiArgs, size) RW(XgmiArgs, n) RW(XgmiArgs, chunk) RW(XgmiArgs, sub)
       RW(XgmiArgs, timeout_ticks) RW(XgmiArgs, mode) RW(XgmiArgs, fence) PTR(XgmiArgs, grad) PTR(XgmiArgs, ctr) PTR(XgmiArgs, err)
       RW(XgmiArgs, opt)

@@ -53,7 +53,7 @@ __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) 
 // One layer over the workgroup's conv-output rows [c0, c1).  Local conv row y reads rows
 // y + roff + ky of the input halo image `in`; stage output row py lands in row py - obase
 // of `outimg` (skipped outside [0, OH)); codes are kept for the local stage rows.
-template <int NT, int TM, bool CS4>
+template <int NT, int TM, bool CS4, int NW = STACK_WAVES>
 __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                             int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
                                             int OW, int XPo, LDS uint8_t* codes, const lbf16* wl, const LDS int* tab,
@@ -80,7 +80,7 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
     const int n = nt * 16 + r;
     bias[nt] = n < Cout ? lb[n] : 0.f;     // staged in LDS at kernel start
   }
-  for (int tb = wave * TM; tb < ntiles; tb += STACK_WAVES * TM) {
+  for (int tb = wave * TM; tb < ntiles; tb += NW * TM) {
     bool rv[TM];
     int xo[TM];                                   // element offset of the lane's pixel row
 #pragma unroll
@@ -210,7 +210,7 @@ __device__ __forceinline__ void stack_layer(const ConvStackArgs& A, const StackL
 // argmax codes and dropout counters as stack_layer (bit-identical).
 // K16: 1 = the k16 tail (below) always, 0 = never, -1 = as A.k16 says (generic kernel);
 // TS: the diagnostics stamps are compiled in (timeline builds; A.ts may still be null)
-template <int NT, int TM, bool CS4, int KS, bool FULL, int K16 = -1, bool TS = true>
+template <int NT, int TM, bool CS4, int KS, bool FULL, int K16 = -1, bool TS = true, int NW = STACK_WAVES>
 __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                                  int roff, const lbf16* in, lbf16* outimg, int obase, int OH, int ol,
                                                  int OW, int XPo, LDS uint8_t* codes, const lbf16* wl, uint32_t step,
@@ -256,7 +256,7 @@ __device__ __forceinline__ void stack_layer_rows(const ConvStackArgs& A, const S
   const int lo_g = g * XPo + r, lc_g = g * Cso + r;
   const uint32_t qlane = (uint32_t)g * (uint32_t)Cout + (uint32_t)r;
   // FULL: Cso == Cout == NT * 16 (no padded channels): no per-lane channel guards
-  for (int tb = wave * TM; tb < ntiles; tb += STACK_WAVES * TM) {
+  for (int tb = wave * TM; tb < ntiles; tb += NW * TM) {
     int base[TM];
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
@@ -438,7 +438,7 @@ template <unsigned C> struct StackLC {
 };
 
 // one layer of a specialised stack: code C's body, no run-time dispatch
-template <unsigned C, bool TS>
+template <unsigned C, bool TS, int NW>
 __device__ __forceinline__ void stack_run_code(const ConvStackArgs& A, const StackLayer& L, int b, int c0, int c1,
                                                int roff, const lbf16* in, lbf16* out, int obase, int OH, int ol,
                                                int ORS, int OPS, LDS uint8_t* codes, const lbf16* wl,
@@ -446,17 +446,21 @@ __device__ __forceinline__ void stack_run_code(const ConvStackArgs& A, const Sta
                                                const LDS float* lb, bool last) {
   using D = StackLC<C>;
   if constexpr (D::kind == 1) {
-    stack_layer_rows<D::NT, D::TM, D::cs4, D::KS, D::full, 1, TS>(A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS,
-                                                                    OPS, codes, wl, step, lb, last);
+    stack_layer_rows<D::NT, D::TM, D::cs4, D::KS, D::full, 1, TS, NW>(A, L, b, c0, c1, roff, in, out, obase, OH, ol,
+                                                                        ORS, OPS, codes, wl, step, lb, last);
   } else if constexpr (D::kind == 2) {
-    stack_layer<D::NT, D::TM, D::cs4>(A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, tab, zl,
-                                      step, lb, 0);
+    stack_layer<D::NT, D::TM, D::cs4, NW>(A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, tab,
+                                          zl, step, lb, 0);
   }
 }
 
 // SPEC: a specialised instance for the layer codes C0..C3 (0 = no layer); TS: stamps compiled in
-template <bool SPEC, bool TS, unsigned C0, unsigned C1, unsigned C2, unsigned C3>
-__global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvStackArgs A) {
+// (12-wave instances only: the stamp buffer is indexed by STACK_WAVES); NTH: threads per
+// workgroup (768 = 12 waves; 1024 = 16 waves for signatures whose registers fit 128 VGPRs)
+template <bool SPEC, bool TS, unsigned C0, unsigned C1, unsigned C2, unsigned C3, int NTH = STACK_THREADS>
+__global__ __launch_bounds__(NTH) void conv_stack_kernel(const ConvStackArgs A) {
+  static_assert(!TS || NTH == STACK_THREADS, "stamps index NWV waves per workgroup");
+  constexpr int NWV = NTH / 64;
   extern __shared__ __attribute__((aligned(16))) char smem_[];
   LDS char* smem = (LDS char*)smem_;
   constexpr int NL = SPEC ? (C0 != 0) + (C1 != 0) + (C2 != 0) + (C3 != 0) : 0;
@@ -479,13 +483,13 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
   // Weight packs -> LDS.  Layer 0's synchronously; the later layers' are loaded into
   // registers now (issued after the image, so waiting for the image does not wait for them)
   // and written to LDS only before layer 1 -- their latency hides behind layer 0.
-  constexpr int PF = (4096 + STACK_THREADS - 1) / STACK_THREADS;
+  constexpr int PF = (4096 + NTH - 1) / NTH;
   // vectors of layers 1, 2, 3 (static indices: the kernarg loads hoist out of the loops)
   const int nv1 = nlayers > 1 ? A.L[1].KS * A.L[1].NT * 64 : 0;
   const int nv2 = nlayers > 2 ? A.L[2].KS * A.L[2].NT * 64 : 0;
   const int nv3 = nlayers > 3 ? A.L[3].KS * A.L[3].NT * 64 : 0;
   // (specialised instances: the launcher checked these geometry conditions on the host)
-  const bool prefetch = SPEC ? NL > 1 : !(dbg & 40) && nlayers > 1 && nv1 + nv2 + nv3 <= PF * STACK_THREADS;
+  const bool prefetch = SPEC ? NL > 1 : !(dbg & 40) && nlayers > 1 && nv1 + nv2 + nv3 <= PF * NTH;
   // Fast prologue (the RPV / MNIST stacks: 4-channel input, one batch of image loads per
   // thread): every global round trip of the staging in ONE batch -- the biases and layer 0's
   // weight pack are loaded first (independent of the image), then the image's dataset row
@@ -495,8 +499,8 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
   LDS float* lbias = (LDS float*)(smem + A.off_bias);
   const int nv0 = A.L[0].KS * A.L[0].NT * 64;
   const int hiwi0 = A.rows[0][sp][5] * (A.L[0].Wo + A.L[0].KW - 1);
-  const bool fastpro = SPEC || (!(dbg & (8 | 128)) && prefetch && A.L[0].Cs_in == 4 && nv0 <= STACK_THREADS &&
-                                nlayers * 64 <= STACK_THREADS && hiwi0 <= 4 * STACK_THREADS);
+  const bool fastpro = SPEC || (!(dbg & (8 | 128)) && prefetch && A.L[0].Cs_in == 4 && nv0 <= NTH &&
+                                nlayers * 64 <= NTH && hiwi0 <= 4 * NTH);
   if (fastpro) {
     const StackLayer& L = A.L[0];
     const int bl = min(tid, nlayers * 64 - 1), bc = bl & 63;
@@ -516,7 +520,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
     bf16x4 iv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int i = min(tid + u * STACK_THREADS, hiwi0 - 1);
+      const int i = min(tid + u * NTH, hiwi0 - 1);
       const int hy = fwi.div(i), hx = i - hy * Wi;
       const int iy = y0 + hy, ix = hx - L.pad_l;
       const bool ok = iy >= 0 && ix >= 0 && iy < L.H && ix < L.W;
@@ -526,7 +530,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
     if (tid < nv0) *reinterpret_cast<LDS bf16x8*>(wlds + L.w_lds + tid * 8) = wv;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int i = tid + u * STACK_THREADS;
+      const int i = tid + u * NTH;
       if (i < hiwi0) {
         const int hy = fwi.div(i);
         *reinterpret_cast<LDS bf16x4*>(img + (hy * XR + (i - hy * Wi)) * XP) = iv[u];
@@ -535,7 +539,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
   } else {
     // biases -> LDS [layer][64] (read by the epilogues: no global load after the prefetch
     // below, which would otherwise make its first use wait for every prefetched vector)
-    for (int i = tid; i < nlayers * 64; i += STACK_THREADS) {
+    for (int i = tid; i < nlayers * 64; i += NTH) {
       const StackLayer& L = A.L[i >> 6];
       const int c = i & 63;
       lbias[i] = (L.bias && c < L.Cout) ? L.bias[c] : 0.f;
@@ -547,7 +551,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
       const bf16* src = L.wpk;
       lbf16* dst = wlds + L.w_lds;
       staged_copy<4, bf16x8>(
-          nv, tid, STACK_THREADS, [&](int i) { return load_bf16x8(src + (size_t)i * 8); },
+          nv, tid, NTH, [&](int i) { return load_bf16x8(src + (size_t)i * 8); },
           [&](int i, const bf16x8& v) { *reinterpret_cast<LDS bf16x8*>(dst + i * 8) = v; });
     }
     // the image rows layer 0 needs -> its zero-padded halo image
@@ -566,7 +570,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
       if (Cs == 4) {
         const FastDiv fwi(Wi);
         staged_copy<8, bf16x4>(
-            Hi * Wi, tid, STACK_THREADS,
+            Hi * Wi, tid, NTH,
             [&](int i) {
               const int hy = fwi.div(i), hx = i - hy * Wi;
               const int iy = y0 + hy, ix = hx - L.pad_l;
@@ -581,7 +585,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
         const int cpp = Cs >> 3;
         const FastDiv fcpp(cpp), fwi(Wi);
         staged_copy<8, bf16x8>(
-            Hi * Wi * cpp, tid, STACK_THREADS,
+            Hi * Wi * cpp, tid, NTH,
             [&](int i) {
               const int pix = fcpp.div(i), c = (i - pix * cpp) * 8;
               const int hy = fwi.div(pix), hx = pix - hy * Wi;
@@ -607,7 +611,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
     const StackLayer& L = A.L[l];
     const int Wi = L.xrow, KHW = L.KH * L.KW, cw = L.Cs_in == 4 ? 4 : 8;
     const int ntab = L.Cs_in == 4 ? L.KS * 8 : L.KS * 4;
-    for (int c = tid; c < ntab; c += STACK_THREADS) {
+    for (int c = tid; c < ntab; c += NTH) {
       const int k0 = c * cw, tap = k0 / L.Cs_in;
       int e = -1;
       if (tap < KHW) {
@@ -637,7 +641,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
     LDS char* wdst = (LDS char*)(wlds + A.L[1].w_lds);
 #pragma unroll
     for (int j = 0; j < PF; ++j) {                  // wave-uniform 64-vector chunks
-      const int vb = wave * 64 + j * STACK_THREADS;
+      const int vb = wave * 64 + j * NTH;
       if (vb >= ntot) break;
       const int v = vb + lane;
       const bf16* src = v < nv1 ? A.L[1].wpk + (size_t)v * 8
@@ -686,17 +690,17 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
       if (L.Cs_out == L.Cout && wr0 < wr1 && !(dbg & 3)) {
         const int ntop = wr0 * nrow, nbot = (OH - wr1) * nrow;
         const int nside = (OW - L.Wp) * vpp;                // border vectors per written row
-        for (int i = tid; i < ntop + nbot; i += STACK_THREADS) z[i < ntop ? i : wr1 * nrow + (i - ntop)] = zero8;
+        for (int i = tid; i < ntop + nbot; i += NTH) z[i < ntop ? i : wr1 * nrow + (i - ntop)] = zero8;
         if (nside > 0) {
           const int lcols = ol * vpp;
-          for (int i = tid; i < (wr1 - wr0) * nside; i += STACK_THREADS) {
+          for (int i = tid; i < (wr1 - wr0) * nside; i += NTH) {
             const int rr = i / nside, c = i - rr * nside;
             z[(wr0 + rr) * nrow + (c < lcols ? c : c + L.Wp * vpp)] = zero8;
           }
         }
       } else {
         const int nz = OH * nrow;
-        for (int i = tid; i < nz; i += STACK_THREADS) z[i] = zero8;
+        for (int i = tid; i < nz; i += NTH) z[i] = zero8;
         __syncthreads();                                    // before any epilogue store
       }
     }
@@ -707,17 +711,17 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
     if constexpr (SPEC) {
 #define CODE_ARGS A, L, b, c0, c1, roff, in, out, obase, OH, ol, ORS, OPS, codes, wl, tab + l * STACK_TABN, zl, step, \
                   lbias + l * 64, l == nlayers - 1
-      if (l == 0) stack_run_code<C0, TS>(CODE_ARGS);
-      else if (l == 1) stack_run_code<C1, TS>(CODE_ARGS);
-      else if (l == 2) stack_run_code<C2, TS>(CODE_ARGS);
-      else stack_run_code<C3, TS>(CODE_ARGS);
+      if (l == 0) stack_run_code<C0, TS, NWV>(CODE_ARGS);
+      else if (l == 1) stack_run_code<C1, TS, NWV>(CODE_ARGS);
+      else if (l == 2) stack_run_code<C2, TS, NWV>(CODE_ARGS);
+      else stack_run_code<C3, TS, NWV>(CODE_ARGS);
 #undef CODE_ARGS
     } else {
     // row-aligned fast path (pooled, pooled width % 4 == 0, 3x3, instantiated KS), else generic
     const bool rows_ok = stack_rows_ok(A, L);
     // TM = 1 when it evens out the waves' tile counts (few tiles per workgroup)
     const int ntl = ((c1 - c0) >> 1) * (L.Wp >> 2);
-    const bool tm1 = ntl <= STACK_WAVES || cdiv(ntl, STACK_WAVES) < 2 * cdiv(ntl, 2 * STACK_WAVES);
+    const bool tm1 = ntl <= NWV || cdiv(ntl, NWV) < 2 * cdiv(ntl, 2 * NWV);
     const bool full = L.Cs_out == L.Cout && L.Cout == L.NT * 16;
 #define ROWS(NT_, TM_, CS4_, KS_)                                                   \
   {                                                                                 \
@@ -766,7 +770,7 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
       bf16* gout = L.out + ((size_t)b * L.Hp + own0) * L.Wp * L.Cs_out;
       // write-through (A.wt): the next launch reads these rows from other XCDs anyway
       const bool wt = A.wt && (L.Cs_out & 15) == 0;
-      for (int i = tid; i < n; i += STACK_THREADS) {
+      for (int i = tid; i < n; i += NTH) {
         const int pix = fc.div(i), c = (i - pix * cch) * 8;
         const int pyo = fw.div(pix), px = pix - pyo * L.Wp;
         const u32x4 v = *reinterpret_cast<const LDS u32x4*>(out + ((own0 + pyo - obase) * ORS + px + ol) * OPS + c);
@@ -778,12 +782,12 @@ __global__ __launch_bounds__(STACK_THREADS) void conv_stack_kernel(const ConvSta
         uint8_t* gcb = L.code + ((size_t)b * L.Hp + own0) * L.Wp * L.Cs_out;
         const LDS uint8_t* lcb = codes + (own0 - p0) * L.Wp * L.Cs_out;
         if (wt) {   // 16-byte code vectors (Cs_out % 16 == 0: whole vectors, 16-byte aligned)
-          for (int i = tid; i < (nbytes >> 4); i += STACK_THREADS)
+          for (int i = tid; i < (nbytes >> 4); i += NTH)
             st_wt16(gcb, (unsigned)i * 16u, *reinterpret_cast<const LDS u32x4*>(lcb + i * 16));
         } else {
           unsigned long long* gc = reinterpret_cast<unsigned long long*>(gcb);
           const LDS unsigned long long* lc = (const LDS unsigned long long*)lcb;
-          for (int i = tid; i < (nbytes >> 3); i += STACK_THREADS) gc[i] = lc[i];
+          for (int i = tid; i < (nbytes >> 3); i += NTH) gc[i] = lc[i];
         }
       }
     }
@@ -797,15 +801,15 @@ int conv_stack_tabn() { return STACK_TABN; }
 
 // ----------------------------------------------------------------------- host-side dispatch
 // Layer l's code as the generic kernel would pick its body (stack_rows_ok, the TM rule per
-// band, FULL); 0 if the bands disagree on TM (no specialised instance can serve them).
-static unsigned host_layer_code(const ConvStackArgs& a, int l) {
+// band for nw waves, FULL); 0 if the bands disagree on TM (no specialised instance serves them).
+static unsigned host_layer_code(const ConvStackArgs& a, int l, int nw) {
   const StackLayer& L = a.L[l];
   const bool rows_ok = !(a.dbg & 19) && L.pool && (L.Wp & 3) == 0 && L.KH == 3 && L.KW == 3;
   const bool full = L.Cs_out == L.Cout && L.Cout == L.NT * 16;
   int tm = 0;
   for (int sp = 0; sp < a.splits; ++sp) {
     const int ntl = ((a.rows[l][sp][1] - a.rows[l][sp][0]) >> 1) * (L.Wp >> 2);
-    const bool tm1 = ntl <= STACK_WAVES || cdiv(ntl, STACK_WAVES) < 2 * cdiv(ntl, 2 * STACK_WAVES);
+    const bool tm1 = ntl <= nw || cdiv(ntl, nw) < 2 * cdiv(ntl, 2 * nw);
     const int t = tm1 ? 1 : 2;
     if (tm && t != tm) return 0;
     tm = t;
@@ -822,51 +826,68 @@ static unsigned host_layer_code(const ConvStackArgs& a, int l) {
 
 // the specialised instances: the DistTrain_rpv stack (64x64x{1,3} -> conv 16 / 32 / 64, each
 // + ReLU + 2x2 pool; the TM of layers 1 and 2 depends on the row bands) and the
-// DistTrain_mnist stack (28x28x1 -> conv 32 'valid' unpooled, conv 64 + pool)
+// DistTrain_mnist stack (28x28x1 -> conv 32 'valid' unpooled, conv 64 + pool).  The RPV
+// stack's all-TM-1 signature also has a 16-wave instance (its 12-wave build needs 120 VGPRs:
+// at 16 waves the 128-VGPR cap holds without spills) -- chosen with spec = 2.
 #define RPV_L0 stack_lc(1, true, 2, 1, 4, true)
 #define RPV_L1(tm) stack_lc(1, false, 5, 2, tm, true)
 #define RPV_L2(tm) stack_lc(1, false, 9, 4, tm, true)
 #define MN_L0 stack_lc(2, true, 0, 2, 2, false)
 #define MN_L1(tm) stack_lc(1, false, 9, 4, tm, true)
 typedef void (*StackKernel)(const ConvStackArgs);
-struct StackSig { unsigned c[MAX_STACK]; StackKernel k[2]; };   // k[TS]
+struct StackSig { int nth; unsigned c[MAX_STACK]; StackKernel k[2]; };   // k[TS] (k[1] null: no stamp build)
 #define SIG(c0, c1, c2, c3) \
-  {{c0, c1, c2, c3}, {conv_stack_kernel<true, false, c0, c1, c2, c3>, conv_stack_kernel<true, true, c0, c1, c2, c3>}}
+  {STACK_THREADS, {c0, c1, c2, c3}, \
+   {conv_stack_kernel<true, false, c0, c1, c2, c3>, conv_stack_kernel<true, true, c0, c1, c2, c3>}}
+#define SIG16(c0, c1, c2, c3) {1024, {c0, c1, c2, c3}, {conv_stack_kernel<true, false, c0, c1, c2, c3, 1024>, nullptr}}
 static const StackSig kStackSigs[] = {
+    SIG16(RPV_L0, RPV_L1(1), RPV_L2(1), 0u),
     SIG(RPV_L0, RPV_L1(2), RPV_L2(1), 0u), SIG(RPV_L0, RPV_L1(2), RPV_L2(2), 0u),
     SIG(RPV_L0, RPV_L1(1), RPV_L2(1), 0u), SIG(RPV_L0, RPV_L1(1), RPV_L2(2), 0u),
     SIG(MN_L0, MN_L1(1), 0u, 0u), SIG(MN_L0, MN_L1(2), 0u, 0u),
 };
 #undef SIG
+#undef SIG16
 
-// 1 + index of the specialised instance serving these args, or 0 (generic kernel)
-int conv_stack_variant(const ConvStackArgs& a) {
-  if (!a.spec || a.dbg || a.n < 2 || a.n > MAX_STACK) return 0;
-  unsigned code[MAX_STACK] = {0u, 0u, 0u, 0u};
-  for (int l = 0; l < a.n; ++l)
-    if (!(code[l] = host_layer_code(a, l))) return 0;
-  // the specialised prologue's geometry conditions (the generic kernel tests them per launch)
-  constexpr int PF = (4096 + STACK_THREADS - 1) / STACK_THREADS;
+// does signature i serve these args (its layer codes for its wave count, and the
+// specialised prologue's geometry conditions -- the generic kernel tests those per launch)
+static bool stack_sig_matches(const ConvStackArgs& a, const StackSig& g) {
+  const int nth = g.nth, nw = nth / 64;
+  for (int l = 0; l < MAX_STACK; ++l) {
+    const unsigned c = l < a.n ? host_layer_code(a, l, nw) : 0u;
+    if (c == 0u && l < a.n) return false;
+    if (c != g.c[l]) return false;
+  }
+  const int PF = (4096 + nth - 1) / nth;
   int nv_later = 0;
   for (int l = 1; l < a.n; ++l) nv_later += a.L[l].KS * a.L[l].NT * 64;
   const StackLayer& L0 = a.L[0];
-  if (L0.Cs_in != 4 || L0.KS * L0.NT * 64 > STACK_THREADS || a.n * 64 > STACK_THREADS ||
-      nv_later > PF * STACK_THREADS)
-    return 0;
+  if (L0.Cs_in != 4 || L0.KS * L0.NT * 64 > nth || a.n * 64 > nth || nv_later > PF * nth) return false;
   for (int sp = 0; sp < a.splits; ++sp)
-    if (a.rows[0][sp][5] * (L0.Wo + L0.KW - 1) > 4 * STACK_THREADS) return 0;
-  for (int i = 0; i < (int)(sizeof(kStackSigs) / sizeof(kStackSigs[0])); ++i) {
-    bool same = true;
-    for (int l = 0; l < MAX_STACK; ++l) same = same && kStackSigs[i].c[l] == code[l];
-    if (same) return i + 1;
-  }
+    if (a.rows[0][sp][5] * (L0.Wo + L0.KW - 1) > 4 * nth) return false;
+  return true;
+}
+
+// 1 + index of the specialised instance serving these args, or 0 (generic kernel).  spec = 1:
+// the 12-wave instances; spec = 2: a 16-wave instance first where one matches; a stamp
+// request (ts) takes the 12-wave stamp builds.
+int conv_stack_variant(const ConvStackArgs& a) {
+  if (!a.spec || a.dbg || a.n < 2 || a.n > MAX_STACK) return 0;
+  const int nsig = (int)(sizeof(kStackSigs) / sizeof(kStackSigs[0]));
+  for (int pass = (a.spec >= 2 && !a.ts) ? 0 : 1; pass < 2; ++pass)
+    for (int i = 0; i < nsig; ++i) {
+      const bool wide = kStackSigs[i].nth != STACK_THREADS;
+      if (wide != (pass == 0)) continue;
+      if (stack_sig_matches(a, kStackSigs[i])) return i + 1;
+    }
   return 0;
 }
 
 void launch_conv_stack_fwd(const ConvStackArgs& a, hipStream_t s) {
   const int v = conv_stack_variant(a);
   StackKernel k = v ? kStackSigs[v - 1].k[a.ts ? 1 : 0] : conv_stack_kernel<false, true, 0u, 0u, 0u, 0u>;
+  const int nth = v ? kStackSigs[v - 1].nth : STACK_THREADS;
   if (a.lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, a.lds_bytes);
-  hipLaunchKernelGGL(k, dim3(a.B * a.splits), dim3(STACK_THREADS), a.lds_bytes, s, a);
+  hipLaunchKernelGGL(k, dim3(a.B * a.splits), dim3(nth), a.lds_bytes, s, a);
 }

@@ -5,7 +5,11 @@
 #include "wgrad_halo_body.h"
 #include "reduce_body.h"
 
-template <int NTC, int MTW, int NTT, int TM>
+// XP: the early-bucket workgroups also push their reduced elements to the owners' inboxes
+// (XgmiPush, the xGMI data plane's producer push).  A separate instance: compiled into the
+// production kernel, that path raised its SGPR spills 165 -> 207 (even as a non-inlined call:
+// a call reserves ABI registers for the whole kernel).
+template <int NTC, int MTW, int NTT, int TM, bool XP>
 __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, const WgradArgs wa, const int MT,
                                                         const int n_w, const int wgx, const int wgy, const int cgx,
                                                         const DualExtra x) {
@@ -14,7 +18,8 @@ __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, con
   if (x.n_r) {   // early-bucket reduction + optimizer workgroups
     const int r = x.rfirst ? id : id - (int)gridDim.x + x.n_r;
     if (r >= 0 && r < x.n_r) {
-      reduce_optim_block_rt(x.grad, x.rt, x.ro, r, reinterpret_cast<float*>(smem));
+      if constexpr (XP) reduce_push_block(x.grad, x.rt, x.ro, r, reinterpret_cast<float*>(smem), x.xp);
+      else reduce_optim_block_rt(x.grad, x.rt, x.ro, r, reinterpret_cast<float*>(smem));
       return;
     }
     if (x.rfirst) id -= x.n_r;
@@ -32,10 +37,10 @@ __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, con
   }
 }
 
-template <int NTC, int MTW, int NTT, int TM>
+template <int NTC, int MTW, int NTT, int TM, bool XP>
 static void dual_t(const ConvMMArgs& ca, const WgradArgs& wa, int MT, dim3 wg, int cgx, int cgy, size_t lds,
                    const DualExtra& x, hipStream_t s) {
-  auto k = dual_halo_kernel<NTC, MTW, NTT, TM>;
+  auto k = dual_halo_kernel<NTC, MTW, NTT, TM, XP>;
   if (lds > 65536) hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int n_w = wg.x * wg.y * wg.z;
   hipLaunchKernelGGL(k, dim3(n_w + cgx * cgy + x.n_r), dim3(256), lds, s, ca, wa, MT, n_w, (int)wg.x, (int)wg.y, cgx,
@@ -43,18 +48,25 @@ static void dual_t(const ConvMMArgs& ca, const WgradArgs& wa, int MT, dim3 wg, i
 }
 
 // tm: m-tiles per wave per pass of the dgrad body (TM_DEFAULT, or 1 / 2 for NTC <= 2 when
-// that evens out the four waves' tile counts on small row blocks)
+// that evens out the four waves' tile counts on small row blocks).  Producer-push launches
+// (x.xp.on) have instances at the default TM only; false = not launched (the caller falls back)
 template <int NTC>
 static bool dual_w(const ConvMMArgs& ca, const WgradArgs& wa, int MT, int NTT, int mtw, int tm, dim3 wg, int cgx,
                    int cgy, size_t lds, const DualExtra& x, hipStream_t s) {
   constexpr int TMD = NTC >= 8 ? 2 : 4;
+  const bool xp = x.n_r && x.xp.on;
 #define C(M_, N_)                                                          \
   if (mtw <= M_ && NTT == N_) {                                            \
-    if constexpr (NTC <= 2) {                                              \
-      if (tm == 1) { dual_t<NTC, M_, N_, 1>(ca, wa, MT, wg, cgx, cgy, lds, x, s); return true; } \
-      if (tm == 2) { dual_t<NTC, M_, N_, 2>(ca, wa, MT, wg, cgx, cgy, lds, x, s); return true; } \
+    if (xp) {                                                              \
+      if (tm != TMD && NTC <= 2 && (tm == 1 || tm == 2)) return false;     \
+      dual_t<NTC, M_, N_, TMD, true>(ca, wa, MT, wg, cgx, cgy, lds, x, s); \
+      return true;                                                         \
     }                                                                      \
-    dual_t<NTC, M_, N_, TMD>(ca, wa, MT, wg, cgx, cgy, lds, x, s);            \
+    if constexpr (NTC <= 2) {                                              \
+      if (tm == 1) { dual_t<NTC, M_, N_, 1, false>(ca, wa, MT, wg, cgx, cgy, lds, x, s); return true; } \
+      if (tm == 2) { dual_t<NTC, M_, N_, 2, false>(ca, wa, MT, wg, cgx, cgy, lds, x, s); return true; } \
+    }                                                                      \
+    dual_t<NTC, M_, N_, TMD, false>(ca, wa, MT, wg, cgx, cgy, lds, x, s);  \
     return true;                                                           \
   }
   C(1, 1) C(2, 1) C(4, 1) C(1, 2) C(2, 2) C(4, 2) C(1, 4) C(2, 4) C(4, 4) C(1, 8) C(2, 8)
@@ -69,4 +81,3 @@ DUAL_N_DECL(1);
 DUAL_N_DECL(2);
 DUAL_N_DECL(4);
 DUAL_N_DECL(8);
-

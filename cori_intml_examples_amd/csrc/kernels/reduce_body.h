@@ -104,11 +104,26 @@ __device__ __forceinline__ bool slab_reduce_vec4(const RedDesc& d, int blk, int&
   return true;
 }
 
+// Producer push of one finalised gradient element / float4 (XgmiPush; e: flat element, the
+// float4 is 4-aligned in the bucket and never straddles an owner chunk: chunk % 4 == 0)
+__device__ __forceinline__ void xpush1(const XgmiPush& xp, long long e, float v) {
+  const long long idx = e - xp.lo;
+  const int j = (int)(idx / xp.chunk);
+  if (j != xp.rank) xp.inbox[j][(size_t)xp.rank * xp.chunk + (size_t)(idx - (long long)j * xp.chunk)] = v;
+}
+__device__ __forceinline__ void xpush4(const XgmiPush& xp, long long e, const float4& v) {
+  const long long idx = e - xp.lo;
+  const int j = (int)(idx / xp.chunk);
+  if (j != xp.rank)
+    *reinterpret_cast<float4*>(xp.inbox[j] + (size_t)xp.rank * xp.chunk + (size_t)(idx - (long long)j * xp.chunk)) = v;
+}
+
 // Reduction + Keras update of table block `blk`: the thread that produces an element's
-// gradient writes it and applies the update at once.  `red`: 256 floats of LDS.
+// gradient writes it and applies the update at once.  `red`: 256 floats of LDS.  xp (grad_only
+// tables of the data-parallel step): also push the reduced elements to their owners.
 template <int KIND>
 __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
-                                                   int blk, float* red) {
+                                                   int blk, float* red, const XgmiPush* xp = nullptr) {
   const RedDesc& dsc = tab.d[red_desc(tab, blk)];
   if (dsc.vec4) {
     int e;
@@ -125,6 +140,7 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
     bf16* tl = reinterpret_cast<bf16*>(red);
     const bool mine = slab_reduce_vec4(dsc, blk, e, g);
     if (mine) *reinterpret_cast<float4*>(grad + e) = g;
+    if (mine && xp) xpush4(*xp, e, g);
     if (mine && !a.grad_only) {           // (grad_only: the reduced gradient is all)
       float4 p = *reinterpret_cast<const float4*>(a.p + e);
       float4 s0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : float4{0.f, 0.f, 0.f, 0.f};
@@ -169,6 +185,7 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
     float g;
     const bool mine = slab_reduce_elem(tab, blk, red, e, g);
     if (mine) grad[e] = g;
+    if (mine && xp) xpush1(*xp, e, g);
     if (mine && !a.grad_only) {
       float p = a.p[e];
       float s0 = a.s0 ? a.s0[e] : 0.f, s1 = a.s1 ? a.s1[e] : 0.f;
@@ -180,6 +197,13 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
     }
   }
   if (a.defer_pack && !a.nroutes && !a.grad_only && blk == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
+}
+
+// data-parallel early bucket (a grad_only table): reduction + producer push, no update
+__device__ __forceinline__ void reduce_push_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
+                                                  int blk, float* red, const XgmiPush& xp) {
+  reduce_optim_block<OPT_SGD>(grad, tab, a, blk, red, &xp);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the pushes complete with this workgroup
 }
 
 // the same with the optimizer kind chosen at run time (a workgroup-uniform switch)

@@ -17,17 +17,22 @@
 
 #include "wgrad_halo_body.h"
 
-template <int MTW, int NTT, bool CS4, bool PIPE>
+// INSTR: ablation (a.dbg) and diagnostics-stamp (a.ts / a.ts2) code compiled in; the
+// production instance (INSTR = false) is launched whenever none of them is asked for -- that
+// code's register pressure (SGPRs spilled to VGPR lanes) is then not in the launch
+template <int MTW, int NTT, bool CS4, bool PIPE, bool INSTR>
 __global__ __launch_bounds__(256) void wgrad_halo_kernel(const WgradArgs a, const int MT) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const size_t lin = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
-  if (a.ts && threadIdx.x == 0) a.ts[2 * lin] = wall_clock64();
-  wgrad_halo_body<MTW, NTT, CS4, PIPE>(a, MT, blockIdx.x, blockIdx.y, blockIdx.z, smem);
-  if (a.ts) {
+  if (INSTR && a.ts && threadIdx.x == 0) a.ts[2 * lin] = wall_clock64();
+  wgrad_halo_body<MTW, NTT, CS4, PIPE, INSTR>(a, MT, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  if (INSTR && a.ts) {
     __syncthreads();
     if (threadIdx.x == 0) a.ts[2 * lin + 1] = wall_clock64();
   }
 }
+
+static bool wh_instr(const WgradArgs& a) { return a.dbg || a.ts || a.ts2; }
 
 size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT) {
   const int W_in = (a.Wo - 1) * a.stride + a.KW;
@@ -45,7 +50,8 @@ static void wh_t(const WgradArgs& a, int MT, dim3 grid, size_t lds, hipStream_t 
   // few workgroups streaming several blocks each: pipeline their staging; a large grid
   // already hides it with resident workgroups (and keeps the lower VGPR count)
   const bool pipe = grid.x * grid.y * grid.z < 512 && a.blocks_per_split > 1;
-  auto k = pipe ? wgrad_halo_kernel<MTW, NTT, CS4, true> : wgrad_halo_kernel<MTW, NTT, CS4, false>;
+  auto k = wh_instr(a) ? (pipe ? wgrad_halo_kernel<MTW, NTT, CS4, true, true> : wgrad_halo_kernel<MTW, NTT, CS4, false, true>)
+                       : (pipe ? wgrad_halo_kernel<MTW, NTT, CS4, true, false> : wgrad_halo_kernel<MTW, NTT, CS4, false, false>);
   if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a, MT);
 }
@@ -76,9 +82,13 @@ int wgrad_halo_resident(const WgradArgs& a, int MT, int NTT, bool bias) {
   const size_t lds = wgrad_halo_lds_bytes(a, MT, NTT);
   const int mtw = (MT + (bias ? 1 : 0) + 3) / 4;
   const void* k = nullptr;
-#define C(M_, N_)                                                                               \
-  if (!k && mtw <= M_ && NTT == N_)                                                             \
-    k = cs4 ? (const void*)wgrad_halo_kernel<M_, N_, true, false> : (const void*)wgrad_halo_kernel<M_, N_, false, false>;
+  const bool in = wh_instr(a);
+#define C(M_, N_)                                                                                       \
+  if (!k && mtw <= M_ && NTT == N_)                                                                     \
+    k = cs4 ? (in ? (const void*)wgrad_halo_kernel<M_, N_, true, false, true>                           \
+                  : (const void*)wgrad_halo_kernel<M_, N_, true, false, false>)                         \
+            : (in ? (const void*)wgrad_halo_kernel<M_, N_, false, false, true>                          \
+                  : (const void*)wgrad_halo_kernel<M_, N_, false, false, false>);
   C(1, 1) C(2, 1) C(4, 1) C(1, 2) C(2, 2) C(4, 2) C(1, 4) C(2, 4) C(4, 4) C(1, 8) C(2, 8)
 #undef C
   if (!k) return 0;

@@ -11,10 +11,12 @@
 //             relaxed system-scope flag store (the drained stores are complete: nothing is left
 //             in any cache to write back -- the write-through publish of Guideline 16 R1);
 //   consumer: relaxed system-scope poll (bounded) -> acquire -> barrier -> loads.
-// a.fence selects the fences around the flags: 2 (default) = an agent-scope acquire only (drops
-// this CU's L1 lines of the reused inbox / outbox addresses; no L2 writeback, no L2
-// invalidate); 1 = system-scope release + acquire (the original form: every workgroup's
-// release writes back its XCD's whole L2 and every acquire invalidates it); 0 = none.
+// a.fence selects the fences around the flags: 3 (default) = none, and every load of a peer's
+// payload (inbox / outbox) is an sc1 buffer load that bypasses this CU's L1 (Guideline 16: a
+// hand-off stored write-through and drained, read with sc1 loads, needs no acquire); 2 = an
+// agent-scope acquire (drops this CU's L1 lines of the reused inbox / outbox addresses:
+// ~4 us per phase-wait here); 1 = system-scope release + acquire (the original form: the
+// release writes back the XCD's whole L2, the acquire invalidates it); 0 = none, plain loads.
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -92,10 +94,23 @@ __device__ __forceinline__ bool wait_all(const XgmiArgs& a, const unsigned* flag
     } else if (a.fence == 2) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       drain_stores();
+    } else {   // (3: the payload loads are sc1; this only keeps them below the poll)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
   __syncthreads();
   return s_ok != 0;
+}
+
+// 16-byte payload load from a peer-written buffer (wave-uniform base): sc1 (fence 3: bypasses
+// this CU's L1, no acquire needed) or plain
+__device__ __forceinline__ float4 load_peer4(const float* base, size_t idx, int fence) {
+  if (fence == 3) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(idx * 4), 0, 16));
+  }
+  return *reinterpret_cast<const float4*>(base + idx);
 }
 
 __device__ __forceinline__ float4 load4_guarded(const float* p, long long idx, long long n) {
@@ -183,8 +198,12 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
       for (int j = 0; j < XGMI_MAX_RANKS; ++j)
         if (j < P && j != r) v[j] = load4_guarded(grad, (long long)j * C + k, n);
 #pragma unroll
-      for (int j = 0; j < XGMI_MAX_RANKS; ++j)
-        if (j < P && j != r) *reinterpret_cast<float4*>(a.inbox[j] + (size_t)r * C + k) = v[j];
+      for (int j = 0; j < XGMI_MAX_RANKS; ++j) {
+        const long long e = (long long)j * C + k;
+        // (elements the backward already pushed -- XgmiPush -- are in the inbox)
+        if (j < P && j != r && !(e >= a.skip_lo && e + 4 <= a.skip_hi))
+          *reinterpret_cast<float4*>(a.inbox[j] + (size_t)r * C + k) = v[j];
+      }
     }
   }
   signal_all(a.flag1, w * P + r, P, seq, a.fence);
@@ -199,7 +218,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
       float4 v[XGMI_MAX_RANKS];
 #pragma unroll
       for (int q = 0; q < XGMI_MAX_RANKS; ++q)
-        if (q < P) v[q] = q == r ? load4_guarded(grad, own, n) : *reinterpret_cast<const float4*>(in + (size_t)q * C + k);
+        if (q < P) v[q] = q == r ? load4_guarded(grad, own, n) : load_peer4(in, (size_t)q * C + k, a.fence);
       float4 s4 = v[0];
 #pragma unroll
       for (int q = 1; q < XGMI_MAX_RANKS; ++q)
@@ -220,7 +239,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
       float4 g[XGMI_MAX_RANKS];
 #pragma unroll
       for (int q = 0; q < XGMI_MAX_RANKS; ++q)
-        if (q < P && q != r) g[q] = *reinterpret_cast<const float4*>(red + (size_t)q * C + k);
+        if (q < P && q != r) g[q] = load_peer4(red, (size_t)q * C + k, a.fence);
 #pragma unroll
       for (int q = 0; q < XGMI_MAX_RANKS; ++q)
         if (q < P && q != r) finish4<KIND>(a, grad, (long long)q * C + k, n, g[q]);

@@ -1037,6 +1037,15 @@ class BatchPlan(GeometryMixin):
             # left (the update stays behind the all-reduce)
             if len(bucket_groups) == 1 and self.comm_in_graph and tune("dp_early", True):
                 dp_early = self._early_groups(grad_only=True)
+                # producer push (xGMI plane): the early groups' reduced gradient goes straight to
+                # its owners' inboxes from the launch that reduces it, inside the backward, and
+                # the fused all-reduce kernel skips those elements in its phase 1
+                self.early_push, self.pushed = {}, None
+                if tune("xgmi_push", True):
+                    for nm, (tab_, (elo, ehi), go) in self.early_red.items():
+                        xp = reducer.push_args(elo, ehi) if go else None
+                        if xp is not None:
+                            self.early_push[nm], self.pushed = xp, (elo, ehi)
         else:
             # single stream, no all-reduce to overlap: ONE reduction launch at the end of the
             # backward (each launch boundary costs ~5 us here), if the descriptors fit a table
@@ -1100,7 +1109,8 @@ class BatchPlan(GeometryMixin):
                               (lambda s: self._launch_optim_comm(k, s)), "comm"))
             # the xGMI bucket: all-reduce + Keras update in one kernel on the main stream
             extra.append(("xgmi_allreduce_optim_b%d", lambda k: None if k != xk else
-                          (lambda s: reducer.launch_fused(ex.store.grad, ex._optim_args(False, defer_pack=True), s)),
+                          (lambda s: reducer.launch_fused(ex.store.grad, ex._optim_args(False, defer_pack=True), s,
+                                                          pushed=getattr(self, "pushed", None))),
                           "main"))
         self.launches, self.bucket_ready = splice_bucket_launches(
             self.launches, inserts,

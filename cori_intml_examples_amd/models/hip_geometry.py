@@ -63,8 +63,10 @@ class GeometryMixin:
         a.dbg = tune("stack_dbg", 0)
         a.k16 = int(tune("stack_k16", True))
         a.wt = int(bool(int(tune("wt", 7)) & 1))      # write-through stage outputs / codes
-        # a layer-signature-specialised instance when one matches (conv_stack.hip kStackSigs)
-        a.spec = int(tune("stack_spec", True))
+        # a layer-signature-specialised instance when one matches (conv_stack.hip kStackSigs):
+        # 1 = 12-wave instances, 2 (default: +0.4 %, profiles/r5e_ab.txt) = a 16-wave instance first
+        # where one exists, 0 = generic
+        a.spec = int(tune("stack_spec", 2))
         a.set_buf_offsets(off_b0, off_b1)
         a.splits = splits
         for l in range(n):
@@ -219,15 +221,18 @@ class GeometryMixin:
     def _dual(self, a, ntc, wa, cfg, s, name=None):
         K, ex = self.ex.K, self.ex
         early = (self.early_red or {}).get(name)
+        xp = (getattr(self, "early_push", None) or {}).get(name)   # producer push (xGMI plane)
         kw = {}
         if early is not None:   # this launch also carries an early bucket's reduction (+ optimizer)
             kw.update(rt=early[0], ro=self._early_ro(early), rgrad=ex.store.grad.data_ptr())
+            if xp is not None:
+                kw["xp"] = xp
         ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, **kw)
         if not ok:   # unsupported combination
             K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
             K.conv_halo(a, ntc, s)
             if early is not None:
-                K.reduce_optim(ex.store.grad.data_ptr(), early[0], self._early_ro(early), s)
+                K.reduce_optim(ex.store.grad.data_ptr(), early[0], self._early_ro(early), s, xp)
 
     def _early_ro(self, early):
         """OptimArgs of an early reduction table: the Keras update, or (data-parallel step,

@@ -366,16 +366,24 @@ class GradReducer:
             grad[: self.store.numel].div_(self.size)
 
 
-def adaptive_bucket_bytes(groups: Sequence[Tuple[int, int]]) -> int:
-    """Bucket size for the captured RCCL data plane.  A gradient of <= 16 MB (e.g. the RPV
-    model's 2.2 MB) is ONE fused all-reduce at the end of the backward on the main stream:
-    a linear graph, because every cross-stream edge of a graph replay costs several us on
-    MI355X (measured: two forked buckets 170 us/step vs one fused 147 us at N=1) -- more than
-    the overlap can win back for a transfer of that size.  Larger gradients (the 34.5M-param
-    legacy RPV model: 138 MB) get ~4 buckets of >= 16 MB forked onto the comm stream so the
-    all-reduces overlap the rest of the backward."""
+def adaptive_bucket_bytes(groups: Sequence[Tuple[int, int]], size: int = 1) -> int:
+    """Bucket size for the captured RCCL data plane.
+
+    * A real multi-rank job (size > 1): the first bucket closes after the backward-ordered
+      groups reach 1 MiB -- for the RPV model the head + dense gradient (2.1 MB, 96 % of the
+      bytes, final ~57 us before the backward ends) -- and every bucket's all-reduce is forked
+      onto the comm stream, where its optimizer update also runs: the dense layer's all-reduce
+      and Adam overlap the conv backward instead of trailing it (the small conv bucket is the
+      exposed tail).  At N = 1 (loopback) the forked plane costs the same as one bucket
+      (119.4 vs 119.1 us/step, profiles/r4_plane_probe_n1.json; profiles/r5_*_ab.txt).
+    * size 1 (INTML_DP_FORCE loopback runs) and gradients <= 16 MB otherwise: ONE fused
+      all-reduce at the end of the backward on the main stream -- a linear graph.
+    * Larger gradients (the 34.5M-param legacy RPV model: 138 MB) get ~4 buckets of >= 16 MB,
+      forked onto the comm stream so the all-reduces overlap the rest of the backward."""
     total = 4 * sum(hi - lo for lo, hi in groups)
     if total <= (16 << 20):
+        if size > 1 and total > (1 << 20) and tune("dp_overlap", True):
+            return 1 << 20
         return total + 1
     return max(16 << 20, total // 4)
 
@@ -435,7 +443,7 @@ class NativeGradReducer:
             bb = 1 << 62                    # the whole gradient is ONE fused xGMI bucket
         elif self.plane == "hybrid" and not bb:
             bb = 1 << 20                    # dense bucket(s) over RCCL, the conv tail over xGMI
-        bg, spans = merge_buckets(groups, bb or adaptive_bucket_bytes(groups))
+        bg, spans = merge_buckets(groups, bb or adaptive_bucket_bytes(groups, self.size))
         if self._configured and spans == self.buckets and bg == self.bucket_groups:
             return self.bucket_groups       # same layout (another batch size): keep the staging
         self.bucket_groups, self.buckets = bg, spans   # buffers earlier graphs reference
@@ -483,12 +491,24 @@ class NativeGradReducer:
             raise RuntimeError("data parallel without RCCL (INTML_COMM=xgmi, or ranks sharing a GPU): the "
                                "fused xGMI all-reduce failed its collective setup / self-test (see stderr)")
 
-    def launch_fused(self, grad: torch.Tensor, opt_args, stream: int) -> None:
+    def launch_fused(self, grad: torch.Tensor, opt_args, stream: int, pushed=None) -> None:
         """The fused all-reduce + optimizer of the xGMI bucket (capturable); ``opt_args``
-        cover the whole flat buffer and are offset to the bucket here."""
+        cover the whole flat buffer and are offset to the bucket here.  ``pushed``: the flat
+        (lo, hi) range the backward already pushed to its owners (push_args)."""
         from . import xgmi as X
         lo, _ = self.buckets[self.xgmi_bucket]
-        self.xgmi.launch(grad.data_ptr() + 4 * lo, stream, opt=X.offset_optim(opt_args, lo))
+        skip = (pushed[0] - lo, pushed[1] - lo) if pushed else (0, 0)
+        self.xgmi.launch(grad.data_ptr() + 4 * lo, stream, opt=X.offset_optim(opt_args, lo), skip=skip)
+
+    def push_args(self, lo: int, hi: int):
+        """XgmiPush for an early range [lo, hi) finalised inside the backward, when it lies in
+        the xGMI bucket and there are peers to push to; else None."""
+        if self.xgmi is None or self.xgmi_bucket is None:
+            return None
+        blo, bhi = self.buckets[self.xgmi_bucket]
+        if lo < blo or hi > bhi:
+            return None
+        return self.xgmi.push_args(blo)
 
     def launch(self, bucket: int, grad: torch.Tensor, stream: torch.cuda.Stream) -> None:
         """Enqueue bucket ``bucket``'s all-reduce on ``stream`` (capturable)."""

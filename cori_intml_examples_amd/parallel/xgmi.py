@@ -118,20 +118,36 @@ class XgmiAllreduce:
         self.timeout_s = float(timeout_s or default_timeout_s())
         a.timeout_ticks = int(self.timeout_s * _TICKS_PER_S)
         a.ctr, a.err = self.ctr.data_ptr(), self.err.data_ptr()
-        # 2: agent-scope acquire only (uncached payload needs no release: xgmi.hip header);
-        # 1: the system-scope release + acquire form; 0: none
-        a.fence = int(tune("xgmi_fence", 2))
+        # 3: no fences, sc1 payload loads; 2: agent-scope acquire; 1: system-scope release +
+        # acquire; 0: none (xgmi.hip header; uncached payload never needs a release)
+        a.fence = int(tune("xgmi_fence", 3))
         if err is None:
             for j, b in enumerate(bases):
                 a.set_peer(j, b + self.off_in, b + self.off_out, b + self.off_f1, b + self.off_f2, b + self.off_ab)
+        self.bases = bases if err is None else []
         self.args = a
         self.setup_error = err
 
     # ------------------------------------------------------------------ launches
-    def launch(self, grad: int, stream: int, opt=None) -> None:
+    def push_args(self, lo: int = 0):
+        """XgmiPush for the kernels that finalise part of this all-reduce's bucket inside the
+        backward (the early head / dense reduction): they store each reduced element straight
+        into its owner's inbox row -- phase 1 of the all-reduce, overlapping the rest of the
+        backward.  ``lo``: the bucket's first flat element.  None at size 1 (nothing to push)."""
+        if self.size < 2 or not self.bases:
+            return None
+        x = self.K.XgmiPush()
+        x.on, x.rank, x.size, x.chunk, x.lo = 1, self.rank, self.size, self.chunk, int(lo)
+        for j, b in enumerate(self.bases):
+            x.set_inbox(j, b + self.off_in)
+        return x
+
+    def launch(self, grad: int, stream: int, opt=None, skip=(0, 0)) -> None:
         """Enqueue the fused all-reduce on `stream` (capturable): the reduced SUM lands in
-        `grad`; with `opt` (OptimArgs, grad_scale = 1/size) the Keras update follows."""
+        `grad`; with `opt` (OptimArgs, grad_scale = 1/size) the Keras update follows.
+        ``skip``: bucket-relative element range already pushed by the backward (push_args)."""
         a = self.args
+        a.skip_lo, a.skip_hi = int(skip[0]), int(skip[1])
         a.grad = grad
         if opt is not None:
             a.mode, a.opt = 1, opt

@@ -4,11 +4,12 @@
 # in this order, each only if its variable is set, each under its own time limit; a crash, a
 # timeout or a failed test stops the pass (TESTS_CONTINUE=1: a failed test is reported and the
 # measurements still run):
-#   TESTS="<pytest args>"     e.g. "tests/test_hip_model.py -k specialised"  (or "all" = -m gpu)
+#   TESTS="<pytest args>"     e.g. "tests/test_hip_model.py -k 'spec or dual'"  (or "all" = -m gpu)
 #   SMOKE=1                   __graft_entry__.smoke()
 #   DRIVER=1                  the driver's exact bench command (bench.py --gpus 1 --steps 20 --warmup 5)
 #   AB="a|b|c"                interleaved bench A/B of INTML_TUNE variants ("" = defaults), with
-#                             AB_MODEL (rpv), AB_STEPS (600), AB_ROUNDS (3), AB_ENV (extra env)
+#                             AB_MODEL (rpv), AB_STEPS (600), AB_ROUNDS (3), AB_ENV (extra env);
+#                             a variant "ENV=v ENV2=w;tune" also sets environment for that arm
 #   BENCH="<bench args>"      one bench.py line (BENCH_ENV: extra env)
 #   PROF="rpv mnist ..."      rocprofv3 kernel stats of each model's bench step (PROF_ENV)
 #   PMC=<model>               the two PMC counter passes of that model (gpu_pmc.sh)
@@ -22,7 +23,7 @@ TAG=${TAG:-pass}
 O=gpurun_out/$TAG
 if [ -n "$TESTS" ]; then
   if [ "$TESTS" = "all" ]; then TESTS="tests -m gpu"; fi
-  $T ${TESTS_LIMIT:-900} python -u -m pytest -v --timeout 200 --timeout-method thread $TESTS > ${O}_tests.log 2>&1
+  eval "$T ${TESTS_LIMIT:-900} python -u -m pytest -v --timeout 200 --timeout-method thread $TESTS" > ${O}_tests.log 2>&1
   rc=$?; grep -E "passed|failed" ${O}_tests.log | tail -n 2; grep -E "FAILED|ERROR" ${O}_tests.log | head -n 20
   if [ $rc -ne 0 ]; then
     grep -B2 -A14 "^E  " ${O}_tests.log | head -n 60
@@ -42,7 +43,9 @@ if [ -n "$AB" ]; then
   IFS='|' read -ra VARIANTS <<< "$AB"
   for i in $(seq 1 ${AB_ROUNDS:-3}); do
     for v in "${VARIANTS[@]}"; do
-      env $AB_ENV INTML_TUNE="$v" $T 200 python bench.py --model ${AB_MODEL:-rpv} --steps ${AB_STEPS:-600} --warmup 80 --no-hpo --no-dp-delta \
+      venv=""; tv="$v"
+      if [[ "$v" == *";"* ]]; then venv="${v%%;*}"; tv="${v#*;}"; fi
+      env $AB_ENV $venv INTML_TUNE="$tv" $T 200 python bench.py --model ${AB_MODEL:-rpv} --steps ${AB_STEPS:-600} --warmup 80 --no-hpo --no-dp-delta \
         > ${O}_ab.tmp 2>&1 || { tail -n 30 ${O}_ab.tmp; exit 1; }
       line ${O}_ab.tmp "r$i [${v:-default}]" | tee -a ${O}_ab.txt
     done

@@ -82,6 +82,10 @@ def run(opt, lr, outdir, r, P, dev):
     rep["buckets"] = [list(x) for x in red.buckets]
     rep["comm_in_graph"] = bool(plan.comm_in_graph)
     rep["fused_launches"] = [it[0] for it in plan.launches if "xgmi" in it[0] or "allreduce" in it[0]]
+    # producer push: the launches that reduce the early (head / dense) groups inside the
+    # backward and push them to their owners' inboxes, and the range the all-reduce skips
+    rep["push_launches"] = sorted((getattr(plan, "early_push", None) or {}).keys())
+    rep["pushed"] = list(getattr(plan, "pushed", None) or [])
     rep["err"] = int(red.xgmi.err[0].item()) if red.xgmi is not None else -1
     rep["digest"] = hashlib.sha256(w.tobytes()).hexdigest()
     rep["finite"] = bool(np.isfinite(w).all())
