@@ -361,11 +361,36 @@ struct RedTable {
 // (head / dense) bucket's reduced gradient also stores it straight into its owner's inbox row
 // -- phase 1 of the step's fused all-reduce (xgmi.hip) happens inside the backward, behind
 // the conv layers still running, and the all-reduce kernel skips those elements.
+//
+// Exchange (mode 2): a LATER backward launch's extra workgroups finish that bucket's part of
+// the all-reduce and apply its update, so the head / dense layers' whole all-reduce + Adam
+// runs inside the backward and the fused all-reduce kernel is left with the conv layers:
+//   mode 1 (first dual launch): reduce the table block, push each element to its owner's
+//          inbox row, raise the block's push flag bflag1[blk][me] on every rank;
+//   mode 2 (next dual launch): the owner of a block's elements waits for every sender's push
+//          flag, sums the rows in rank order, pushes the sum into every peer's outbox and raises
+//          bflag2[blk][me] on every rank; every rank waits for the owners of the block's other
+//          elements and reads their sums; then the Keras update of the block (tiled dense
+//          pack writes, as the single-GPU early reduction).
+// Every wait depends only on other GPUs' earlier launches or on the same block of the same
+// launch on another GPU, whose owner part precedes its wait -- no cycle.  Ranks sharing a
+// GPU use nx workgroups looping over the blocks in order (a few spinning workgroups cannot
+// starve the peers' launches).  Sequence numbers: ctrb[blk] + 1 (ctrb advanced by mode 2).
 #define XGMI_MAX_RANKS 8
 struct XgmiPush {
   int on = 0, rank = 0, size = 1, chunk = 0;
   long long lo = 0;                      // first flat element of the all-reduce bucket
   float* inbox[XGMI_MAX_RANKS] = {};     // rank j's inbox [P][chunk] (as mapped here)
+  int mode = 1;                          // 1 reduce + push (+ block flags), 2 exchange + update
+  float* outbox[XGMI_MAX_RANKS] = {};    // rank j's outbox [P * chunk] (bucket index)
+  unsigned* bflag1[XGMI_MAX_RANKS] = {}; // rank j's per-block push flags [nblk][P] (null: no flags)
+  unsigned* bflag2[XGMI_MAX_RANKS] = {}; // rank j's per-block owner-sum flags [nblk][P]
+  unsigned* abort_[XGMI_MAX_RANKS] = {}; // rank j's sticky abort word
+  unsigned* ctrb = nullptr;              // [nblk] this rank's per-block sequence counters
+  int* err = nullptr;                    // the all-reduce's error record (xgmi.hip wait_all)
+  long long timeout_ticks = 0;
+  int nblk = 0;                          // blocks of the table
+  int nx = 0;                            // mode 2: workgroups looping over the blocks (0: one each)
 };
 
 // Optional extra workgroups of the dual conv backward launch: the fused reduction + optimizer
@@ -401,8 +426,10 @@ struct XgmiArgs {
   int fence = 3;                 // fences around the flags: 3 none + sc1 payload loads, 2 agent acquire,
                                  // 1 system release + acquire, 0 none (xgmi.hip)
   // bucket elements [skip_lo, skip_hi) were pushed to their owners already (XgmiPush, in the
-  // backward): phase 1 skips every float4 wholly inside
+  // backward): phase 1 skips every float4 wholly inside; skip_mode 2: they were also
+  // all-reduced and updated there (exchange), so no phase touches them
   long long skip_lo = 0, skip_hi = 0;
+  int skip_mode = 0;
   float* grad = nullptr;         // local bucket gradient (read in 1, reduced sum written in 2/3)
   float* inbox[XGMI_MAX_RANKS] = {};     // rank j's inbox [P][chunk] (as mapped here)
   float* outbox[XGMI_MAX_RANKS] = {};    // rank j's outbox [P * chunk] = reduced gradient

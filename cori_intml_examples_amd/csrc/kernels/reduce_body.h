@@ -118,6 +118,74 @@ __device__ __forceinline__ void xpush4(const XgmiPush& xp, long long e, const fl
     *reinterpret_cast<float4*>(xp.inbox[j] + (size_t)xp.rank * xp.chunk + (size_t)(idx - (long long)j * xp.chunk)) = v;
 }
 
+// Keras update of the elements a table block's thread holds (vec4 descriptor: the float4 at
+// e; `mine` false: the thread holds none) -- with the tiled pack writes of a dense route
+// (dsc.tile: the workgroup's 1024 updated weights are whole 8-row groups of the route, staged
+// as bf16 in LDS -- red: >= 2 KB -- and written as 16-byte vectors).  Every thread of the
+// workgroup calls it (it may synchronise the workgroup).
+template <int KIND>
+__device__ __forceinline__ void update_vec4(const RedDesc& dsc, const OptimArgs& a, int blk, float* red, bool mine,
+                                            int e, const float4& g) {
+  const PackRoute* tr = nullptr;
+  if (a.nroutes && dsc.tile) {
+    for (int r = 0; r < a.nroutes; ++r) {           // uniform: the descriptor's route
+      const PackRoute& R = a.routes[r];
+      if (R.kind == 2 && R.Cin == R.Cs && dsc.dst_off >= R.lo && dsc.dst_off < R.hi) tr = &R;
+    }
+  }
+  bf16* tl = reinterpret_cast<bf16*>(red);
+  if (mine) {
+    float4 p = *reinterpret_cast<const float4*>(a.p + e);
+    float4 s0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : float4{0.f, 0.f, 0.f, 0.f};
+    float4 s1 = a.s1 ? *reinterpret_cast<const float4*>(a.s1 + e) : float4{0.f, 0.f, 0.f, 0.f};
+    const float gs = a.grad_scale;
+    opt_update<KIND>(a, a.st, p.x, g.x * gs, &s0.x, &s1.x);
+    opt_update<KIND>(a, a.st, p.y, g.y * gs, &s0.y, &s1.y);
+    opt_update<KIND>(a, a.st, p.z, g.z * gs, &s0.z, &s1.z);
+    opt_update<KIND>(a, a.st, p.w, g.w * gs, &s0.w, &s1.w);
+    *reinterpret_cast<float4*>(a.p + e) = p;
+    if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
+    if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
+    if (tr) {
+      bf16x4 v;
+      v[0] = f2bf(p.x); v[1] = f2bf(p.y); v[2] = f2bf(p.z); v[3] = f2bf(p.w);
+      *reinterpret_cast<bf16x4*>(tl + 4 * threadIdx.x) = v;
+    } else if (a.nroutes) {
+      pack_write4(a, e, p);
+    }
+  }
+  if (tr) {
+    __syncthreads();
+    const PackRoute R = *tr;
+    const int N = R.Cout, le0 = e_block0(dsc, blk) - R.lo, r0 = le0 / N;
+    const int t = threadIdx.x;
+    if (t < 128) {          // forward: 8 consecutive rows (k) of column n
+      const int gi = t / N, n = t - gi * N;
+      if (R.fwd >= 0) {
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = tl[(gi * 8 + j) * N + n];
+        *reinterpret_cast<bf16x8*>(a.arena + R.fwd + frag_off(r0 + gi * 8, n, R.NT)) = v;
+      }
+    } else if (R.bwd >= 0) {  // backward: 8 consecutive columns (n) of row k
+      const int v8 = t - 128, per = N >> 3, row = v8 / per, c8 = (v8 - row * per) * 8;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(tl + row * N + c8);
+      *reinterpret_cast<bf16x8*>(a.arena + R.bwd + frag_off(c8, r0 + row, R.NTb)) = v;
+    }
+  }
+}
+
+template <int KIND>
+__device__ __forceinline__ void update_elem(const OptimArgs& a, int e, float g) {
+  float p = a.p[e];
+  float s0 = a.s0 ? a.s0[e] : 0.f, s1 = a.s1 ? a.s1[e] : 0.f;
+  opt_update<KIND>(a, a.st, p, g * a.grad_scale, &s0, &s1);
+  a.p[e] = p;
+  if (a.s0) a.s0[e] = s0;
+  if (a.s1) a.s1[e] = s1;
+  if (a.nroutes) pack_write(a, e, p);
+}
+
 // Reduction + Keras update of table block `blk`: the thread that produces an element's
 // gradient writes it and applies the update at once.  `red`: 256 floats of LDS.  xp (grad_only
 // tables of the data-parallel step): also push the reduced elements to their owners.
@@ -128,73 +196,17 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
   if (dsc.vec4) {
     int e;
     float4 g;
-    // tiled pack writes (dsc.tile): the workgroup's 1024 updated weights are whole 8-row groups
-    // of its dense route -- staged as bf16 in LDS (red: >= 2 KB), written as 16-byte vectors
-    const PackRoute* tr = nullptr;
-    if (a.nroutes && dsc.tile && !a.grad_only) {
-      for (int r = 0; r < a.nroutes; ++r) {           // uniform: the descriptor's route
-        const PackRoute& R = a.routes[r];
-        if (R.kind == 2 && R.Cin == R.Cs && dsc.dst_off >= R.lo && dsc.dst_off < R.hi) tr = &R;
-      }
-    }
-    bf16* tl = reinterpret_cast<bf16*>(red);
     const bool mine = slab_reduce_vec4(dsc, blk, e, g);
     if (mine) *reinterpret_cast<float4*>(grad + e) = g;
     if (mine && xp) xpush4(*xp, e, g);
-    if (mine && !a.grad_only) {           // (grad_only: the reduced gradient is all)
-      float4 p = *reinterpret_cast<const float4*>(a.p + e);
-      float4 s0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : float4{0.f, 0.f, 0.f, 0.f};
-      float4 s1 = a.s1 ? *reinterpret_cast<const float4*>(a.s1 + e) : float4{0.f, 0.f, 0.f, 0.f};
-      const float gs = a.grad_scale;
-      opt_update<KIND>(a, a.st, p.x, g.x * gs, &s0.x, &s1.x);
-      opt_update<KIND>(a, a.st, p.y, g.y * gs, &s0.y, &s1.y);
-      opt_update<KIND>(a, a.st, p.z, g.z * gs, &s0.z, &s1.z);
-      opt_update<KIND>(a, a.st, p.w, g.w * gs, &s0.w, &s1.w);
-      *reinterpret_cast<float4*>(a.p + e) = p;
-      if (a.s0) *reinterpret_cast<float4*>(a.s0 + e) = s0;
-      if (a.s1) *reinterpret_cast<float4*>(a.s1 + e) = s1;
-      if (tr) {
-        bf16x4 v;
-        v[0] = f2bf(p.x); v[1] = f2bf(p.y); v[2] = f2bf(p.z); v[3] = f2bf(p.w);
-        *reinterpret_cast<bf16x4*>(tl + 4 * threadIdx.x) = v;
-      } else if (a.nroutes) {
-        pack_write4(a, e, p);
-      }
-    }
-    if (tr) {
-      __syncthreads();
-      const PackRoute R = *tr;
-      const int N = R.Cout, le0 = e_block0(dsc, blk) - R.lo, r0 = le0 / N;
-      const int t = threadIdx.x;
-      if (t < 128) {          // forward: 8 consecutive rows (k) of column n
-        const int gi = t / N, n = t - gi * N;
-        if (R.fwd >= 0) {
-          bf16x8 v;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = tl[(gi * 8 + j) * N + n];
-          *reinterpret_cast<bf16x8*>(a.arena + R.fwd + frag_off(r0 + gi * 8, n, R.NT)) = v;
-        }
-      } else if (R.bwd >= 0) {  // backward: 8 consecutive columns (n) of row k
-        const int v8 = t - 128, per = N >> 3, row = v8 / per, c8 = (v8 - row * per) * 8;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(tl + row * N + c8);
-        *reinterpret_cast<bf16x8*>(a.arena + R.bwd + frag_off(c8, r0 + row, R.NTb)) = v;
-      }
-    }
+    if (!a.grad_only) update_vec4<KIND>(dsc, a, blk, red, mine, e, g);   // (grad_only: the reduced gradient is all)
   } else {
     int e;
     float g;
     const bool mine = slab_reduce_elem(tab, blk, red, e, g);
     if (mine) grad[e] = g;
     if (mine && xp) xpush1(*xp, e, g);
-    if (mine && !a.grad_only) {
-      float p = a.p[e];
-      float s0 = a.s0 ? a.s0[e] : 0.f, s1 = a.s1 ? a.s1[e] : 0.f;
-      opt_update<KIND>(a, a.st, p, g * a.grad_scale, &s0, &s1);
-      a.p[e] = p;
-      if (a.s0) a.s0[e] = s0;
-      if (a.s1) a.s1[e] = s1;
-      if (a.nroutes) pack_write(a, e, p);
-    }
+    if (mine && !a.grad_only) update_elem<KIND>(a, e, g);
   }
   if (a.defer_pack && !a.nroutes && !a.grad_only && blk == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
 }

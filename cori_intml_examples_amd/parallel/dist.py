@@ -369,20 +369,21 @@ class GradReducer:
 def adaptive_bucket_bytes(groups: Sequence[Tuple[int, int]], size: int = 1) -> int:
     """Bucket size for the captured RCCL data plane.
 
-    * A real multi-rank job (size > 1): the first bucket closes after the backward-ordered
-      groups reach 1 MiB -- for the RPV model the head + dense gradient (2.1 MB, 96 % of the
-      bytes, final ~57 us before the backward ends) -- and every bucket's all-reduce is forked
-      onto the comm stream, where its optimizer update also runs: the dense layer's all-reduce
-      and Adam overlap the conv backward instead of trailing it (the small conv bucket is the
-      exposed tail).  At N = 1 (loopback) the forked plane costs the same as one bucket
-      (119.4 vs 119.1 us/step, profiles/r4_plane_probe_n1.json; profiles/r5_*_ab.txt).
-    * size 1 (INTML_DP_FORCE loopback runs) and gradients <= 16 MB otherwise: ONE fused
-      all-reduce at the end of the backward on the main stream -- a linear graph.
+    * Gradients <= 16 MB: ONE fused all-reduce at the end of the backward on the main stream
+      -- a linear graph.  (INTML_TUNE=dp_overlap=1, size > 1: the first bucket closes after
+      the backward-ordered groups reach 1 MiB -- for the RPV model the head + dense gradient,
+      96 % of the bytes -- and every bucket's all-reduce + update is forked onto the comm
+      stream, overlapping the conv backward.  Measured 135.7 vs 103.0 us/step at N = 1 on the
+      round-5 kernels, so it is not the default; the xGMI plane overlaps the dense bucket's
+      transfer inside the backward instead -- producer push.)
     * Larger gradients (the 34.5M-param legacy RPV model: 138 MB) get ~4 buckets of >= 16 MB,
       forked onto the comm stream so the all-reduces overlap the rest of the backward."""
     total = 4 * sum(hi - lo for lo, hi in groups)
     if total <= (16 << 20):
-        if size > 1 and total > (1 << 20) and tune("dp_overlap", True):
+        # (opt-in: on the round-5 kernels the forked two-bucket step measured 135.7 us/step at
+        # N = 1 against 103.0 for one bucket -- profiles/r5f_ab.txt; bench.py's probe times it
+        # on the real fabric at N > 1 and keeps whichever plane is faster)
+        if size > 1 and total > (1 << 20) and tune("dp_overlap", False):
             return 1 << 20
         return total + 1
     return max(16 << 20, total // 4)
