@@ -74,6 +74,31 @@ static void check_last(const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// host-side checks of an early-bucket xGMI push / exchange (XgmiPush, args.h) against its
+// reduction table: every pointer the device code dereferences, the block count its flags are
+// indexed by, and float4 groups that never straddle an owner chunk
+static void check_xgmi_push(const XgmiPush& x, const RedTable& t, const OptimArgs& a) {
+  if (x.size < 2 || x.size > XGMI_MAX_RANKS || x.rank < 0 || x.rank >= x.size || x.chunk <= 0 || x.chunk % 4)
+    throw std::invalid_argument("xgmi push: ranks / chunk");
+  if (x.mode != 1 && x.mode != 2) throw std::invalid_argument("xgmi push: mode");
+  if ((x.mode == 1) != (a.grad_only != 0))
+    throw std::invalid_argument("xgmi push: mode 1 needs a grad_only table, mode 2 an updating one");
+  const bool flags = x.mode == 2 || x.bflag1[0] != nullptr;
+  for (int j = 0; j < x.size; ++j) {
+    if (!x.inbox[j]) throw std::invalid_argument("xgmi push: inbox");
+    if (flags && !x.bflag1[j]) throw std::invalid_argument("xgmi push: block flags");
+    if (x.mode == 2 && (!x.outbox[j] || !x.bflag2[j] || !x.abort_[j])) throw std::invalid_argument("xgmi push: peers");
+  }
+  if (flags && (!x.ctrb || x.nblk != t.nblocks)) throw std::invalid_argument("xgmi push: block counters / nblk");
+  if (x.mode == 2 && (!x.err || x.timeout_ticks <= 0 || x.nx < 0)) throw std::invalid_argument("xgmi push: err / timeout");
+  for (int i = 0; i < t.n; ++i) {
+    const RedDesc& d = t.d[i];
+    if (d.dst_off < x.lo || d.dst_off + (long long)d.numel > x.lo + (long long)x.chunk * x.size)
+      throw std::invalid_argument("xgmi push: table outside the bucket");
+    if (d.vec4 && ((d.dst_off - x.lo) % 4 || d.numel % 4)) throw std::invalid_argument("xgmi push: float4 alignment");
+  }
+}
+
 PYBIND11_MODULE(_kernels, m) {
   m.doc() = "cori_intml_examples_amd gfx950 HIP kernels";
 
@@ -320,7 +345,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("gather_gx", &gather_gx);
   m.def("head_epi_max", &head_epi_max);
   m.def("reduce_optim", [](uintptr_t grad, const RedTable& t, const OptimArgs& a, uintptr_t s, const XgmiPush* xp) {
-    if (xp && xp->on && !a.grad_only) throw std::invalid_argument("producer push needs a grad_only table");
+    if (xp && xp->on) check_xgmi_push(*xp, t, a);
     launch_reduce_optim(reinterpret_cast<float*>(grad), t, a, S(s), xp); check_last("reduce_optim"); },
     py::arg("grad"), py::arg("t"), py::arg("a"), py::arg("s"), py::arg("xp") = nullptr);
   m.def("dense_bwd_dual", [](const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da, uintptr_t s) {
@@ -345,8 +370,9 @@ PYBIND11_MODULE(_kernels, m) {
           x.rt = *rt, x.ro = *ro, x.grad = reinterpret_cast<float*>(rgrad);
           x.n_r = rt->nblocks, x.rfirst = rfirst;
           if (xp && xp->on) {
-            if (!ro->grad_only) throw std::invalid_argument("producer push needs a grad_only table");
+            check_xgmi_push(*xp, *rt, *ro);
             x.xp = *xp;
+            if (xp->mode == 2 && xp->nx) x.n_r = xp->nx;   // (workgroups looping over the blocks)
           }
         }
         const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, x, S(s));
@@ -376,13 +402,24 @@ PYBIND11_MODULE(_kernels, m) {
   py::class_<XgmiPush>(m, "XgmiPush")
       .def(py::init<>())
       RW(XgmiPush, on) RW(XgmiPush, rank) RW(XgmiPush, size) RW(XgmiPush, chunk) RW(XgmiPush, lo)
+      RW(XgmiPush, mode) RW(XgmiPush, nblk) RW(XgmiPush, nx) RW(XgmiPush, timeout_ticks)
+      PTR(XgmiPush, ctrb) PTR(XgmiPush, err)
       .def("set_inbox", [](XgmiPush& x, int j, uintptr_t p) {
         if (j < 0 || j >= XGMI_MAX_RANKS) throw std::out_of_range("peer index");
         x.inbox[j] = reinterpret_cast<float*>(p);
+      })
+      .def("set_peer", [](XgmiPush& x, int j, uintptr_t inbox, uintptr_t outbox, uintptr_t bf1, uintptr_t bf2,
+                          uintptr_t ab) {
+        if (j < 0 || j >= XGMI_MAX_RANKS) throw std::out_of_range("peer index");
+        x.inbox[j] = reinterpret_cast<float*>(inbox);
+        x.outbox[j] = reinterpret_cast<float*>(outbox);
+        x.bflag1[j] = reinterpret_cast<unsigned*>(bf1);
+        x.bflag2[j] = reinterpret_cast<unsigned*>(bf2);
+        x.abort_[j] = reinterpret_cast<unsigned*>(ab);
       });
   py::class_<XgmiArgs>(m, "XgmiArgs")
       .def(py::init<>())
-      RW(XgmiArgs, skip_lo) RW(XgmiArgs, skip_hi)
+      RW(XgmiArgs, skip_lo) RW(XgmiArgs, skip_hi) RW(XgmiArgs, skip_mode)
       RW(XgmiArgs, rank) RW(XgmiArgs, size) RW(XgmiArgs, n) RW(XgmiArgs, chunk) RW(XgmiArgs, sub)
       RW(XgmiArgs, timeout_ticks) RW(XgmiArgs, mode) RW(XgmiArgs, fence) PTR(XgmiArgs, grad) PTR(XgmiArgs, ctr) PTR(XgmiArgs, err)
       RW(XgmiArgs, opt)

@@ -362,19 +362,20 @@ __global__ __launch_bounds__(256) void reduce_optim_kernel(float* __restrict__ g
   reduce_optim_block<KIND>(grad, tab, a, blockIdx.x, red);
 }
 
-// the early bucket's reduction + producer push as a launch of its own (the dual launch that
-// normally carries it declined: ablation / stamp args)
-__global__ __launch_bounds__(256) void reduce_push_kernel(float* __restrict__ grad, const RedTable tab,
-                                                          const OptimArgs a, const XgmiPush xp) {
-  __shared__ __attribute__((aligned(16))) float red[512];
-  reduce_push_block(grad, tab, a, blockIdx.x, red, xp);
+// the early bucket's reduction + producer push (mode 1) or exchange + update (mode 2) as a
+// launch of its own (the dual launch that normally carries it declined: ablation / stamp args)
+__global__ __launch_bounds__(256) void xgmi_early_kernel(float* __restrict__ grad, const RedTable tab,
+                                                         const OptimArgs a, const XgmiPush xp) {
+  __shared__ __attribute__((aligned(16))) float red[1024];   // (mode 2: the wait word at [1023])
+  xgmi_early_block(grad, tab, a, blockIdx.x, red, xp);
 }
 
 void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, hipStream_t s,
                          const XgmiPush* xp) {
   if (tab.nblocks <= 0) return;
   if (xp && xp->on) {
-    hipLaunchKernelGGL(reduce_push_kernel, dim3(tab.nblocks), dim3(256), 0, s, grad, tab, a, *xp);
+    const int grid = xp->mode == 2 && xp->nx ? xp->nx : tab.nblocks;
+    hipLaunchKernelGGL(xgmi_early_kernel, dim3(grid), dim3(256), 0, s, grad, tab, a, *xp);
     return;
   }
   const dim3 g(tab.nblocks), b(256);

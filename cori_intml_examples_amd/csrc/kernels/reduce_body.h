@@ -211,11 +211,178 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
   if (a.defer_pack && !a.nroutes && !a.grad_only && blk == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
 }
 
-// data-parallel early bucket (a grad_only table): reduction + producer push, no update
+// ---------------------------------------------------------------- xGMI early-bucket exchange
+// (XgmiPush, args.h).  The peer buffers are uncached device memory: the protocol is xgmi.hip's
+// (payload stores drained before a relaxed system-scope flag store; bounded relaxed polls; the
+// payload read with sc1 loads that bypass this CU's L1) -- see that file's header.
+__device__ __forceinline__ unsigned xs_load(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void xs_store(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool xs_set_err(int* err, int v) {
+  int zero = 0;
+  return __hip_atomic_compare_exchange_strong(err, &zero, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// n (1 or 4) floats at base[idx] of a peer-written buffer (sc1: not from this CU's L1)
+__device__ __forceinline__ float4 xs_peer(const float* base, size_t idx, int n) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+  if (n == 4) return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(idx * 4), 0, 16));
+  return float4{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (unsigned)(idx * 4), 0, 16)), 0.f,
+                0.f, 0.f};
+}
+__device__ __forceinline__ float4 xs_local(const float* p, int n) {
+  return n == 4 ? *reinterpret_cast<const float4*>(p) : float4{*p, 0.f, 0.f, 0.f};
+}
+__device__ __forceinline__ void xs_put(float* p, const float4& v, int n) {
+  if (n == 4) *reinterpret_cast<float4*>(p) = v;
+  else *p = v.x;
+}
+__device__ __forceinline__ void xs_drain_sync() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+// Lanes q < size with bit q of `mask` wait until flags[q] >= seq -- bounded in time, with
+// xgmi.hip wait_all's failure protocol (a timeout records `phase` and raises every rank's
+// sticky abort word; a raised abort word ends the wait as err 3).  Every thread calls it;
+// false on failure.  s_ok: one int of LDS no other code of the block touches meanwhile.
+__device__ __forceinline__ bool xs_wait(const XgmiPush& x, const unsigned* flags, unsigned mask, unsigned seq,
+                                        int phase, int* s_ok) {
+  const int t = threadIdx.x;
+  if (t == 0) *s_ok = 1;
+  __syncthreads();
+  if (t < x.size && ((mask >> t) & 1u)) {
+    const unsigned long long t0 = wall_clock64();
+    while (xs_load(flags + t) < seq) {
+      if (xs_load(x.abort_[x.rank])) {
+        *s_ok = 0;
+        xs_set_err(x.err, 3);
+        break;
+      }
+      if ((long long)(wall_clock64() - t0) > x.timeout_ticks) {
+        *s_ok = 0;
+        if (xs_set_err(x.err, phase)) {
+          x.err[1] = (int)seq;
+          x.err[2] = (int)xs_load(flags + t);
+          x.err[3] = (int)blockIdx.x * 64 + t;
+        }
+        for (int j = 0; j < x.size; ++j) xs_store(x.abort_[j], 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (keeps the sc1 loads below the poll)
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+
+// data-parallel early bucket (a grad_only table), mode 1: reduction + producer push, no
+// update; with block flags (exchange), the block's push flag is raised on every peer
 __device__ __forceinline__ void reduce_push_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
                                                   int blk, float* red, const XgmiPush& xp) {
   reduce_optim_block<OPT_SGD>(grad, tab, a, blk, red, &xp);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the pushes complete with this workgroup
+  if (xp.bflag1[0] == nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the pushes complete with this workgroup
+    return;
+  }
+  const unsigned seq = xp.ctrb[blk] + 1u;
+  xs_drain_sync();
+  const int t = threadIdx.x;
+  if (t < xp.size && t != xp.rank) xs_store(xp.bflag1[t] + (size_t)blk * xp.size + xp.rank, seq);
+}
+
+// mode 2: finish the all-reduce of table block `blk` (pushed by mode 1 of an earlier launch on
+// every rank) and apply its Keras update.  Element ownership and summation order are the fused
+// all-reduce kernel's (owner chunks of x.chunk bucket elements; rows summed in rank order, the
+// owner's own row from grad), so the sums are those the end-of-step kernel would produce.
+template <int KIND>
+__device__ void xchg_update_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a, int blk,
+                                  float* red, const XgmiPush& x) {
+  const RedDesc& d = tab.d[red_desc(tab, blk)];
+  const int P = x.size, me = x.rank, t = threadIdx.x, C = x.chunk;
+  const unsigned seq = x.ctrb[blk] + 1u;
+  int* s_ok = reinterpret_cast<int*>(red) + 1023;   // (past update_vec4's 2 KB tile stage)
+  // the block's elements [b_lo, b_hi) and this thread's n elements at e (the reduce map)
+  int b_lo, b_hi, e = 0, n = 0;
+  if (d.vec4) {
+    b_lo = e_block0(d, blk);
+    b_hi = min(b_lo + 1024, d.dst_off + d.numel);
+    if (b_lo + 4 * t < b_hi) e = b_lo + 4 * t, n = 4;
+  } else {
+    const int E = 256 / d.tpe;   // (slab_reduce_elem: thread t < E holds element t)
+    b_lo = d.dst_off + (blk - d.blk0) * E;
+    b_hi = min(b_lo + E, d.dst_off + d.numel);
+    if (t < E && b_lo + t < b_hi) e = b_lo + t, n = 1;
+  }
+  const int j0 = (int)((b_lo - x.lo) / C), j1 = (int)((b_hi - 1 - x.lo) / C);
+  const long long ie = (long long)e - x.lo;     // bucket index
+  const int own = n ? (int)(ie / C) : -1;
+  float4 g = {0.f, 0.f, 0.f, 0.f};
+  if (me >= j0 && me <= j1) {
+    // the owner part: every sender's row of the block is in my inbox
+    if (!xs_wait(x, x.bflag1[me] + (size_t)blk * P, ~(1u << me), seq, 4, s_ok)) return;
+    if (own == me) {
+      const size_t k = (size_t)(ie - (long long)me * C);
+      float4 v[XGMI_MAX_RANKS];
+#pragma unroll
+      for (int q = 0; q < XGMI_MAX_RANKS; ++q)
+        if (q < P) v[q] = q == me ? xs_local(grad + e, n) : xs_peer(x.inbox[me], (size_t)q * C + k, n);
+      g = v[0];
+#pragma unroll
+      for (int q = 1; q < XGMI_MAX_RANKS; ++q)
+        if (q < P) g.x += v[q].x, g.y += v[q].y, g.z += v[q].z, g.w += v[q].w;
+      xs_put(grad + e, g, n);
+#pragma unroll
+      for (int j = 0; j < XGMI_MAX_RANKS; ++j)
+        if (j < P && j != me) xs_put(x.outbox[j] + ie, g, n);
+    }
+    xs_drain_sync();
+    if (t < P && t != me) xs_store(x.bflag2[t] + (size_t)blk * P + me, seq);
+  }
+  // the other owners' sums of this block's elements are in my outbox
+  unsigned need = 0;
+  for (int j = j0; j <= j1; ++j)
+    if (j != me) need |= 1u << j;
+  if (need) {
+    if (!xs_wait(x, x.bflag2[me] + (size_t)blk * P, need, seq, 5, s_ok)) return;
+    if (n && own != me) {
+      g = xs_peer(x.outbox[me], (size_t)ie, n);
+      xs_put(grad + e, g, n);
+    }
+  }
+  if (d.vec4) update_vec4<KIND>(d, a, blk, red, n == 4, e, g);
+  else if (n) update_elem<KIND>(a, e, g.x);
+  if (a.defer_pack && !a.nroutes && blk == 0 && t == 0) a.st->packs_stale = 1;
+  if (t == 0) x.ctrb[blk] = seq;
+}
+
+// the data-parallel early-bucket workgroup r of a launch (mode 1: one table block each; mode 2:
+// one block each, or x.nx workgroups looping over the blocks in order -- ranks sharing a GPU)
+__device__ __forceinline__ void xgmi_early_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
+                                                 int r, float* red, const XgmiPush& x) {
+  if (x.mode != 2) {
+    reduce_push_block(grad, tab, a, r, red, x);
+    return;
+  }
+  if (xs_load(x.abort_[x.rank])) {   // sticky abort (an earlier wait timed out): touch nothing
+    if (threadIdx.x == 0) xs_set_err(x.err, 3);
+    return;
+  }
+  const int step = x.nx ? x.nx : x.nblk;
+  for (int b = r; b < x.nblk; b += step) {
+    switch (a.kind) {
+      case OPT_ADAM: xchg_update_block<OPT_ADAM>(grad, tab, a, b, red, x); break;
+      case OPT_NADAM: xchg_update_block<OPT_NADAM>(grad, tab, a, b, red, x); break;
+      case OPT_ADADELTA: xchg_update_block<OPT_ADADELTA>(grad, tab, a, b, red, x); break;
+      case OPT_RMSPROP: xchg_update_block<OPT_RMSPROP>(grad, tab, a, b, red, x); break;
+      default: xchg_update_block<OPT_SGD>(grad, tab, a, b, red, x); break;
+    }
+    __syncthreads();   // (the next block reuses red)
+  }
 }
 
 // the same with the optimizer kind chosen at run time (a workgroup-uniform switch)

@@ -123,14 +123,24 @@ __device__ __forceinline__ float4 load4_guarded(const float* p, long long idx, l
   return v;
 }
 
+// skip_mode 2: bucket elements [skip_lo, skip_hi) were all-reduced and updated inside the
+// backward (XgmiPush exchange): no phase touches them
+__device__ __forceinline__ bool xchg_done(const XgmiArgs& a, long long e) {
+  return a.skip_mode == 2 && e >= a.skip_lo && e < a.skip_hi;
+}
+__device__ __forceinline__ bool xchg_done4(const XgmiArgs& a, long long e) {
+  return a.skip_mode == 2 && e >= a.skip_lo && e + 4 <= a.skip_hi;
+}
+
 // grad[idx .. idx+4) = g4 (the reduced SUM) and, in mode 1, the Keras update of those
-// parameters with the 1/size average folded in (elements past n skipped)
+// parameters with the 1/size average folded in (elements past n, and exchanged ones, skipped)
 template <int KIND>
 __device__ __forceinline__ void finish4(const XgmiArgs& a, float* __restrict__ grad, long long idx, long long n,
                                         const float4 g4) {
   if (idx >= n) return;
   const OptimArgs& o = a.opt;
-  if (idx + 4 <= n) {       // float4 path (idx, C, k multiples of 4: 16-byte aligned)
+  const bool part = a.skip_mode == 2 && idx + 4 > a.skip_lo && idx < a.skip_hi;   // (straddles the range)
+  if (idx + 4 <= n && !part) {       // float4 path (idx, C, k multiples of 4: 16-byte aligned)
     *reinterpret_cast<float4*>(grad + idx) = g4;
     if (a.mode == 1) {
       float4 p4 = *reinterpret_cast<const float4*>(o.p + idx);
@@ -149,7 +159,8 @@ __device__ __forceinline__ void finish4(const XgmiArgs& a, float* __restrict__ g
     return;
   }
   const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
-  for (int e = 0; e < (int)(n - idx); ++e) {
+  for (int e = 0; e < (int)min(n - idx, 4LL); ++e) {
+    if (xchg_done(a, idx + e)) continue;
     grad[idx + e] = gv[e];
     if (a.mode == 1) {
       float pe = o.p[idx + e];
@@ -215,6 +226,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
     const float* __restrict__ in = a.inbox[r];
     for (int k = k0 + 4 * t; k < k1; k += 1024) {
       const long long own = (long long)r * C + k;
+      if (xchg_done4(a, own)) continue;
       float4 v[XGMI_MAX_RANKS];
 #pragma unroll
       for (int q = 0; q < XGMI_MAX_RANKS; ++q)
@@ -239,10 +251,10 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(const XgmiArgs a) {
       float4 g[XGMI_MAX_RANKS];
 #pragma unroll
       for (int q = 0; q < XGMI_MAX_RANKS; ++q)
-        if (q < P && q != r) g[q] = load_peer4(red, (size_t)q * C + k, a.fence);
+        if (q < P && q != r && !xchg_done4(a, (long long)q * C + k)) g[q] = load_peer4(red, (size_t)q * C + k, a.fence);
 #pragma unroll
       for (int q = 0; q < XGMI_MAX_RANKS; ++q)
-        if (q < P && q != r) finish4<KIND>(a, grad, (long long)q * C + k, n, g[q]);
+        if (q < P && q != r && !xchg_done4(a, (long long)q * C + k)) finish4<KIND>(a, grad, (long long)q * C + k, n, g[q]);
     }
   }
   if (a.mode == 1 && a.opt.defer_pack && !a.opt.nroutes && w == 0 && t == 0) a.opt.st->packs_stale = 1;

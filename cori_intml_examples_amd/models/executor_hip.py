@@ -1028,6 +1028,7 @@ class BatchPlan(GeometryMixin):
         groups = [(lo, hi) for lo, hi, _ in self.red_groups]
         reducer = ex.reducer
         dp_early = []
+        self.early_push, self.pushed, self.early_xchg, self.exchanged = {}, None, {}, False
         if reducer is not None:
             bucket_groups = reducer.configure(groups)
             # one bucket at the end of the backward (the adaptive plan for gradients <= 16 MB):
@@ -1040,10 +1041,20 @@ class BatchPlan(GeometryMixin):
                 # producer push (xGMI plane): the early groups' reduced gradient goes straight to
                 # its owners' inboxes from the launch that reduces it, inside the backward, and
                 # the fused all-reduce kernel skips those elements in its phase 1
-                self.early_push, self.pushed = {}, None
+                # ... and (exchange) the NEXT dual launch finishes that range's all-reduce and
+                # applies its update in extra workgroups of its own, so the fused kernel after
+                # the backward is left with the conv layers only
                 if tune("xgmi_push", True):
                     for nm, (tab_, (elo, ehi), go) in self.early_red.items():
-                        xp = reducer.push_args(elo, ehi) if go else None
+                        if not go:
+                            continue
+                        nxt = self._xchg_launch(nm, elo, ehi) if tune("xgmi_xchg", True) else None
+                        pair = reducer.exchange_args(elo, ehi, tab_.nblocks) if nxt else None
+                        if pair is not None:
+                            self.early_push[nm], self.early_xchg[nxt] = pair[0], (tab_, pair[1])
+                            self.pushed, self.exchanged = (elo, ehi), True
+                            continue
+                        xp = reducer.push_args(elo, ehi)
                         if xp is not None:
                             self.early_push[nm], self.pushed = xp, (elo, ehi)
         else:
@@ -1110,7 +1121,8 @@ class BatchPlan(GeometryMixin):
             # the xGMI bucket: all-reduce + Keras update in one kernel on the main stream
             extra.append(("xgmi_allreduce_optim_b%d", lambda k: None if k != xk else
                           (lambda s: reducer.launch_fused(ex.store.grad, ex._optim_args(False, defer_pack=True), s,
-                                                          pushed=getattr(self, "pushed", None))),
+                                                          pushed=getattr(self, "pushed", None),
+                                                          exchanged=getattr(self, "exchanged", False))),
                           "main"))
         self.launches, self.bucket_ready = splice_bucket_launches(
             self.launches, inserts,
@@ -1171,6 +1183,20 @@ class BatchPlan(GeometryMixin):
             self.early_red[names[t]] = (tab, (lo, hi), grad_only)
             taken += grp
         return taken
+
+    def _xchg_launch(self, name, lo, hi):
+        """The dual launch after ``name`` that can run the exchange (all-reduce finish + update)
+        of the early range [lo, hi): the next dual backward launch, provided no launch from it
+        on reads the range's bf16 packs (the update rewrites them).  None if there is none."""
+        names = [it[0] for it in self.launches]
+        i = names.index(name)
+        nxt = [j for j in range(i + 1, len(names)) if names[j].startswith("wgrad_dgrad_conv")]
+        if not nxt:
+            return None
+        later = set(names[nxt[0]:])
+        if any(nm in later and rlo < hi and rhi > lo for nm, rlo, rhi in self.pack_readers):
+            return None
+        return names[nxt[0]]
 
     def _launch_optim_comm(self, k, stream):
         """Keras update of bucket k's parameters on the comm stream after its all-reduce;

@@ -222,17 +222,22 @@ class GeometryMixin:
         K, ex = self.ex.K, self.ex
         early = (self.early_red or {}).get(name)
         xp = (getattr(self, "early_push", None) or {}).get(name)   # producer push (xGMI plane)
+        # exchange (xGMI plane): this launch finishes an earlier launch's pushed range -- its
+        # all-reduce + Keras update in extra workgroups (XgmiPush mode 2)
+        xe = (getattr(self, "early_xchg", None) or {}).get(name)
         kw = {}
         if early is not None:   # this launch also carries an early bucket's reduction (+ optimizer)
             kw.update(rt=early[0], ro=self._early_ro(early), rgrad=ex.store.grad.data_ptr())
             if xp is not None:
                 kw["xp"] = xp
+        elif xe is not None:
+            kw.update(rt=xe[0], ro=ex._optim_args(False, defer_pack=True), rgrad=ex.store.grad.data_ptr(), xp=xe[1])
         ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, **kw)
         if not ok:   # unsupported combination
             K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
             K.conv_halo(a, ntc, s)
-            if early is not None:
-                K.reduce_optim(ex.store.grad.data_ptr(), early[0], self._early_ro(early), s, xp)
+            if kw:
+                K.reduce_optim(kw["rgrad"], kw["rt"], kw["ro"], s, kw.get("xp"))
 
     def _early_ro(self, early):
         """OptimArgs of an early reduction table: the Keras update, or (data-parallel step,

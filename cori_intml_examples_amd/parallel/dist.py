@@ -485,6 +485,7 @@ class NativeGradReducer:
             max_wg = int(tune("xgmi_shared_wg", 8)) if shared else None
             self.xgmi = X.create(self.rank, self.size, n, self.device, allgather, max_wg=max_wg)
             if self.xgmi is not None:
+                self.xgmi.shared = shared
                 self._xgmi_err_host = torch.zeros(4, dtype=torch.int32).pin_memory()
         if self.xgmi is not None:
             self.xgmi_bucket = k
@@ -492,24 +493,40 @@ class NativeGradReducer:
             raise RuntimeError("data parallel without RCCL (INTML_COMM=xgmi, or ranks sharing a GPU): the "
                                "fused xGMI all-reduce failed its collective setup / self-test (see stderr)")
 
-    def launch_fused(self, grad: torch.Tensor, opt_args, stream: int, pushed=None) -> None:
+    def launch_fused(self, grad: torch.Tensor, opt_args, stream: int, pushed=None, exchanged=False) -> None:
         """The fused all-reduce + optimizer of the xGMI bucket (capturable); ``opt_args``
         cover the whole flat buffer and are offset to the bucket here.  ``pushed``: the flat
-        (lo, hi) range the backward already pushed to its owners (push_args)."""
+        (lo, hi) range the backward already pushed to its owners (push_args); ``exchanged``:
+        that range was also all-reduced and updated in the backward (exchange_args)."""
         from . import xgmi as X
         lo, _ = self.buckets[self.xgmi_bucket]
         skip = (pushed[0] - lo, pushed[1] - lo) if pushed else (0, 0)
-        self.xgmi.launch(grad.data_ptr() + 4 * lo, stream, opt=X.offset_optim(opt_args, lo), skip=skip)
+        self.xgmi.launch(grad.data_ptr() + 4 * lo, stream, opt=X.offset_optim(opt_args, lo), skip=skip,
+                         exchanged=bool(pushed) and exchanged)
 
     def push_args(self, lo: int, hi: int):
         """XgmiPush for an early range [lo, hi) finalised inside the backward, when it lies in
         the xGMI bucket and there are peers to push to; else None."""
+        blo = self._xgmi_lo(lo, hi)
+        return None if blo is None else self.xgmi.push_args(blo)
+
+    def exchange_args(self, lo: int, hi: int, nblk: int):
+        """(push, exchange) XgmiPush pair for an early range [lo, hi) whose reduction table has
+        ``nblk`` blocks: the launch that reduces it pushes + flags (mode 1), a later backward
+        launch finishes its all-reduce and applies its update (mode 2); None when the range
+        is not in the xGMI bucket, there are no peers, or the flags cannot cover the table."""
+        blo = self._xgmi_lo(lo, hi)
+        if blo is None:
+            return None
+        x1 = self.xgmi.push_args(blo, mode=1, nblk=nblk)
+        x2 = self.xgmi.push_args(blo, mode=2, nblk=nblk)
+        return None if x1 is None or x2 is None else (x1, x2)
+
+    def _xgmi_lo(self, lo: int, hi: int):
         if self.xgmi is None or self.xgmi_bucket is None:
             return None
         blo, bhi = self.buckets[self.xgmi_bucket]
-        if lo < blo or hi > bhi:
-            return None
-        return self.xgmi.push_args(blo)
+        return None if lo < blo or hi > bhi else blo
 
     def launch(self, bucket: int, grad: torch.Tensor, stream: torch.cuda.Stream) -> None:
         """Enqueue bucket ``bucket``'s all-reduce on ``stream`` (capturable)."""

@@ -34,6 +34,7 @@ from ..ops.hip import kernels
 from ..utils.env import tune
 
 _FLAG_WORDS = 256 * 8          # XGMI_MAX_WG x XGMI_MAX_RANKS
+XCHG_MAX_BLOCKS = 4096         # early-bucket exchange: table blocks with flags (x XGMI_MAX_RANKS)
 _TICKS_PER_S = 100_000_000     # wall_clock64 (s_memrealtime) runs at 100 MHz on gfx950
 
 
@@ -81,10 +82,13 @@ class XgmiAllreduce:
             raise ValueError("xgmi all-reduce supports at most %d ranks" % K.XGMI_MAX_RANKS)
         self.chunk, self.sub, self.grid = geometry(n, size, min(max_wg or K.XGMI_MAX_WG, K.XGMI_MAX_WG))
         words = self.chunk * size
-        # layout (bytes): flag1 | flag2 | abort word | inbox [P][chunk] fp32 | outbox [P*chunk] fp32
+        # layout (bytes): flag1 | flag2 | abort word | block flags 1 | block flags 2 (the early
+        # bucket's exchange, XgmiPush) | inbox [P][chunk] fp32 | outbox [P*chunk] fp32
         self.off_f1, self.off_f2 = 0, 4 * _FLAG_WORDS
         self.off_ab = self.off_f2 + 4 * _FLAG_WORDS
-        self.off_in = _align(self.off_ab + 256, 256)
+        self.off_bf1 = _align(self.off_ab + 256, 256)
+        self.off_bf2 = self.off_bf1 + 4 * XCHG_MAX_BLOCKS * 8
+        self.off_in = _align(self.off_bf2 + 4 * XCHG_MAX_BLOCKS * 8, 256)
         self.off_out = _align(self.off_in + 4 * words, 256)
         self.nbytes = _align(self.off_out + 4 * words, 4096)
         self.buf = 0
@@ -112,6 +116,8 @@ class XgmiAllreduce:
             except Exception as e:    # noqa: BLE001
                 err = "ipc: %s" % e
         self.ctr = torch.zeros(K.XGMI_MAX_WG, dtype=torch.int32, device=device)
+        self.ctrb = torch.zeros(XCHG_MAX_BLOCKS, dtype=torch.int32, device=device)   # exchange blocks
+        self.shared = False            # ranks share a GPU (set by the reducer): looping exchange WGs
         self.err = torch.zeros(4, dtype=torch.int32, device=device)   # code, seq, seen, wg*64+peer
         a = K.XgmiArgs()
         a.rank, a.size, a.n, a.chunk, a.sub = rank, size, n, self.chunk, self.sub
@@ -129,25 +135,41 @@ class XgmiAllreduce:
         self.setup_error = err
 
     # ------------------------------------------------------------------ launches
-    def push_args(self, lo: int = 0):
+    def push_args(self, lo: int = 0, mode: int = 1, nblk: int = 0):
         """XgmiPush for the kernels that finalise part of this all-reduce's bucket inside the
-        backward (the early head / dense reduction): they store each reduced element straight
-        into its owner's inbox row -- phase 1 of the all-reduce, overlapping the rest of the
-        backward.  ``lo``: the bucket's first flat element.  None at size 1 (nothing to push)."""
-        if self.size < 2 or not self.bases:
+        backward (the early head / dense reduction).  mode 1: they store each reduced element
+        straight into its owner's inbox row -- phase 1 of the all-reduce, overlapping the rest
+        of the backward; with ``nblk`` (the table's blocks) they also raise per-block flags for
+        an exchange.  mode 2 (the exchange, a later backward launch): the owners sum the rows
+        and send the sums back, and every rank applies the update -- the range's whole
+        all-reduce + optimizer inside the backward (args.h XgmiPush).  ``lo``: the bucket's
+        first flat element.  None at size 1 (nothing to push) or past the flag capacity."""
+        if self.size < 2 or not self.bases or nblk > XCHG_MAX_BLOCKS:
             return None
         x = self.K.XgmiPush()
         x.on, x.rank, x.size, x.chunk, x.lo = 1, self.rank, self.size, self.chunk, int(lo)
+        x.mode = mode
         for j, b in enumerate(self.bases):
-            x.set_inbox(j, b + self.off_in)
+            if nblk:
+                x.set_peer(j, b + self.off_in, b + self.off_out, b + self.off_bf1, b + self.off_bf2, b + self.off_ab)
+            else:
+                x.set_inbox(j, b + self.off_in)
+        if nblk:
+            x.nblk, x.ctrb, x.err = nblk, self.ctrb.data_ptr(), self.err.data_ptr()
+            x.timeout_ticks = self.args.timeout_ticks
+            # ranks sharing a GPU: a few workgroups looping over the blocks (one per block would
+            # let one rank's spinning workgroups fill the CUs its peers' launches need)
+            x.nx = int(tune("xgmi_xchg_wg", 4)) if (mode == 2 and self.shared) else 0
         return x
 
-    def launch(self, grad: int, stream: int, opt=None, skip=(0, 0)) -> None:
+    def launch(self, grad: int, stream: int, opt=None, skip=(0, 0), exchanged: bool = False) -> None:
         """Enqueue the fused all-reduce on `stream` (capturable): the reduced SUM lands in
         `grad`; with `opt` (OptimArgs, grad_scale = 1/size) the Keras update follows.
-        ``skip``: bucket-relative element range already pushed by the backward (push_args)."""
+        ``skip``: bucket-relative element range already pushed by the backward (push_args);
+        ``exchanged``: ... and also all-reduced and updated there (mode-2 exchange)."""
         a = self.args
         a.skip_lo, a.skip_hi = int(skip[0]), int(skip[1])
+        a.skip_mode = 2 if exchanged else 0
         a.grad = grad
         if opt is not None:
             a.mode, a.opt = 1, opt

@@ -86,6 +86,8 @@ def run(opt, lr, outdir, r, P, dev):
     # backward and push them to their owners' inboxes, and the range the all-reduce skips
     rep["push_launches"] = sorted((getattr(plan, "early_push", None) or {}).keys())
     rep["pushed"] = list(getattr(plan, "pushed", None) or [])
+    rep["xchg_launches"] = sorted((getattr(plan, "early_xchg", None) or {}).keys())
+    rep["exchanged"] = bool(getattr(plan, "exchanged", False))
     rep["err"] = int(red.xgmi.err[0].item()) if red.xgmi is not None else -1
     rep["digest"] = hashlib.sha256(w.tobytes()).hexdigest()
     rep["finite"] = bool(np.isfinite(w).all())

@@ -219,8 +219,8 @@ def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
     all on GPU 0, so the RCCL-free plane is chosen on its own) train 24 captured steps (3
     replays x 8) at per-rank batch 128/P through the fused xGMI all-reduce + optimizer
     kernel, with Adam and with SGD -- the head / dense gradient pushed to its owners by the
-    first dual backward launch (producer push), the rest by the all-reduce
-    kernel: no wait times out, every rank ends with bit-identical weights, and those match a
+    first dual backward launch (producer push) and all-reduced + updated by the
+    next one (exchange), the rest by the all-reduce kernel: no wait times out, every rank ends with bit-identical weights, and those match a
     single-process run at global batch 128 from the same weights and permutation (SGD within
     fp32 reordering; Adam within its sign-flip bound)."""
     env = dict(os.environ, PYTHONPATH=ROOT, INTML_DP_TIMEOUT="60")
@@ -250,6 +250,9 @@ def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
             assert rep["err"] == 0 and rep["finite"] and rep["moved"] > 1e-4, rep
             # the dense / head gradient was pushed to its owners from inside the backward
             assert rep["push_launches"] == ["wgrad_dgrad_conv2"] and rep["pushed"][1] > rep["pushed"][0], rep
+            # ... and all-reduced + updated by the next one (exchange): the fused kernel after the
+            # backward only had the conv layers left
+            assert rep["xchg_launches"] == ["wgrad_dgrad_conv1"] and rep["exchanged"], rep
     for opt in ("Adam", "SGD"):
         assert len({top[opt]["digest"] for top in reps}) == 1, [top[opt]["digest"] for top in reps]
     # SGD: linear in the gradient -- the per-rank partial sums and the all-reduce reorder the
