@@ -293,18 +293,6 @@ struct HeadArgs {
   int generic = 0;
 };
 
-// The last hidden dense layer + the binary output head in one launch (dense_head.hip):
-// 16-row x 16-column output tiles over 1/kh of K per 16-wave workgroup, the last arriving
-// workgroup of each 16-row group finishing the layer and running the head for those rows.
-struct DenseHeadArgs {
-  DenseFwdArgs f;                // x, wpk, NT, KS, Ks, M; part: the fp32 tile partials
-                                 // [kh][M][NT*16]; book / sb: the step bookkeeping
-  HeadArgs h;                    // the head; h.epi: the dense layer's epilogue (bias, ReLU,
-                                 // dropout, out)
-  unsigned* ticket = nullptr;    // [row groups + 1] monotonic arrival counters (zeroed once)
-  int kh = 2;                    // workgroups along K per output tile
-};
-
 struct GatherArgs {
   const bf16* xs = nullptr;      // dataset [Nd][R] bf16
   const float* ys = nullptr;     // [Nd][C]
@@ -381,7 +369,8 @@ struct XgmiPush {
   int on = 0, rank = 0, size = 1, chunk = 0;
   long long lo = 0;                      // first flat element of the all-reduce bucket
   float* inbox[XGMI_MAX_RANKS] = {};     // rank j's inbox [P][chunk] (as mapped here)
-  int mode = 1;                          // 1 reduce + push (+ block flags), 2 exchange + update
+  int mode = 1;                          // 1 reduce + push (+ block flags), 2 exchange + update,
+                                         // 3 both in one launch (the end-of-backward bucket)
   float* outbox[XGMI_MAX_RANKS] = {};    // rank j's outbox [P * chunk] (bucket index)
   unsigned* bflag1[XGMI_MAX_RANKS] = {}; // rank j's per-block push flags [nblk][P] (null: no flags)
   unsigned* bflag2[XGMI_MAX_RANKS] = {}; // rank j's per-block owner-sum flags [nblk][P]

@@ -29,8 +29,6 @@ void launch_dense_epi(const DenseEpiArgs& a, hipStream_t s);
 int dense_groups(int M, int NT, int KS);
 bool dense_big(int NT, int KS);
 void launch_head(const HeadArgs& a, hipStream_t s);
-void launch_dense_head(const DenseHeadArgs& a, hipStream_t s);
-int dense_head_blocks(const DenseHeadArgs& a);
 bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT, int NTT, int splits,
                       const DualExtra& x, hipStream_t s);
 bool launch_dense_bwd_dual(const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da,
@@ -78,19 +76,20 @@ static void check_last(const char* what) {
 // reduction table: every pointer the device code dereferences, the block count its flags are
 // indexed by, and float4 groups that never straddle an owner chunk
 static void check_xgmi_push(const XgmiPush& x, const RedTable& t, const OptimArgs& a) {
-  if (x.size < 2 || x.size > XGMI_MAX_RANKS || x.rank < 0 || x.rank >= x.size || x.chunk <= 0 || x.chunk % 4)
+  if (x.size < 1 || x.size > XGMI_MAX_RANKS || x.rank < 0 || x.rank >= x.size || x.chunk <= 0 || x.chunk % 4)
     throw std::invalid_argument("xgmi push: ranks / chunk");
-  if (x.mode != 1 && x.mode != 2) throw std::invalid_argument("xgmi push: mode");
+  if (x.mode < 1 || x.mode > 3) throw std::invalid_argument("xgmi push: mode");
+  if (x.size == 1 && x.mode == 1 && !x.bflag1[0]) throw std::invalid_argument("xgmi push: nothing to push");
   if ((x.mode == 1) != (a.grad_only != 0))
     throw std::invalid_argument("xgmi push: mode 1 needs a grad_only table, mode 2 an updating one");
-  const bool flags = x.mode == 2 || x.bflag1[0] != nullptr;
+  const bool flags = x.mode >= 2 || x.bflag1[0] != nullptr;
   for (int j = 0; j < x.size; ++j) {
     if (!x.inbox[j]) throw std::invalid_argument("xgmi push: inbox");
     if (flags && !x.bflag1[j]) throw std::invalid_argument("xgmi push: block flags");
-    if (x.mode == 2 && (!x.outbox[j] || !x.bflag2[j] || !x.abort_[j])) throw std::invalid_argument("xgmi push: peers");
+    if (x.mode >= 2 && (!x.outbox[j] || !x.bflag2[j] || !x.abort_[j])) throw std::invalid_argument("xgmi push: peers");
   }
   if (flags && (!x.ctrb || x.nblk != t.nblocks)) throw std::invalid_argument("xgmi push: block counters / nblk");
-  if (x.mode == 2 && (!x.err || x.timeout_ticks <= 0 || x.nx < 0)) throw std::invalid_argument("xgmi push: err / timeout");
+  if (x.mode >= 2 && (!x.err || x.timeout_ticks <= 0 || x.nx < 0)) throw std::invalid_argument("xgmi push: err / timeout");
   for (int i = 0; i < t.n; ++i) {
     const RedDesc& d = t.d[i];
     if (d.dst_off < x.lo || d.dst_off + (long long)d.numel > x.lo + (long long)x.chunk * x.size)
@@ -156,9 +155,6 @@ PYBIND11_MODULE(_kernels, m) {
       PTR(HeadArgs, wslab) PTR(HeadArgs, bslab) RW(HeadArgs, bt) RW(HeadArgs, epi) PTR(HeadArgs, ts)
       PTR(HeadArgs, yidx) RW(HeadArgs, generic);
 
-  py::class_<DenseHeadArgs>(m, "DenseHeadArgs")
-      .def(py::init<>())
-      RW(DenseHeadArgs, f) RW(DenseHeadArgs, h) PTR(DenseHeadArgs, ticket) RW(DenseHeadArgs, kh);
 
   py::class_<GatherArgs>(m, "GatherArgs")
       .def(py::init<>())
@@ -273,6 +269,7 @@ PYBIND11_MODULE(_kernels, m) {
   py::class_<RedTable>(m, "RedTable")
       .def(py::init([]() { RedTable t; memset(&t, 0, sizeof(t)); return t; }))
       .def_readonly("n", &RedTable::n)
+      .def_readonly("nblocks", &RedTable::nblocks)
       .def("add", [](RedTable& t, uintptr_t slab, long long stride_s, int S, int ld, int dst_off, int numel,
                       int type, int KH, int KW, int Cin, int Cout, int Cs, int tpe) {
         if (t.n >= MAX_RED) throw std::runtime_error("RedTable full");
@@ -337,9 +334,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("dense_big", &dense_big, "dense_fwd uses the large-weight LDS path for (NT, KS)");
   m.def("dense_epi", [](const DenseEpiArgs& a, uintptr_t s) { launch_dense_epi(a, S(s)); check_last("dense_epi"); });
   m.def("head", [](const HeadArgs& a, uintptr_t s) { launch_head(a, S(s)); check_last("head"); });
-  m.def("dense_head", [](const DenseHeadArgs& a, uintptr_t s) { launch_dense_head(a, S(s)); check_last("dense_head"); },
-        "last hidden dense layer + binary head in one launch (dense_head.hip)");
-  m.def("dense_head_blocks", &dense_head_blocks);
   m.def("prologue", [](const PrologueArgs& a, const PackTable& t, uintptr_t s) {
     launch_prologue(a, t, S(s)); check_last("prologue"); });
   m.def("gather_gx", &gather_gx);
@@ -372,7 +366,7 @@ PYBIND11_MODULE(_kernels, m) {
           if (xp && xp->on) {
             check_xgmi_push(*xp, *rt, *ro);
             x.xp = *xp;
-            if (xp->mode == 2 && xp->nx) x.n_r = xp->nx;   // (workgroups looping over the blocks)
+            if (xp->mode >= 2 && xp->nx) x.n_r = xp->nx;   // (workgroups looping over the blocks)
           }
         }
         const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, x, S(s));

@@ -30,7 +30,7 @@ bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT
   const int mtw = (MT + (wa.bslab ? 1 : 0) + 3) / 4;
   const size_t lds = std::max(conv_halo_lds_bytes(ca, ntc), wgrad_halo_lds_bytes(wa, MT, NTT));
   if (lds > 160 * 1024 || (x.n_r && lds < 2048)) return false;   // (the reduce body stages <= 2 KB)
-  if (x.n_r && x.xp.on && x.xp.mode == 2 && lds < 4096) return false;   // (+ the exchange's wait word)
+  if (x.n_r && x.xp.on && x.xp.mode >= 2 && lds < 4096) return false;   // (+ the exchange's wait word)
   // dgrad m-tiles per wave per pass: the TM in {4, 2} that minimises the busiest wave's
   // tile count over the block (ties -> larger TM: more fragment reuse); TM = 1 only when
   // the block has <= 4 tiles (measured: TM 1 loses its fragment reuse on longer blocks)

@@ -362,8 +362,9 @@ __global__ __launch_bounds__(256) void reduce_optim_kernel(float* __restrict__ g
   reduce_optim_block<KIND>(grad, tab, a, blockIdx.x, red);
 }
 
-// the early bucket's reduction + producer push (mode 1) or exchange + update (mode 2) as a
-// launch of its own (the dual launch that normally carries it declined: ablation / stamp args)
+// a data-parallel table launch of its own: the early bucket's reduction + producer push (mode 1)
+// or exchange + update (mode 2) when the dual launch that normally carries it declined
+// (ablation / stamp args), or the end-of-backward bucket's whole all-reduce + update (mode 3)
 __global__ __launch_bounds__(256) void xgmi_early_kernel(float* __restrict__ grad, const RedTable tab,
                                                          const OptimArgs a, const XgmiPush xp) {
   __shared__ __attribute__((aligned(16))) float red[1024];   // (mode 2: the wait word at [1023])
@@ -374,7 +375,7 @@ void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, h
                          const XgmiPush* xp) {
   if (tab.nblocks <= 0) return;
   if (xp && xp->on) {
-    const int grid = xp->mode == 2 && xp->nx ? xp->nx : tab.nblocks;
+    const int grid = xp->mode >= 2 && xp->nx ? xp->nx : tab.nblocks;
     hipLaunchKernelGGL(xgmi_early_kernel, dim3(grid), dim3(256), 0, s, grad, tab, a, *xp);
     return;
   }

@@ -187,28 +187,29 @@ __device__ __forceinline__ void update_elem(const OptimArgs& a, int e, float g) 
 }
 
 // Reduction + Keras update of table block `blk`: the thread that produces an element's
-// gradient writes it and applies the update at once.  `red`: 256 floats of LDS.  xp (grad_only
-// tables of the data-parallel step): also push the reduced elements to their owners.
+// gradient writes it and applies the update at once.  `red`: 256 floats of LDS.  xp (the
+// data-parallel step): also push the reduced elements to their owners, and no update.
 template <int KIND>
 __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
                                                    int blk, float* red, const XgmiPush* xp = nullptr) {
   const RedDesc& dsc = tab.d[red_desc(tab, blk)];
+  const bool upd = !a.grad_only && !xp;
   if (dsc.vec4) {
     int e;
     float4 g;
     const bool mine = slab_reduce_vec4(dsc, blk, e, g);
     if (mine) *reinterpret_cast<float4*>(grad + e) = g;
     if (mine && xp) xpush4(*xp, e, g);
-    if (!a.grad_only) update_vec4<KIND>(dsc, a, blk, red, mine, e, g);   // (grad_only: the reduced gradient is all)
+    if (upd) update_vec4<KIND>(dsc, a, blk, red, mine, e, g);   // (grad_only: the reduced gradient is all)
   } else {
     int e;
     float g;
     const bool mine = slab_reduce_elem(tab, blk, red, e, g);
     if (mine) grad[e] = g;
     if (mine && xp) xpush1(*xp, e, g);
-    if (mine && !a.grad_only) update_elem<KIND>(a, e, g);
+    if (mine && upd) update_elem<KIND>(a, e, g);
   }
-  if (a.defer_pack && !a.nroutes && !a.grad_only && blk == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
+  if (a.defer_pack && !a.nroutes && upd && blk == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
 }
 
 // ---------------------------------------------------------------- xGMI early-bucket exchange
@@ -285,7 +286,7 @@ __device__ __forceinline__ bool xs_wait(const XgmiPush& x, const unsigned* flags
 __device__ __forceinline__ void reduce_push_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
                                                   int blk, float* red, const XgmiPush& xp) {
   reduce_optim_block<OPT_SGD>(grad, tab, a, blk, red, &xp);
-  if (xp.bflag1[0] == nullptr) {
+  if (xp.bflag1[0] == nullptr || xp.size == 1) {   // (no flags / no peers to flag)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the pushes complete with this workgroup
     return;
   }
@@ -300,7 +301,7 @@ __device__ __forceinline__ void reduce_push_block(float* __restrict__ grad, cons
 // all-reduce kernel's (owner chunks of x.chunk bucket elements; rows summed in rank order, the
 // owner's own row from grad), so the sums are those the end-of-step kernel would produce.
 template <int KIND>
-__device__ void xchg_update_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a, int blk,
+__device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a, int blk,
                                   float* red, const XgmiPush& x) {
   const RedDesc& d = tab.d[red_desc(tab, blk)];
   const int P = x.size, me = x.rank, t = threadIdx.x, C = x.chunk;
@@ -322,7 +323,9 @@ __device__ void xchg_update_block(float* __restrict__ grad, const RedTable& tab,
   const long long ie = (long long)e - x.lo;     // bucket index
   const int own = n ? (int)(ie / C) : -1;
   float4 g = {0.f, 0.f, 0.f, 0.f};
-  if (me >= j0 && me <= j1) {
+  if (P == 1) {                                 // (no peers: the reduced gradient is final)
+    if (n) g = xs_local(grad + e, n);
+  } else if (me >= j0 && me <= j1) {
     // the owner part: every sender's row of the block is in my inbox
     if (!xs_wait(x, x.bflag1[me] + (size_t)blk * P, ~(1u << me), seq, 4, s_ok)) return;
     if (own == me) {
@@ -345,7 +348,7 @@ __device__ void xchg_update_block(float* __restrict__ grad, const RedTable& tab,
   }
   // the other owners' sums of this block's elements are in my outbox
   unsigned need = 0;
-  for (int j = j0; j <= j1; ++j)
+  for (int j = j0; j <= j1 && P > 1; ++j)
     if (j != me) need |= 1u << j;
   if (need) {
     if (!xs_wait(x, x.bflag2[me] + (size_t)blk * P, need, seq, 5, s_ok)) return;
@@ -360,19 +363,28 @@ __device__ void xchg_update_block(float* __restrict__ grad, const RedTable& tab,
   if (t == 0) x.ctrb[blk] = seq;
 }
 
-// the data-parallel early-bucket workgroup r of a launch (mode 1: one table block each; mode 2:
-// one block each, or x.nx workgroups looping over the blocks in order -- ranks sharing a GPU)
+// workgroup r of a data-parallel table launch: mode 1 (reduce + push) one table block each;
+// mode 2 (exchange + update) and mode 3 (both, one launch: the end-of-backward bucket) one
+// block each, or x.nx workgroups looping over the blocks in order (ranks sharing a GPU; mode 3
+// then pushes all of its blocks before its first wait)
 __device__ __forceinline__ void xgmi_early_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
                                                  int r, float* red, const XgmiPush& x) {
-  if (x.mode != 2) {
+  if (x.mode == 1) {
     reduce_push_block(grad, tab, a, r, red, x);
     return;
   }
-  if (xs_load(x.abort_[x.rank])) {   // sticky abort (an earlier wait timed out): touch nothing
+  if (x.size > 1 && xs_load(x.abort_[x.rank])) {   // sticky abort (an earlier wait timed out): touch nothing
     if (threadIdx.x == 0) xs_set_err(x.err, 3);
     return;
   }
   const int step = x.nx ? x.nx : x.nblk;
+  if (x.mode == 3) {
+    for (int b = r; b < x.nblk; b += step) {
+      reduce_push_block(grad, tab, a, b, red, x);
+      __syncthreads();
+    }
+    if (x.size == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   for (int b = r; b < x.nblk; b += step) {
     switch (a.kind) {
       case OPT_ADAM: xchg_update_block<OPT_ADAM>(grad, tab, a, b, red, x); break;

@@ -7,7 +7,7 @@
 // bias-correction scalars for this step.  (The data cursor is advanced by the head kernel,
 // after every prologue workgroup has read it.)
 // write_t false: every scalar of step st->t + 1 but the counter itself, which the caller
-// advances once no reader of the old count remains (dense_head.hip)
+// advances once no reader of the old count remains
 __device__ __forceinline__ void step_bookkeeping(const StepBeginArgs& a, bool write_t = true) {
   StepState* st = a.st;
   if (!a.training) return;

@@ -602,32 +602,6 @@ class BatchPlan(GeometryMixin):
         idx = self.srcidx.long()
         return d.x[idx], d.y[idx]
 
-    def _dense_head_args(self, h, epi, last_fwd, training):
-        """DenseHeadArgs for the fused dense layer + binary head launch (opt-in, dense_head=1:
-        measured 15.6 us for the launch against 13.3 us for the split-K dense launch + head
-        launch it replaces at RPV B=128 -- its 128 tile workgroups stream K at per-CU bandwidth
-        where the split-K launch spreads it over 512) when it applies: a
-        training step whose head (sigmoid, one output) reads the last hidden dense layer's
-        output (<= 256 columns), that layer on the small-weight path; else None."""
-        ex, K = self.ex, self.ex.K
-        if last_fwd is None or not training or not tune("dense_head", False):
-            return None
-        i, a, g = last_fwd
-        hd = ex.plan.head
-        kh = int(tune("dense_head_kh", 2))
-        splits = self.dense_splits[g.j][0]
-        if not (ex.head_act == 1 and hd.N == 1 and ex.head_src.kind == "dense" and g.Ns <= 256
-                and hd.K <= g.Ns and h.flat_C == h.flat_Cs and not K.dense_big(a.NT, a.KS)
-                and 1 <= kh <= splits and h.bt.dy and h.bt.prev_out == epi.out
-                and h.bt.pH == 1 and h.bt.pW == 1):
-            return None
-        d = K.DenseHeadArgs()
-        d.f, d.h, d.kh = a, h, kh
-        mgroups = cdiv(a.M, 16)
-        self.dense_head_ticket = torch.zeros(mgroups + 1, dtype=torch.int32, device=ex.device)
-        d.ticket = self.dense_head_ticket.data_ptr()
-        return d
-
     def _src_buf(self, src: Src):
         if src.kind == "input":
             return self.xb
@@ -816,13 +790,10 @@ class BatchPlan(GeometryMixin):
             bt = self._bt_for(src)
             if bt is not None:
                 h.bt = bt
-        dh = self._dense_head_args(h, head_epi, last_fwd if head_epi is not None else None, training)
-        if dh is not None:
-            # the last dense layer and the head in ONE launch (dense_head.hip) in place of the
-            # split-K dense launch; no separate head launch
-            self.launches[last_fwd[0]] = ("dense_head", lambda s, a=dh: K.dense_head(a, s))
-        else:
-            self.launches.append(("head", lambda s, a=h: K.head(a, s)))
+        # (a fused dense layer + head launch -- 16-wave K-slice tiles, the last arriving workgroup
+        # of each row group running the head -- measured 15.6 us against 13.3 us for the split-K
+        # dense launch + this head launch at RPV B=128, and was removed in round 5)
+        self.launches.append(("head", lambda s, a=h: K.head(a, s)))
         if not training:
             return
 
@@ -1029,6 +1000,7 @@ class BatchPlan(GeometryMixin):
         reducer = ex.reducer
         dp_early = []
         self.early_push, self.pushed, self.early_xchg, self.exchanged = {}, None, {}, False
+        self.bucket_xchg = {}
         if reducer is not None:
             bucket_groups = reducer.configure(groups)
             # one bucket at the end of the backward (the adaptive plan for gradients <= 16 MB):
@@ -1103,6 +1075,22 @@ class BatchPlan(GeometryMixin):
             inserts.append((max(self.red_ready[i] for i in bg), k))
         extra = []
         xk = getattr(reducer, "xgmi_bucket", None) if self.comm_in_graph else None
+        # xGMI exchange of the end-of-backward table too (XgmiPush mode 3): its launch reduces the
+        # conv layers' slabs, pushes them to their owners, finishes their all-reduce and applies
+        # the update -- with the early range exchanged inside the backward, the whole step's
+        # all-reduce + optimizer then runs in table launches and the fused kernel is not launched
+        self.bucket_xchg = {}
+        if xk is not None and tune("xgmi_xchg", True) and (self.exchanged or not dp_early):
+            blo, bhi, btab = self.bucket_tables[xk]
+            rlo, rhi = reducer.buckets[xk]
+            early_n = (self.pushed[1] - self.pushed[0]) if self.exchanged else 0
+            tab_n = sum(self.red_groups[i][1] - self.red_groups[i][0]
+                        for i in bucket_groups[xk] if i not in dp_early)
+            if btab.nblocks > 0 and early_n + tab_n == rhi - rlo:
+                fb = next(iter(self.early_xchg.values()))[0].nblocks if self.exchanged else 0
+                x3 = reducer.exchange_args(blo, bhi, btab.nblocks, fbase=fb, fused=True)
+                if x3 is not None:
+                    self.bucket_xchg[xk] = x3
         if self.comm_in_graph:
             rccl_buckets = [k for k in range(len(bucket_groups)) if k != xk]
             # fork the comm stream only when an RCCL bucket has later backward work to overlap
@@ -1119,7 +1107,7 @@ class BatchPlan(GeometryMixin):
                 extra.append(("optim_b%d", lambda k: None if k == xk else
                               (lambda s: self._launch_optim_comm(k, s)), "comm"))
             # the xGMI bucket: all-reduce + Keras update in one kernel on the main stream
-            extra.append(("xgmi_allreduce_optim_b%d", lambda k: None if k != xk else
+            extra.append(("xgmi_allreduce_optim_b%d", lambda k: None if (k != xk or k in self.bucket_xchg) else
                           (lambda s: reducer.launch_fused(ex.store.grad, ex._optim_args(False, defer_pack=True), s,
                                                           pushed=getattr(self, "pushed", None),
                                                           exchanged=getattr(self, "exchanged", False))),
@@ -1234,7 +1222,10 @@ class BatchPlan(GeometryMixin):
     def _launch_bucket_reduce(self, k, s):
         lo, hi, tab = self.bucket_tables[k]
         ex = self.ex
-        if self.optim_fused:     # gradient reduction + Keras update in one launch (re-pack deferred)
+        xp = (getattr(self, "bucket_xchg", None) or {}).get(k)
+        if xp is not None:       # reduction + all-reduce (exchange) + Keras update in one launch
+            ex.K.reduce_optim(ex.store.grad.data_ptr(), tab, ex._optim_args(False, defer_pack=True), s, xp)
+        elif self.optim_fused:     # gradient reduction + Keras update in one launch (re-pack deferred)
             ex.K.reduce_optim(ex.store.grad.data_ptr(), tab, ex._optim_args(False, defer_pack=True), s)
         else:
             ex.K.slab_reduce(ex.store.grad.data_ptr(), lo, hi, tab, s)

@@ -231,12 +231,13 @@ class GeometryMixin:
             if xp is not None:
                 kw["xp"] = xp
         elif xe is not None:
-            kw.update(rt=xe[0], ro=ex._optim_args(False, defer_pack=True), rgrad=ex.store.grad.data_ptr(), xp=xe[1])
+            kw.update(rt=xe[0], ro=ex._optim_args(False, defer_pack=True), rgrad=ex.store.grad.data_ptr(), xp=xe[1],
+                      rfirst=int(tune("xchg_rfirst", 1)))   # (dispatched first: their waits overlap the convs)
         ok = K.dual_halo(a, ntc, wa, cfg[0], cfg[1], cfg[2], s, **kw)
         if not ok:   # unsupported combination
             K.wgrad_halo(wa, cfg[0], cfg[1], cfg[2], s)
             K.conv_halo(a, ntc, s)
-            if kw:
+            if "rt" in kw:
                 K.reduce_optim(kw["rgrad"], kw["rt"], kw["ro"], s, kw.get("xp"))
 
     def _early_ro(self, early):

@@ -510,16 +510,20 @@ class NativeGradReducer:
         blo = self._xgmi_lo(lo, hi)
         return None if blo is None else self.xgmi.push_args(blo)
 
-    def exchange_args(self, lo: int, hi: int, nblk: int):
+    def exchange_args(self, lo: int, hi: int, nblk: int, fbase: int = 0, fused: bool = False):
         """(push, exchange) XgmiPush pair for an early range [lo, hi) whose reduction table has
         ``nblk`` blocks: the launch that reduces it pushes + flags (mode 1), a later backward
-        launch finishes its all-reduce and applies its update (mode 2); None when the range
-        is not in the xGMI bucket, there are no peers, or the flags cannot cover the table."""
+        launch finishes its all-reduce and applies its update (mode 2).  ``fused``: ONE
+        XgmiPush doing both in one launch (mode 3, the end-of-backward table).  ``fbase``: the
+        table's first block-flag slot.  None when the range is not in the xGMI bucket or the
+        flags cannot cover the table."""
         blo = self._xgmi_lo(lo, hi)
         if blo is None:
             return None
-        x1 = self.xgmi.push_args(blo, mode=1, nblk=nblk)
-        x2 = self.xgmi.push_args(blo, mode=2, nblk=nblk)
+        if fused:
+            return self.xgmi.push_args(blo, mode=3, nblk=nblk, fbase=fbase)
+        x1 = self.xgmi.push_args(blo, mode=1, nblk=nblk, fbase=fbase)
+        x2 = self.xgmi.push_args(blo, mode=2, nblk=nblk, fbase=fbase)
         return None if x1 is None or x2 is None else (x1, x2)
 
     def _xgmi_lo(self, lo: int, hi: int):

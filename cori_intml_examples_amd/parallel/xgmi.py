@@ -135,31 +135,36 @@ class XgmiAllreduce:
         self.setup_error = err
 
     # ------------------------------------------------------------------ launches
-    def push_args(self, lo: int = 0, mode: int = 1, nblk: int = 0):
+    def push_args(self, lo: int = 0, mode: int = 1, nblk: int = 0, fbase: int = 0):
         """XgmiPush for the kernels that finalise part of this all-reduce's bucket inside the
         backward (the early head / dense reduction).  mode 1: they store each reduced element
         straight into its owner's inbox row -- phase 1 of the all-reduce, overlapping the rest
         of the backward; with ``nblk`` (the table's blocks) they also raise per-block flags for
         an exchange.  mode 2 (the exchange, a later backward launch): the owners sum the rows
         and send the sums back, and every rank applies the update -- the range's whole
-        all-reduce + optimizer inside the backward (args.h XgmiPush).  ``lo``: the bucket's
-        first flat element.  None at size 1 (nothing to push) or past the flag capacity."""
-        if self.size < 2 or not self.bases or nblk > XCHG_MAX_BLOCKS:
+        all-reduce + optimizer inside the backward (args.h XgmiPush); mode 3: both in one
+        launch (the end-of-backward bucket's table).  ``lo``: the bucket's first flat element;
+        ``fbase``: the table's first block-flag slot (tables of one step use disjoint slots).  None past the flag capacity, or at size 1 without an exchange
+        (nothing to push; at size 1 the exchange is the range's update in the later launch --
+        the same structure, no peer traffic)."""
+        if not self.bases or fbase + nblk > XCHG_MAX_BLOCKS or (self.size < 2 and not nblk):
             return None
+        fo = 4 * fbase * self.size             # byte offset of the table's flag rows
         x = self.K.XgmiPush()
         x.on, x.rank, x.size, x.chunk, x.lo = 1, self.rank, self.size, self.chunk, int(lo)
         x.mode = mode
         for j, b in enumerate(self.bases):
             if nblk:
-                x.set_peer(j, b + self.off_in, b + self.off_out, b + self.off_bf1, b + self.off_bf2, b + self.off_ab)
+                x.set_peer(j, b + self.off_in, b + self.off_out, b + self.off_bf1 + fo, b + self.off_bf2 + fo,
+                           b + self.off_ab)
             else:
                 x.set_inbox(j, b + self.off_in)
         if nblk:
-            x.nblk, x.ctrb, x.err = nblk, self.ctrb.data_ptr(), self.err.data_ptr()
+            x.nblk, x.ctrb, x.err = nblk, self.ctrb.data_ptr() + 4 * fbase, self.err.data_ptr()
             x.timeout_ticks = self.args.timeout_ticks
             # ranks sharing a GPU: a few workgroups looping over the blocks (one per block would
             # let one rank's spinning workgroups fill the CUs its peers' launches need)
-            x.nx = int(tune("xgmi_xchg_wg", 4)) if (mode == 2 and self.shared) else 0
+            x.nx = int(tune("xgmi_xchg_wg", 4)) if (mode >= 2 and self.shared) else 0
         return x
 
     def launch(self, grad: int, stream: int, opt=None, skip=(0, 0), exchanged: bool = False) -> None:

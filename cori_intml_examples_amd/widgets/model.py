@@ -76,7 +76,10 @@ class ModelPlotTable:
             raise ValueError("column %r has %d values, table has %d rows" % (name, len(fill), len(self._records)))
         self._add_name(name)
         if fill is not None:
-            self._records = [rec + (v,) for rec, v in zip(self._records, fill)]
+            # records older than an earlier value-less column are short: pad them to the new
+            # column's slot so the value lands under its own name
+            j = self._slot[name]
+            self._records = [rec + (None,) * (j - len(rec)) + (v,) for rec, v in zip(self._records, fill)]
         # (without values, older records are shorter than ``columns``: read as None)
 
     def append_row(self, row: Dict[str, Any]) -> None:

@@ -9,8 +9,6 @@ import torch
 from cori_intml_examples_amd.apps import zoo
 
 os.environ["INTML_GRAPHS"] = "0"
-# the head kernel's own launch (the training step fuses the binary head into dense_head.hip)
-os.environ["INTML_TUNE"] = ",".join(x for x in (os.environ.get("INTML_TUNE", ""), "dense_head=0") if x)
 dev = torch.device("cuda", 0)
 B = 128
 rs = np.random.RandomState(0)

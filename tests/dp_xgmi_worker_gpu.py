@@ -88,6 +88,7 @@ def run(opt, lr, outdir, r, P, dev):
     rep["pushed"] = list(getattr(plan, "pushed", None) or [])
     rep["xchg_launches"] = sorted((getattr(plan, "early_xchg", None) or {}).keys())
     rep["exchanged"] = bool(getattr(plan, "exchanged", False))
+    rep["bucket_xchg"] = sorted((getattr(plan, "bucket_xchg", None) or {}).keys())
     rep["err"] = int(red.xgmi.err[0].item()) if red.xgmi is not None else -1
     rep["digest"] = hashlib.sha256(w.tobytes()).hexdigest()
     rep["finite"] = bool(np.isfinite(w).all())

@@ -220,7 +220,7 @@ def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
     replays x 8) at per-rank batch 128/P through the fused xGMI all-reduce + optimizer
     kernel, with Adam and with SGD -- the head / dense gradient pushed to its owners by the
     first dual backward launch (producer push) and all-reduced + updated by the
-    next one (exchange), the rest by the all-reduce kernel: no wait times out, every rank ends with bit-identical weights, and those match a
+    next one (exchange), the rest by the end-of-backward reduction launch (mode-3 exchange): no wait times out, every rank ends with bit-identical weights, and those match a
     single-process run at global batch 128 from the same weights and permutation (SGD within
     fp32 reordering; Adam within its sign-flip bound)."""
     env = dict(os.environ, PYTHONPATH=ROOT, INTML_DP_TIMEOUT="60")
@@ -246,7 +246,10 @@ def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
             rep = top[opt]
             assert rep["reducer"] == "NativeGradReducer", rep
             assert rep["plane"] == "xgmi" and rep["comm_in_graph"] and len(rep["buckets"]) == 1, rep
-            assert rep["fused_launches"] == ["xgmi_allreduce_optim_b0"], rep
+            # the whole all-reduce + update runs in the two table launches (exchange): the early
+            # range inside the backward, the conv layers' in the end-of-backward reduction --
+            # the fused two-shot kernel is not launched
+            assert rep["fused_launches"] == [] and rep["bucket_xchg"] == [0], rep
             assert rep["err"] == 0 and rep["finite"] and rep["moved"] > 1e-4, rep
             # the dense / head gradient was pushed to its owners from inside the backward
             assert rep["push_launches"] == ["wgrad_dgrad_conv2"] and rep["pushed"][1] > rep["pushed"][0], rep

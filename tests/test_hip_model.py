@@ -467,7 +467,7 @@ def test_head_fast_paths_bit_identical(kind, drop, cin, hw, opt, monkeypatch):
     write the slabs and dh) train bit-identically to the generic serial path: weights,
     metrics and iteration count over a multi-step graph."""
     res = []
-    for tv in ("head_generic=0,dense_head=0", "head_generic=1,dense_head=0"):
+    for tv in ("head_generic=0", "head_generic=1"):
         monkeypatch.setenv("INTML_TUNE", tv)
         set_random_seed(46)
         m = _build(kind, "cuda", opt=opt, drop=drop, cin=cin, hw=hw)
@@ -695,38 +695,3 @@ def test_dense_dx_tiles_agree(monkeypatch):
         res.append(m.store.master[:m.store.numel].clone())
     for r in res[1:]:
         assert (r - res[0]).abs().max().item() < 1e-5
-
-
-@pytest.mark.parametrize("opt,lr", [("SGD", 0.05), ("Adam", 1e-3)])
-def test_dense_head_matches_split_launches(opt, lr, monkeypatch):
-    """The fused dense layer + binary head launch (dense_head.hip: 16-wave K-slice tiles, the
-    last arriving workgroup of each 16-row group finishing the layer and the head) trains like
-    the split-K dense launch + head launch it replaces.  Only the dense layer's fp32 sum order
-    differs, so the step's weights agree to fp32 reordering level (SGD: linear in the
-    gradient) or within Adam's sign-flip bound, and the loss / accuracy metrics agree; the
-    launch list carries dense_head and no head launch."""
-    res = []
-    for tv in ("dense_head=1", "dense_head=0"):
-        monkeypatch.setenv("INTML_TUNE", tv)
-        set_random_seed(52)
-        m = zoo.rpv_cnn((64, 64, 3), conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.2, optimizer=opt,
-                        lr=lr, device="cuda")
-        x, y = _data(m, 512, seed=16)
-        ex = m._executor
-        d = ex.upload(x, y)
-        perm = torch.randperm(d.n, generator=torch.Generator().manual_seed(13)).to(ex.device)
-        ex.reset_metrics()
-        ex.train_steps(d, perm, 0, 128, 4)
-        torch.cuda.synchronize()
-        names = [it[0] for it in ex._plans[(128, "train")].launches]
-        res.append((m.store.master[:m.store.numel].clone(), ex.read_metrics(), names, int(m.optimizer.iterations)))
-    (w1, m1, n1, i1), (w0, m0, n0, i0) = res
-    assert "dense_head" in n1 and "head" not in n1 and "head" in n0 and "dense_head" not in n0, (n1, n0)
-    assert i1 == i0 == 4
-    d = (w1 - w0).abs()
-    if opt == "SGD":
-        assert float(d.max()) < 1e-4, float(d.max())
-    else:
-        assert float(torch.quantile(d[:1 << 20], 0.999)) < 2e-3 and float(d.max()) < 8e-3, float(d.max())
-    for v1, v0 in zip(m1, m0):
-        assert abs(v1 - v0) <= 1e-3 * max(1.0, abs(v0)), (m1, m0)

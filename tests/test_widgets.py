@@ -26,6 +26,11 @@ def test_plot_table_and_task_data():
         t.append_column("acc")
     with pytest.raises(ValueError):
         t.append_column("x", [1])
+    # a valued column after a value-less one lands under its own name
+    t.append_column("f1", [0.3, 0.4])
+    assert t.to_dict()["acc"] == [None, None] and t.to_dict()["f1"] == [0.3, 0.4]
+    t.append_row({"epoch": 2, "acc": 0.9, "f1": 0.5})
+    assert t.column("acc") == [None, None, 0.9] and t.column("f1") == [0.3, 0.4, 0.5]
     d = ModelTaskData(["epoch", "loss"], ["status", "epoch"])
     assert d.num_data_rows == 0 and d.has_updates
     d.append_plot_data_row({"epoch": 0, "loss": 0.5})
