@@ -380,6 +380,9 @@ struct XgmiPush {
   long long timeout_ticks = 0;
   int nblk = 0;                          // blocks of the table
   int nx = 0;                            // mode 2: workgroups looping over the blocks (0: one each)
+  int p1 = 0;                            // size 1, mode 3: 1 = keep the exchange structure (push /
+                                         // flag / re-read: a measurement of its fixed cost); 0 =
+                                         // reduce + update in place (no peers: nothing to exchange)
 };
 
 // Optional extra workgroups of the dual conv backward launch: the fused reduction + optimizer

@@ -396,7 +396,7 @@ PYBIND11_MODULE(_kernels, m) {
   py::class_<XgmiPush>(m, "XgmiPush")
       .def(py::init<>())
       RW(XgmiPush, on) RW(XgmiPush, rank) RW(XgmiPush, size) RW(XgmiPush, chunk) RW(XgmiPush, lo)
-      RW(XgmiPush, mode) RW(XgmiPush, nblk) RW(XgmiPush, nx) RW(XgmiPush, timeout_ticks)
+      RW(XgmiPush, mode) RW(XgmiPush, nblk) RW(XgmiPush, nx) RW(XgmiPush, p1) RW(XgmiPush, timeout_ticks)
       PTR(XgmiPush, ctrb) PTR(XgmiPush, err)
       .def("set_inbox", [](XgmiPush& x, int j, uintptr_t p) {
         if (j < 0 || j >= XGMI_MAX_RANKS) throw std::out_of_range("peer index");

@@ -18,7 +18,7 @@ __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, con
   if (x.n_r) {   // early-bucket reduction + optimizer workgroups
     const int r = x.rfirst ? id : id - (int)gridDim.x + x.n_r;
     if (r >= 0 && r < x.n_r) {
-      if constexpr (XP) xgmi_early_block(x.grad, x.rt, x.ro, r, reinterpret_cast<float*>(smem), x.xp);
+      if constexpr (XP) xgmi_early_block<false>(x.grad, x.rt, x.ro, r, reinterpret_cast<float*>(smem), x.xp);
       else reduce_optim_block_rt(x.grad, x.rt, x.ro, r, reinterpret_cast<float*>(smem));
       return;
     }

@@ -368,7 +368,7 @@ __global__ __launch_bounds__(256) void reduce_optim_kernel(float* __restrict__ g
 __global__ __launch_bounds__(256) void xgmi_early_kernel(float* __restrict__ grad, const RedTable tab,
                                                          const OptimArgs a, const XgmiPush xp) {
   __shared__ __attribute__((aligned(16))) float red[1024];   // (mode 2: the wait word at [1023])
-  xgmi_early_block(grad, tab, a, blockIdx.x, red, xp);
+  xgmi_early_block<true>(grad, tab, a, blockIdx.x, red, xp);
 }
 
 void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, hipStream_t s,

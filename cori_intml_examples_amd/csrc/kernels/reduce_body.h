@@ -366,7 +366,10 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
 // workgroup r of a data-parallel table launch: mode 1 (reduce + push) one table block each;
 // mode 2 (exchange + update) and mode 3 (both, one launch: the end-of-backward bucket) one
 // block each, or x.nx workgroups looping over the blocks in order (ranks sharing a GPU; mode 3
-// then pushes all of its blocks before its first wait)
+// then pushes all of its blocks before its first wait).  M3: mode 3 compiled in -- the
+// standalone launch only: in the dual conv launch (modes 1 / 2) its extra code made the
+// compiler copy the whole by-value DualExtra argument to scratch (1.7 KB per lane)
+template <bool M3>
 __device__ __forceinline__ void xgmi_early_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
                                                  int r, float* red, const XgmiPush& x) {
   if (x.mode == 1) {
@@ -378,12 +381,27 @@ __device__ __forceinline__ void xgmi_early_block(float* __restrict__ grad, const
     return;
   }
   const int step = x.nx ? x.nx : x.nblk;
+  if constexpr (M3) {
+  if (x.mode == 3 && x.size == 1 && !x.p1) {   // no peers: the single-GPU reduction + update
+    for (int b = r; b < x.nblk; b += step) {
+      switch (a.kind) {
+        case OPT_ADAM: reduce_optim_block<OPT_ADAM>(grad, tab, a, b, red); break;
+        case OPT_NADAM: reduce_optim_block<OPT_NADAM>(grad, tab, a, b, red); break;
+        case OPT_ADADELTA: reduce_optim_block<OPT_ADADELTA>(grad, tab, a, b, red); break;
+        case OPT_RMSPROP: reduce_optim_block<OPT_RMSPROP>(grad, tab, a, b, red); break;
+        default: reduce_optim_block<OPT_SGD>(grad, tab, a, b, red); break;
+      }
+      __syncthreads();
+    }
+    return;
+  }
   if (x.mode == 3) {
     for (int b = r; b < x.nblk; b += step) {
       reduce_push_block(grad, tab, a, b, red, x);
       __syncthreads();
     }
     if (x.size == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   }
   for (int b = r; b < x.nblk; b += step) {
     switch (a.kind) {

@@ -1008,15 +1008,22 @@ class BatchPlan(GeometryMixin):
             # step's early bucket) are REDUCED early there (grad_only: no update), so the
             # end-of-backward reduction ahead of the all-reduce only has the conv layers' slabs
             # left (the update stays behind the all-reduce)
+            # one rank (the N = 1 data-parallel step): nothing to exchange -- the early groups
+            # are reduced AND updated in that launch, as on a single GPU (xchg_p1: keep the
+            # exchange structure, to measure its fixed cost)
+            solo = reducer.size == 1 and getattr(reducer, "xgmi", None) is not None and not tune("xchg_p1", False)
             if len(bucket_groups) == 1 and self.comm_in_graph and tune("dp_early", True):
-                dp_early = self._early_groups(grad_only=True)
+                dp_early = self._early_groups(grad_only=not solo)
+                if solo and self.early_red:
+                    self.pushed = next(iter(self.early_red.values()))[1]
+                    self.exchanged = True
                 # producer push (xGMI plane): the early groups' reduced gradient goes straight to
                 # its owners' inboxes from the launch that reduces it, inside the backward, and
                 # the fused all-reduce kernel skips those elements in its phase 1
                 # ... and (exchange) the NEXT dual launch finishes that range's all-reduce and
                 # applies its update in extra workgroups of its own, so the fused kernel after
                 # the backward is left with the conv layers only
-                if tune("xgmi_push", True):
+                if tune("xgmi_push", True) and not solo:
                     for nm, (tab_, (elo, ehi), go) in self.early_red.items():
                         if not go:
                             continue
@@ -1087,7 +1094,7 @@ class BatchPlan(GeometryMixin):
             tab_n = sum(self.red_groups[i][1] - self.red_groups[i][0]
                         for i in bucket_groups[xk] if i not in dp_early)
             if btab.nblocks > 0 and early_n + tab_n == rhi - rlo:
-                fb = next(iter(self.early_xchg.values()))[0].nblocks if self.exchanged else 0
+                fb = next(iter(self.early_xchg.values()))[0].nblocks if self.early_xchg else 0
                 x3 = reducer.exchange_args(blo, bhi, btab.nblocks, fbase=fb, fused=True)
                 if x3 is not None:
                     self.bucket_xchg[xk] = x3
@@ -1122,8 +1129,9 @@ class BatchPlan(GeometryMixin):
                                                 [(lo, hi) for lo, hi, _ in self.bucket_tables],
                                                 self.pack_readers)
         spans = [(lo, hi) for lo, hi, _ in self.bucket_tables]
-        # (grad-only early reductions lie inside their all-reduce bucket's span)
-        spans += [e[1] for e in (self.early_red or {}).values() if not e[2]]
+        # (data parallel: every early reduction lies inside its all-reduce bucket's span)
+        if reducer is None:
+            spans += [e[1] for e in (self.early_red or {}).values()]
         check_bucket_cover(spans, ex.store.numel)
 
     def _early_groups(self, grad_only: bool = False):

@@ -163,8 +163,11 @@ class XgmiAllreduce:
             x.nblk, x.ctrb, x.err = nblk, self.ctrb.data_ptr() + 4 * fbase, self.err.data_ptr()
             x.timeout_ticks = self.args.timeout_ticks
             # ranks sharing a GPU: a few workgroups looping over the blocks (one per block would
-            # let one rank's spinning workgroups fill the CUs its peers' launches need)
-            x.nx = int(tune("xgmi_xchg_wg", 4)) if (mode >= 2 and self.shared) else 0
+            # let one rank's spinning workgroups fill the CUs its peers' launches need);
+            # xchg_nx (A/B): as many looping workgroups on separate GPUs too
+            x.nx = int(tune("xgmi_xchg_wg", 4)) if self.shared else int(tune("xchg_nx", 0))
+            x.nx = x.nx if mode >= 2 else 0
+            x.p1 = int(tune("xchg_p1", False))
         return x
 
     def launch(self, grad: int, stream: int, opt=None, skip=(0, 0), exchanged: bool = False) -> None:
