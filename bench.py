@@ -167,11 +167,11 @@ def probe_data_planes(args, size, dev, g, B, chunk):
     here; SURVEY.md §5.1 item 3 "benchmark it against RCCL and keep the winner"): unless
     ``INTML_XGMI`` / ``INTML_BUCKET_BYTES`` pin it, time a short probe of the full DP step on
     each candidate data plane --
-      xgmi         the fused two-shot xGMI all-reduce + optimizer kernel (one bucket; the
-                   head / dense part pushed to its owners from inside the backward),
-      rccl         the default plane of fit(): at N > 1 the head / dense bucket's RCCL
-                   all-reduce + update forked onto the comm stream (overlapping the conv
-                   backward), then the small conv bucket (dist.adaptive_bucket_bytes),
+      xgmi         the xGMI plane (fit()'s default on one node, dist.auto_plane): the head /
+                   dense range pushed to its owners, all-reduced and updated inside the
+                   backward (exchange), the conv layers' in the end-of-backward reduction,
+      rccl         the RCCL plane: one all-reduce + optimizer of the whole gradient at the end
+                   of the backward (dist.adaptive_bucket_bytes),
       rccl_single  one RCCL all-reduce of the whole gradient at the end of the backward,
       rccl_forked  1 MiB buckets in backward order, each all-reduce forked onto the comm
                    stream as soon as its gradients are reduced (overlaps the conv backward),
@@ -548,7 +548,7 @@ def main():
         red = ex.reducer
         sums = hvd.allgather(weight_checksum(model)) if size > 1 else [weight_checksum(model)]
         rstats = hvd.allgather(stats) if size > 1 else [stats]
-        from cori_intml_examples_amd.parallel.dist import data_plane
+        from cori_intml_examples_amd.parallel.dist import auto_plane, data_plane
         xk = getattr(red, "xgmi_bucket", None)
         selfcheck = {
             "data_plane": (("xgmi-fused-allreduce+optim" if len(red.buckets) == 1 else
@@ -556,7 +556,8 @@ def main():
                            if xk is not None else
                            "rccl-native" if comm is not None else ("torch-" + str(st.backend))),
             # what a fit() / train_rpv run without the probe uses (INTML_XGMI unset)
-            "default_plane": "rccl-native" if comm is not None else ("torch-" + str(st.backend)),
+            "default_plane": (("xgmi" if auto_plane() == "xgmi" else "rccl-native") if comm is not None
+                              else ("torch-" + str(st.backend))),
             "env_plane": data_plane(),
             "rccl_nranks": comm.nranks if comm is not None else None,
             "world_size": size,

@@ -391,16 +391,33 @@ def adaptive_bucket_bytes(groups: Sequence[Tuple[int, int]], size: int = 1) -> i
 
 def data_plane() -> str:
     """The gradient data plane of the native (captured) reducer, from ``INTML_XGMI``:
-    "rccl" (default, also "auto" / "0"): RCCL all-reduces;  "xgmi" ("1"): the whole gradient
-    as one fused xGMI all-reduce + optimizer kernel;  "hybrid": RCCL for the early (dense)
-    buckets, overlapped with the conv backward, and the fused xGMI kernel for the last (conv)
-    bucket.  Nothing but a measurement picks xGMI: ``bench.py``'s probe times every plane on
-    the job itself and pins the fastest (``probe_data_planes``)."""
+    "xgmi" ("1"): the whole gradient on the xGMI plane -- the early (head / dense) range
+    all-reduced and updated inside the backward (exchange), the rest by the end-of-backward
+    reduction launch;  "rccl" ("0"): one RCCL all-reduce + optimizer;  "hybrid": RCCL for the
+    early buckets, the fused xGMI kernel for the last;  "auto" (default): ``auto_plane()``.
+    ``bench.py``'s probe times every plane on the job itself and pins the fastest
+    (``probe_data_planes``)."""
     mode = os.environ.get("INTML_XGMI", "auto").lower()
     if mode in ("1", "on", "true", "xgmi"):
         return "xgmi"
     if mode == "hybrid":
         return "hybrid"
+    if mode in ("0", "off", "false", "rccl"):
+        return "rccl"
+    return auto_plane()
+
+
+def auto_plane() -> str:
+    """The default plane: "xgmi" when every rank has a GPU of its own on ONE node (the xGMI
+    links reach every peer; the all-reduce of the early range overlaps the conv backward), else
+    "rccl".  The xGMI plane is still only used after its collective setup and self-test --
+    the two-shot kernel and the exchange protocol, on every rank -- pass the vote; otherwise
+    the step keeps the RCCL all-reduce (NativeGradReducer._setup_xgmi)."""
+    if is_initialized():
+        st = _st()
+        if (st.size > 1 and st.local_size == st.size and torch.cuda.is_available()
+                and torch.cuda.device_count() >= st.local_size):
+            return "xgmi"
     return "rccl"
 
 

@@ -209,6 +209,49 @@ class XgmiAllreduce:
             if not torch.equal(g, want):
                 bad = int((g != want).sum())
                 return "selftest: %d of %d elements wrong" % (bad, n)
+        return self._xchg_selftest()
+
+    def _xchg_selftest(self) -> Optional[str]:
+        """The exchange protocol the training step uses (XgmiPush mode 3: per-block flags,
+        owner sums pushed back through the outboxes) on a closed-form table -- a float4 and a
+        split-lane descriptor over a window straddling the first owner boundary -- twice (the
+        block sequence numbers advance); every rank must read back the exact sums.  Uses the
+        top block-flag slots, which no training table reaches."""
+        K, P, r, dev = self.K, self.size, self.rank, self.device
+        lo = max(0, min(self.n, self.chunk) - 2048) // 4 * 4
+        hi = min(self.n, lo + 4096) // 4 * 4
+        nv = (hi - lo) // 64 * 64                        # float4 descriptor: Cout 16 x Cin rows
+        nb = min(hi - lo - nv, 256)                      # split-lane descriptor
+        if nv < 64:
+            return None                                  # (a bucket too small to matter)
+        S, tpe = 4, 2
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        st = torch.zeros(K.STEP_STATE_BYTES, dtype=torch.uint8, device=dev)   # lr 0: the update is a no-op
+        p = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        ramp = lambda m: torch.remainder(torch.arange(m, device=dev, dtype=torch.float32), 7.0) * 0.25
+        for it in range(2):
+            f = float(r + 1 + it)
+            sv = torch.stack([ramp(nv) * f * (s + 1) for s in range(S)])
+            sb = torch.stack([ramp(max(nb, 1)) * f * (s + 1) for s in range(S)])
+            tab = K.RedTable()
+            tab.add(sv.data_ptr(), nv, S, 16, lo, nv, 2, 1, 1, nv // 16, 16, nv // 16, -1)   # RED_FLATW, float4
+            if nb:
+                tab.add(sb.data_ptr(), max(nb, 1), S, nb, lo + nv, nb, 1, 1, 1, 1, nb, nb, tpe)   # RED_BIAS
+            a = K.OptimArgs()
+            a.p, a.n, a.st, a.kind = p.data_ptr(), self.n, st.data_ptr(), 0
+            xp = self.push_args(0, mode=3, nblk=tab.nblocks, fbase=XCHG_MAX_BLOCKS - tab.nblocks)
+            if xp is None:
+                return "exchange selftest: no flag slots"
+            g = torch.zeros(self.n, dtype=torch.float32, device=dev)
+            K.reduce_optim(g.data_ptr(), tab, a, stream, xp)
+            torch.cuda.synchronize(self.device)
+            if int(self.err[0].item()):
+                return "exchange selftest: " + describe_error(*self.err.tolist())
+            k = sum(q + 1 + it for q in range(P)) * S * (S + 1) / 2
+            want = torch.cat([ramp(nv), ramp(nb)[:nb]]) * k
+            if not torch.equal(g[lo:lo + nv + nb], want):
+                bad = int((g[lo:lo + nv + nb] != want).sum())
+                return "exchange selftest: %d of %d elements wrong" % (bad, nv + nb)
         return None
 
     def close(self) -> None:

@@ -269,3 +269,30 @@ def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
     # the whole difference by a tenth of the step
     vs = reps[0]["Adam"]["vs_single"]
     assert vs["max"] < 2.4e-2 and vs["rel"] < 0.1, vs
+
+
+def test_auto_plane(monkeypatch):
+    """fit()'s default data plane: xGMI (exchange inside the backward) when every rank has a GPU
+    of its own on one node, RCCL across nodes, with shared GPUs, or when pinned."""
+    import types
+    from cori_intml_examples_amd.parallel import dist as D
+    monkeypatch.delenv("INTML_XGMI", raising=False)
+    st = types.SimpleNamespace(size=8, local_size=8)
+    monkeypatch.setattr(D, "is_initialized", lambda: True)
+    monkeypatch.setattr(D, "_st", lambda: st)
+    monkeypatch.setattr(D.torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(D.torch.cuda, "device_count", lambda: 8)
+    assert D.data_plane() == "xgmi"
+    st.local_size = 4                        # two nodes
+    assert D.data_plane() == "rccl"
+    st.local_size = 8
+    monkeypatch.setattr(D.torch.cuda, "device_count", lambda: 1)   # ranks share a GPU
+    assert D.data_plane() == "rccl"
+    monkeypatch.setattr(D.torch.cuda, "device_count", lambda: 8)
+    st.size = st.local_size = 1              # one rank
+    assert D.data_plane() == "rccl"
+    st.size = st.local_size = 8
+    monkeypatch.setenv("INTML_XGMI", "rccl")
+    assert D.data_plane() == "rccl"
+    monkeypatch.setenv("INTML_XGMI", "xgmi")
+    assert D.data_plane() == "xgmi"
