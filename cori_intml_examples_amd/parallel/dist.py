@@ -407,6 +407,17 @@ def data_plane() -> str:
     return auto_plane()
 
 
+def device_key(device) -> str:
+    """Identity of the physical GPU behind ``device``: host + PCI location (else UUID)."""
+    import socket
+    try:
+        p = torch.cuda.get_device_properties(device)
+        ident = "pci:%s:%s:%s" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+    except Exception:                  # noqa: BLE001 -- older runtimes: the visible-device index
+        ident = "idx:%s/%s" % (os.environ.get("HIP_VISIBLE_DEVICES", ""), getattr(device, "index", device))
+    return socket.gethostname() + "/" + ident
+
+
 def auto_plane() -> str:
     """The default plane: "xgmi" when every rank has a GPU of its own on ONE node (the xGMI
     links reach every peer; the all-reduce of the early range overlaps the conv backward), else
@@ -497,8 +508,11 @@ class NativeGradReducer:
             # files; at one workgroup per CU they would leave no CU able to host a peer's conv
             # stack workgroup (3 waves x 168 VGPRs per SIMD), and the peer never reaches its own
             # all-reduce -- a deadlock that separate GPUs cannot have
-            st = _st()
-            shared = st.local_size > max(1, torch.cuda.device_count())
+            # (the physical GPUs of every rank compared: processes pinned with set_device
+            # while every GPU stays visible -- farm engines -- share a GPU without it showing
+            # in the device count)
+            keys = allgather(device_key(self.device))
+            shared = len(set(keys)) < len(keys) or _st().local_size > max(1, torch.cuda.device_count())
             max_wg = int(tune("xgmi_shared_wg", 8)) if shared else None
             self.xgmi = X.create(self.rank, self.size, n, self.device, allgather, max_wg=max_wg)
             if self.xgmi is not None:

@@ -94,11 +94,15 @@ def main(out):
     plan = next(iter(m._executor._plans.values()))
     results["xgmi"] = {"active": m._executor.reducer.xgmi is not None,
                        "launches": [it[0] for it in plan.launches if "xgmi" in it[0] or "allreduce" in it[0]],
+                       "bucket_xchg": sorted((getattr(plan, "bucket_xchg", None) or {}).keys()),
                        "max_abs_diff": float(np.abs(w - wb).max()),
                        "p999_abs_diff": float(np.quantile(np.abs(w - wb), 0.999))}
     # hybrid plane: bucket 0 (head + dense) over RCCL on the comm stream with its optimizer,
     # bucket 1 (convs) through the fused xGMI kernel on the main stream
     os.environ["INTML_XGMI"] = "hybrid"
+    # (xgmi_xchg=0: the conv bucket through the fused two-shot kernel -- its training coverage;
+    # by default the end-of-backward reduction launch exchanges it, as in the xgmi case above)
+    os.environ["INTML_TUNE"] = "comm_capture=1,xgmi_xchg=0"
     m = zoo.rpv_cnn((64, 64, 3), use_horovod=True, **kw)
     m.set_weights(w0)
     w = train(m)

@@ -72,7 +72,9 @@ def test_native_comm_engine_gpu(tmp_path):
     assert not seg["comm_in_graph"], seg
     assert rep["train"]["bf16_wire"]["rel_diff"] < 0.05, rep["train"]["bf16_wire"]
     xg = rep["train"]["xgmi"]
-    assert xg["active"] and xg["launches"] == ["xgmi_allreduce_optim_b0"], xg
+    # (one rank: the early range is updated in place, the rest by the end-of-backward
+    # reduction launch -- the exchange tables cover the gradient, no fused two-shot launch)
+    assert xg["active"] and xg["launches"] == [] and xg["bucket_xchg"] == [0], xg
     assert xg["p999_abs_diff"] < 1e-5 and xg["max_abs_diff"] < 2e-3, xg
     hy = rep["train"]["hybrid"]
     assert hy["xgmi_bucket"] == 1 and len(hy["buckets"]) == 2 and hy["comm_fork"], hy
