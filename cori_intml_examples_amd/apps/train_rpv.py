@@ -91,7 +91,10 @@ def main(argv=None):
         print("[train_rpv] gradient reducer %s" % history.data_plane)
     if args.fom in ("best", "last"):
         from ..hpo.evaluator import figure_of_merit
-        print("FoM:", figure_of_merit(history.history["val_loss"], args.fom))
+        # one write per line: the ranks share the launcher's pipe, and print's separate writes
+        # of "FoM:" and the value interleave across ranks
+        sys.stdout.write("FoM: %s\n" % figure_of_merit(history.history["val_loss"], args.fom))
+        sys.stdout.flush()
     sys.stdout.flush()
 
     if hvd.rank() == 0 and args.n_test > 0:
