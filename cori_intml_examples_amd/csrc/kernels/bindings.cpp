@@ -277,15 +277,23 @@ PYBIND11_MODULE(_kernels, m) {
         d.slab = reinterpret_cast<const float*>(slab); d.stride_s = stride_s; d.S = S; d.ld = ld;
         d.dst_off = dst_off; d.numel = numel; d.type = type; d.KH = KH; d.KW = KW; d.Cin = Cin;
         d.Cout = Cout; d.Cs = Cs;
-        // a flattened dense kernel with unpadded channels and slab rows of exactly Cout
-        // columns IS the Keras layout: 4 consecutive elements per thread, float4 traffic
-        d.vec4 = (type == RED_FLATW && Cin == Cs && ld == Cout && numel % 4 == 0 && dst_off % 4 == 0 &&
-                  stride_s % 4 == 0 && S <= 8 && tpe <= 0) ? 1 : 0;
-        d.tile = (d.vec4 && 1024 % Cout == 0 && (1024 / Cout) % 8 == 0 && numel % 1024 == 0) ? 1 : 0;
+        // a flattened dense or conv kernel with unpadded channels and slab rows of exactly Cout
+        // columns IS the Keras layout (so is a bias): 4 consecutive elements per thread, float4
+        // traffic (an explicit tpe keeps the scalar path)
+        const bool ident = type == RED_BIAS || ((type == RED_FLATW || type == RED_CONVW) && Cin == Cs && ld == Cout);
+        d.vec4 = (ident && numel % 4 == 0 && dst_off % 4 == 0 && stride_s % 4 == 0 && tpe <= 0) ? 1 : 0;
+        d.tile = (d.vec4 && type == RED_FLATW && 1024 % Cout == 0 && (1024 / Cout) % 8 == 0 && numel % 1024 == 0)
+                     ? 1 : 0;
         // threads per element (power of 2, <= 64): E = 256 / tpe consecutive elements per
         // workgroup keep each slab-row read >= 16 contiguous bytes; each thread sums its
         // S / tpe partials 8 independent loads at a time
-        if (tpe > 0) {
+        if (d.vec4) {
+          // split-lanes as the scalar path (~S/16 partials per thread); tiled dense blocks
+          // need the 1024-element map (tpe 1)
+          d.tpe = 1;
+          while (d.tpe < 64 && d.tpe * 16 < S) d.tpe *= 2;
+          if (d.tpe > 1) d.tile = 0;
+        } else if (tpe > 0) {
           if (tpe > 256 || (tpe & (tpe - 1))) throw std::invalid_argument("tpe: power of 2 <= 256");
           d.tpe = tpe;
         } else {
@@ -293,7 +301,7 @@ PYBIND11_MODULE(_kernels, m) {
           while (d.tpe < 64 && d.tpe * 16 < S) d.tpe *= 2;   // scripts/red_sweep.py)
         }
         d.blk0 = t.nblocks;
-        const int epb = d.vec4 ? 1024 : 256 / d.tpe;
+        const int epb = d.vec4 ? 1024 / d.tpe : 256 / d.tpe;
         t.nblocks += (numel + epb - 1) / epb;
       }, py::arg("slab"), py::arg("stride_s"), py::arg("S"), py::arg("ld"), py::arg("dst_off"), py::arg("numel"),
       py::arg("type"), py::arg("KH"), py::arg("KW"), py::arg("Cin"), py::arg("Cout"), py::arg("Cs"), py::arg("tpe") = -1);

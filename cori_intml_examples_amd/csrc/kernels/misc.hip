@@ -40,13 +40,13 @@ __device__ __forceinline__ void gather_block(const GatherArgs& a, const StepStat
 }
 
 __global__ __launch_bounds__(256) void slab_reduce_kernel(float* __restrict__ grad, const RedTable tab) {
-  __shared__ float red[256];
+  __shared__ __attribute__((aligned(16))) float red[512];
   const int blk = blockIdx.x;
   const RedDesc& d = tab.d[red_desc(tab, blk)];
   if (d.vec4) {
     int e;
     float4 g;
-    if (slab_reduce_vec4(d, blk, e, g)) *reinterpret_cast<float4*>(grad + e) = g;
+    if (slab_reduce_vec4(d, blk, red, e, g)) *reinterpret_cast<float4*>(grad + e) = g;
     return;
   }
   int e;

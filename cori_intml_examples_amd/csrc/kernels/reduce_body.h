@@ -73,35 +73,71 @@ __device__ __forceinline__ bool slab_reduce_elem(const RedTable& tab, int blk, f
   return true;
 }
 
-// vec4 descriptors (identity layout): thread -> 4 consecutive elements, float4 slab loads in
-// fixed split order (the same per-element order as slab_reduce_elem with tpe = 1).
 __device__ __forceinline__ int red_desc(const RedTable& tab, int blk) {
   int di = 0;
   while (di + 1 < tab.n && blk >= tab.d[di + 1].blk0) ++di;
   return di;
 }
 
+// vec4 descriptors (identity layouts: Keras order = slab order): G = 256 / tpe threads each
+// own 4 consecutive elements (1024 / tpe per block), their tpe split-lanes sum interleaved
+// subsets of the S slabs with float4 loads, 8 in flight -- per element exactly the order of
+// slab_reduce_elem (the accumulators a[u], their fixed combine, the lane tree), so the two
+// paths agree bit for bit.  `red`: >= 2 KB of LDS (tpe 2: one float4 per element group).
+__device__ __forceinline__ int vec4_epb(const RedDesc& d) { return 1024 / d.tpe; }
 // first element (flat index) of vec4 table block blk
-__device__ __forceinline__ int e_block0(const RedDesc& d, int blk) { return d.dst_off + (blk - d.blk0) * 1024; }
+__device__ __forceinline__ int e_block0(const RedDesc& d, int blk) { return d.dst_off + (blk - d.blk0) * vec4_epb(d); }
 
-__device__ __forceinline__ bool slab_reduce_vec4(const RedDesc& d, int blk, int& e, float4& g) {
-  const int le = ((blk - d.blk0) * 256 + (int)threadIdx.x) * 4;
-  if (le >= d.numel) return false;
-  const float* p = d.slab + le;
-  float4 v[8];
+__device__ __forceinline__ void add4(float4& a, const float4& b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; }
+
+__device__ __forceinline__ bool slab_reduce_vec4(const RedDesc& d, int blk, float* red, int& e, float4& g) {
+  const int tpe = d.tpe, G = 256 / tpe;
+  const int gi = (int)threadIdx.x % G, lane = (int)threadIdx.x / G;
+  const int le = ((blk - d.blk0) * G + gi) * 4;
+  const bool in = le < d.numel;
+  float4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (in) {
+    const float* p = d.slab + le;
+    const size_t st = (size_t)d.stride_s;
+    float4 a[8];
 #pragma unroll
-  for (int s = 0; s < 8; ++s)
-    if (s < d.S) v[s] = *reinterpret_cast<const float4*>(p + (size_t)s * d.stride_s);
-  float4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};   // a[s % 2], like the scalar path's a[u]
+    for (int u = 0; u < 8; ++u) a[u] = float4{0.f, 0.f, 0.f, 0.f};
+    int s = lane;
+    for (; s + 7 * tpe < d.S; s += 8 * tpe) {
+      float4 v[8];
 #pragma unroll
-  for (int s = 0; s < 8; ++s)
-    if (s < d.S) {
-      float4& a = (s & 1) ? a1 : a0;
-      a.x += v[s].x; a.y += v[s].y; a.z += v[s].z; a.w += v[s].w;
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + (size_t)(s + u * tpe) * st);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) add4(a[u], v[u]);
     }
-  g = float4{a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w};
+    float4 v[7];
+#pragma unroll
+    for (int u = 0; u < 7; ++u)
+      if (s + u * tpe < d.S) v[u] = *reinterpret_cast<const float4*>(p + (size_t)(s + u * tpe) * st);
+#pragma unroll
+    for (int u = 0; u < 7; ++u)
+      if (s + u * tpe < d.S) add4(a[u], v[u]);
+    add4(a[0], a[1]); add4(a[2], a[3]); add4(a[4], a[5]); add4(a[6], a[7]);
+    add4(a[0], a[2]); add4(a[4], a[6]);
+    acc = a[0];
+    add4(acc, a[4]);
+  }
   e = d.dst_off + le;
-  return true;
+  if (tpe == 1) {
+    g = acc;
+    return in;
+  }
+  // the scalar path's fixed-order tree over the split-lanes (lane l += lane l + off), one
+  // level per round: the upper half's G * off = 128 float4 partials fill the 2 KB of LDS
+  float4* r4 = reinterpret_cast<float4*>(red);
+  for (int off = tpe >> 1; off > 0; off >>= 1) {
+    if (lane >= off && lane < 2 * off) r4[(lane - off) * G + gi] = acc;
+    __syncthreads();
+    if (lane < off) add4(acc, r4[lane * G + gi]);
+    __syncthreads();
+  }
+  g = acc;
+  return lane == 0 && in;
 }
 
 // Producer push of one finalised gradient element / float4 (XgmiPush; e: flat element, the
@@ -197,7 +233,7 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
   if (dsc.vec4) {
     int e;
     float4 g;
-    const bool mine = slab_reduce_vec4(dsc, blk, e, g);
+    const bool mine = slab_reduce_vec4(dsc, blk, red, e, g);
     if (mine) *reinterpret_cast<float4*>(grad + e) = g;
     if (mine && xp) xpush4(*xp, e, g);
     if (upd) update_vec4<KIND>(dsc, a, blk, red, mine, e, g);   // (grad_only: the reduced gradient is all)
@@ -311,8 +347,8 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
   int b_lo, b_hi, e = 0, n = 0;
   if (d.vec4) {
     b_lo = e_block0(d, blk);
-    b_hi = min(b_lo + 1024, d.dst_off + d.numel);
-    if (b_lo + 4 * t < b_hi) e = b_lo + 4 * t, n = 4;
+    b_hi = min(b_lo + vec4_epb(d), d.dst_off + d.numel);
+    if (t < 256 / d.tpe && b_lo + 4 * t < b_hi) e = b_lo + 4 * t, n = 4;   // (slab_reduce_vec4's map)
   } else {
     const int E = 256 / d.tpe;   // (slab_reduce_elem: thread t < E holds element t)
     b_lo = d.dst_off + (blk - d.blk0) * E;
