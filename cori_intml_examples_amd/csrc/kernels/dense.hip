@@ -53,8 +53,14 @@ __global__ __launch_bounds__(512) void dense_lds_kernel(const DenseFwdArgs a) {
   constexpr int STG = DL_KST * DL_ROWS * DL_LDA;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
   const int nblocks = (a.NT + 7) / 8, mgroups = (a.M + DL_ROWS - 1) / DL_ROWS;
-  const int nb = (int)(blockIdx.x % nblocks);
-  const int t2 = (int)(blockIdx.x / nblocks);
+  // XCD-aware order: workgroup b runs on XCD b % 8, so the n-blocks of one (m-group, K-split)
+  // -- which read the same activation slice -- are given consecutive logical indices on ONE
+  // XCD and share its L2 (else every n-block's XCD fetches the slice from HBM again)
+  const int nwg = (int)gridDim.x - (a.book ? 1 : 0);
+  int bid = (int)blockIdx.x;
+  if (nwg % 8 == 0 && (nwg / 8) % nblocks == 0) bid = (bid % 8) * (nwg / 8) + bid / 8;
+  const int nb = bid % nblocks;
+  const int t2 = bid / nblocks;
   const int mg = t2 % mgroups, s = t2 / mgroups;
   const int nt = nb * 8 + wave;
   const int ntc = min(nt, a.NT - 1);
@@ -64,8 +70,19 @@ __global__ __launch_bounds__(512) void dense_lds_kernel(const DenseFwdArgs a) {
   const int ks_lo = s * a.ks_per_split;
   const int ks_hi = min(a.KS, ks_lo + a.ks_per_split);
   const int nst = (ks_hi - ks_lo + DL_KST - 1) / DL_KST;
-  bf16x8 ra[DL_KST], rb[DL_KST], rbn[DL_KST];
-  auto issue = [&](int st) {
+  // weights stream to registers TWO stages ahead (three register sets in rotation: ~64 KB of
+  // weight loads in flight per workgroup -- one stage ahead left the HBM stream latency-bound);
+  // the activation slice goes one stage ahead through LDS (double-buffered)
+  bf16x8 ra[DL_KST], w0[DL_KST], w1[DL_KST], w2[DL_KST];
+  auto load_w = [&](bf16x8 (&w)[DL_KST], int st) {
+#pragma unroll
+    for (int kk = 0; kk < DL_KST; ++kk) {
+      const int k = ks_lo + st * DL_KST + kk;
+      const int ks = k < ks_hi ? k : ks_hi - 1;
+      w[kk] = load_bf16x8(a.wpk + ((size_t)(ks * a.NT + ntc) * 64 + lane) * 8);
+    }
+  };
+  auto load_a = [&](int st) {
 #pragma unroll
     for (int kk = 0; kk < DL_KST; ++kk) {
       const int k = ks_lo + st * DL_KST + kk;
@@ -73,39 +90,43 @@ __global__ __launch_bounds__(512) void dense_lds_kernel(const DenseFwdArgs a) {
       const int ks = kv ? k : ks_hi - 1;
       const int k0 = ks * 32 + (tid & 3) * 8;
       ra[kk] = load_bf16x8_if(kv && av && k0 < a.Ks, ap + ks * 32, a.x);
-      rbn[kk] = load_bf16x8(a.wpk + ((size_t)(ks * a.NT + ntc) * 64 + lane) * 8);
     }
   };
-  auto stash = [&](int buf) {
+  auto stash_a = [&](int buf) {
 #pragma unroll
-    for (int kk = 0; kk < DL_KST; ++kk) {
+    for (int kk = 0; kk < DL_KST; ++kk)
       *reinterpret_cast<bf16x8*>(As + buf * STG + kk * DL_ROWS * DL_LDA + (tid >> 2) * DL_LDA + (tid & 3) * 8) = ra[kk];
-      rb[kk] = rbn[kk];
-    }
   };
   f32x4 acc[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (nst > 0) {
-    issue(0);
-    stash(0);
-  }
-  __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int cur = st & 1;
+  auto step = [&](const bf16x8 (&cur)[DL_KST], bf16x8 (&ahead)[DL_KST], int st) {
     const bool more = st + 1 < nst;
-    if (more) issue(st + 1);
-    const bf16* A = As + cur * STG;
+    if (more) load_a(st + 1);
+    if (st + 2 < nst) load_w(ahead, st + 2);
+    const bf16* A = As + (st & 1) * STG;
 #pragma unroll
     for (int kk = 0; kk < DL_KST; ++kk) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(A + kk * DL_ROWS * DL_LDA + (t * 16 + r) * DL_LDA + 8 * g);
-        acc[t] = mfma16(af, rb[kk], acc[t]);
+        acc[t] = mfma16(af, cur[kk], acc[t]);
       }
     }
-    if (more) stash(cur ^ 1);
+    if (more) stash_a((st & 1) ^ 1);
     __syncthreads();
+  };
+  if (nst > 0) {
+    load_a(0);
+    load_w(w0, 0);
+    stash_a(0);
+  }
+  if (nst > 1) load_w(w1, 1);
+  __syncthreads();
+  for (int st = 0; st < nst; st += 3) {
+    step(w0, w2, st);
+    if (st + 1 < nst) step(w1, w0, st + 1);
+    if (st + 2 < nst) step(w2, w1, st + 2);
   }
   if (nt >= a.NT) return;
   if (a.mode == 1) {

@@ -574,7 +574,8 @@ class BatchPlan(GeometryMixin):
             if K.dense_big(g.NT, g.KS):
                 # large weights: ~256 workgroups (one per CU) of >= 8 k-steps; each owns
                 # 128 rows x 8 n-tiles, so every weight byte streams from HBM once
-                splits = max(1, min(cdiv(256, K.dense_groups(bs, g.NT, g.KS)), cdiv(g.KS, 8)))
+                splits = max(1, min(cdiv(tune("dense_big_wgs", 256), K.dense_groups(bs, g.NT, g.KS)),
+                                    cdiv(g.KS, tune("dense_big_minks", 8))))
             else:
                 # ~2048 16x16-tile waves: latency-bound small layers want parallelism
                 splits = max(1, min(g.KS, tune("dense_waves", 2048) // max(1, K.dense_groups(bs, g.NT, g.KS))))
