@@ -359,7 +359,7 @@ template <int KIND>
 __global__ __launch_bounds__(256) void reduce_optim_kernel(float* __restrict__ grad, const RedTable tab,
                                                            const OptimArgs a) {
   __shared__ __attribute__((aligned(16))) float red[512];   // (>= 2 KB: the tiled pack stage)
-  reduce_optim_block<KIND>(grad, tab, a, blockIdx.x, red);
+  reduce_optim_block<KIND, true>(grad, tab, a, blockIdx.x, red);
 }
 
 // a data-parallel table launch of its own: the early bucket's reduction + producer push (mode 1)

@@ -154,14 +154,32 @@ __device__ __forceinline__ void xpush4(const XgmiPush& xp, long long e, const fl
     *reinterpret_cast<float4*>(xp.inbox[j] + (size_t)xp.rank * xp.chunk + (size_t)(idx - (long long)j * xp.chunk)) = v;
 }
 
+// The optimizer state of the elements a thread will update, loaded BEFORE the reduction whose
+// result it updates them with: its memory round trip overlaps the slab loads instead of
+// following them (~1 us of the reduction launch's latency chain)
+struct OptState4 {
+  float4 p, s0, s1;
+};
+struct OptState1 {
+  float p, s0, s1;
+};
+__device__ __forceinline__ OptState4 load_state4(const OptimArgs& a, int e) {
+  const float4 z = {0.f, 0.f, 0.f, 0.f};
+  return OptState4{*reinterpret_cast<const float4*>(a.p + e), a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : z,
+                   a.s1 ? *reinterpret_cast<const float4*>(a.s1 + e) : z};
+}
+__device__ __forceinline__ OptState1 load_state1(const OptimArgs& a, int e) {
+  return OptState1{a.p[e], a.s0 ? a.s0[e] : 0.f, a.s1 ? a.s1[e] : 0.f};
+}
+
 // Keras update of the elements a table block's thread holds (vec4 descriptor: the float4 at
-// e; `mine` false: the thread holds none) -- with the tiled pack writes of a dense route
+// e, its state in st; `mine` false: the thread holds none) -- with the tiled pack writes of a dense route
 // (dsc.tile: the workgroup's 1024 updated weights are whole 8-row groups of the route, staged
 // as bf16 in LDS -- red: >= 2 KB -- and written as 16-byte vectors).  Every thread of the
 // workgroup calls it (it may synchronise the workgroup).
 template <int KIND>
 __device__ __forceinline__ void update_vec4(const RedDesc& dsc, const OptimArgs& a, int blk, float* red, bool mine,
-                                            int e, const float4& g) {
+                                            int e, const float4& g, const OptState4& st) {
   const PackRoute* tr = nullptr;
   if (a.nroutes && dsc.tile) {
     for (int r = 0; r < a.nroutes; ++r) {           // uniform: the descriptor's route
@@ -171,9 +189,7 @@ __device__ __forceinline__ void update_vec4(const RedDesc& dsc, const OptimArgs&
   }
   bf16* tl = reinterpret_cast<bf16*>(red);
   if (mine) {
-    float4 p = *reinterpret_cast<const float4*>(a.p + e);
-    float4 s0 = a.s0 ? *reinterpret_cast<const float4*>(a.s0 + e) : float4{0.f, 0.f, 0.f, 0.f};
-    float4 s1 = a.s1 ? *reinterpret_cast<const float4*>(a.s1 + e) : float4{0.f, 0.f, 0.f, 0.f};
+    float4 p = st.p, s0 = st.s0, s1 = st.s1;
     const float gs = a.grad_scale;
     opt_update<KIND>(a, a.st, p.x, g.x * gs, &s0.x, &s1.x);
     opt_update<KIND>(a, a.st, p.y, g.y * gs, &s0.y, &s1.y);
@@ -212,9 +228,8 @@ __device__ __forceinline__ void update_vec4(const RedDesc& dsc, const OptimArgs&
 }
 
 template <int KIND>
-__device__ __forceinline__ void update_elem(const OptimArgs& a, int e, float g) {
-  float p = a.p[e];
-  float s0 = a.s0 ? a.s0[e] : 0.f, s1 = a.s1 ? a.s1[e] : 0.f;
+__device__ __forceinline__ void update_elem(const OptimArgs& a, int e, float g, const OptState1& st) {
+  float p = st.p, s0 = st.s0, s1 = st.s1;
   opt_update<KIND>(a, a.st, p, g * a.grad_scale, &s0, &s1);
   a.p[e] = p;
   if (a.s0) a.s0[e] = s0;
@@ -225,25 +240,41 @@ __device__ __forceinline__ void update_elem(const OptimArgs& a, int e, float g) 
 // Reduction + Keras update of table block `blk`: the thread that produces an element's
 // gradient writes it and applies the update at once.  `red`: 256 floats of LDS.  xp (the
 // data-parallel step): also push the reduced elements to their owners, and no update.
-template <int KIND>
+// PRE: the optimizer state is loaded before the reduction (standalone kernels only: compiled
+// into the dual conv launch's extras it made the compiler copy the whole by-value DualExtra
+// argument to scratch -- 1.7 KB per lane, the launch 21 -> 90 us)
+template <int KIND, bool PRE = false>
 __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
                                                    int blk, float* red, const XgmiPush* xp = nullptr) {
   const RedDesc& dsc = tab.d[red_desc(tab, blk)];
   const bool upd = !a.grad_only && !xp;
+  const int t = threadIdx.x;
   if (dsc.vec4) {
+    OptState4 st{};
+    if (PRE && upd) {   // (slab_reduce_vec4's map: split-lane 0 of element group t % G holds the sum)
+      const int G = 256 / dsc.tpe, le = ((blk - dsc.blk0) * G + t % G) * 4;
+      if (t < G && le < dsc.numel) st = load_state4(a, dsc.dst_off + le);
+    }
     int e;
     float4 g;
     const bool mine = slab_reduce_vec4(dsc, blk, red, e, g);
     if (mine) *reinterpret_cast<float4*>(grad + e) = g;
     if (mine && xp) xpush4(*xp, e, g);
-    if (upd) update_vec4<KIND>(dsc, a, blk, red, mine, e, g);   // (grad_only: the reduced gradient is all)
+    if (!PRE && mine && upd) st = load_state4(a, e);
+    if (upd) update_vec4<KIND>(dsc, a, blk, red, mine, e, g, st);   // (grad_only: the reduced gradient is all)
   } else {
+    OptState1 st{};
+    if (PRE && upd) {   // (slab_reduce_elem's map: thread t < E holds element t of the block)
+      const int E = 256 / dsc.tpe, le = (blk - dsc.blk0) * E + t;
+      if (t < E && le < dsc.numel) st = load_state1(a, dsc.dst_off + le);
+    }
     int e;
     float g;
     const bool mine = slab_reduce_elem(tab, blk, red, e, g);
     if (mine) grad[e] = g;
     if (mine && xp) xpush1(*xp, e, g);
-    if (mine && upd) update_elem<KIND>(a, e, g);
+    if (!PRE && mine && upd) st = load_state1(a, e);
+    if (mine && upd) update_elem<KIND>(a, e, g, st);
   }
   if (a.defer_pack && !a.nroutes && upd && blk == 0 && threadIdx.x == 0) a.st->packs_stale = 1;
 }
@@ -355,6 +386,8 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
     b_hi = min(b_lo + E, d.dst_off + d.numel);
     if (t < E && b_lo + t < b_hi) e = b_lo + t, n = 1;
   }
+  OptState4 st4{};
+  OptState1 st1{};
   const int j0 = (int)((b_lo - x.lo) / C), j1 = (int)((b_hi - 1 - x.lo) / C);
   const long long ie = (long long)e - x.lo;     // bucket index
   const int own = n ? (int)(ie / C) : -1;
@@ -393,8 +426,10 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
       xs_put(grad + e, g, n);
     }
   }
-  if (d.vec4) update_vec4<KIND>(d, a, blk, red, n == 4, e, g);
-  else if (n) update_elem<KIND>(a, e, g.x);
+  if (n == 4) st4 = load_state4(a, e);
+  else if (n == 1) st1 = load_state1(a, e);
+  if (d.vec4) update_vec4<KIND>(d, a, blk, red, n == 4, e, g, st4);
+  else if (n) update_elem<KIND>(a, e, g.x, st1);
   if (a.defer_pack && !a.nroutes && blk == 0 && t == 0) a.st->packs_stale = 1;
   if (t == 0) x.ctrb[blk] = seq;
 }

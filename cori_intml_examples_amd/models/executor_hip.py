@@ -1001,7 +1001,7 @@ class BatchPlan(GeometryMixin):
         reducer = ex.reducer
         dp_early = []
         self.early_push, self.pushed, self.early_xchg, self.exchanged = {}, None, {}, False
-        self.bucket_xchg = {}
+        self.bucket_xchg, self.xchg_end = {}, None
         if reducer is not None:
             bucket_groups = reducer.configure(groups)
             # one bucket at the end of the backward (the adaptive plan for gradients <= 16 MB):
@@ -1028,10 +1028,18 @@ class BatchPlan(GeometryMixin):
                     for nm, (tab_, (elo, ehi), go) in self.early_red.items():
                         if not go:
                             continue
-                        nxt = self._xchg_launch(nm, elo, ehi) if tune("xgmi_xchg", True) else None
+                        # (xchg_at=end: the exchange as a launch of its own after the end-of-
+                        # backward reduction instead of extra workgroups of the next dual launch)
+                        at_end = tune("xchg_at", "dual") == "end"
+                        nxt = (("end" if at_end else self._xchg_launch(nm, elo, ehi))
+                               if tune("xgmi_xchg", True) else None)
                         pair = reducer.exchange_args(elo, ehi, tab_.nblocks) if nxt else None
                         if pair is not None:
-                            self.early_push[nm], self.early_xchg[nxt] = pair[0], (tab_, pair[1])
+                            self.early_push[nm] = pair[0]
+                            if at_end:
+                                self.xchg_end = (tab_, pair[1])
+                            else:
+                                self.early_xchg[nxt] = (tab_, pair[1])
                             self.pushed, self.exchanged = (elo, ehi), True
                             continue
                         xp = reducer.push_args(elo, ehi)
@@ -1095,7 +1103,8 @@ class BatchPlan(GeometryMixin):
             tab_n = sum(self.red_groups[i][1] - self.red_groups[i][0]
                         for i in bucket_groups[xk] if i not in dp_early)
             if btab.nblocks > 0 and early_n + tab_n == rhi - rlo:
-                fb = next(iter(self.early_xchg.values()))[0].nblocks if self.early_xchg else 0
+                fb = sum(t.nblocks for t in [e[0] for e in self.early_xchg.values()]
+                         + ([self.xchg_end[0]] if self.xchg_end else []))
                 x3 = reducer.exchange_args(blo, bhi, btab.nblocks, fbase=fb, fused=True)
                 if x3 is not None:
                     self.bucket_xchg[xk] = x3
@@ -1115,6 +1124,11 @@ class BatchPlan(GeometryMixin):
                 extra.append(("optim_b%d", lambda k: None if k == xk else
                               (lambda s: self._launch_optim_comm(k, s)), "comm"))
             # the xGMI bucket: all-reduce + Keras update in one kernel on the main stream
+            # (xchg_at=end: the early range's exchange + update after the end-of-backward reduction)
+            extra.append(("xchg_early_b%d", lambda k: None if (k != xk or self.xchg_end is None) else
+                          (lambda s: K.reduce_optim(ex.store.grad.data_ptr(), self.xchg_end[0],
+                                                    ex._optim_args(False, defer_pack=True), s, self.xchg_end[1])),
+                          "main"))
             extra.append(("xgmi_allreduce_optim_b%d", lambda k: None if (k != xk or k in self.bucket_xchg) else
                           (lambda s: reducer.launch_fused(ex.store.grad, ex._optim_args(False, defer_pack=True), s,
                                                           pushed=getattr(self, "pushed", None),
