@@ -75,6 +75,10 @@ static void check_last(const char* what) {
 // host-side checks of an early-bucket xGMI push / exchange (XgmiPush, args.h) against its
 // reduction table: every pointer the device code dereferences, the block count its flags are
 // indexed by, and float4 groups that never straddle an owner chunk
+// slab partials per split-lane the automatic split-lane choice of RedTable.add aims at
+// (INTML_TUNE red_lanes; set before the tables are built)
+static int g_red_lanes = 16;
+
 static void check_xgmi_push(const XgmiPush& x, const RedTable& t, const OptimArgs& a) {
   if (x.size < 1 || x.size > XGMI_MAX_RANKS || x.rank < 0 || x.rank >= x.size || x.chunk <= 0 || x.chunk % 4)
     throw std::invalid_argument("xgmi push: ranks / chunk");
@@ -291,14 +295,14 @@ PYBIND11_MODULE(_kernels, m) {
           // split-lanes as the scalar path (~S/16 partials per thread); tiled dense blocks
           // need the 1024-element map (tpe 1)
           d.tpe = 1;
-          while (d.tpe < 64 && d.tpe * 16 < S) d.tpe *= 2;
+          while (d.tpe < 64 && d.tpe * g_red_lanes < S) d.tpe *= 2;
           if (d.tpe > 1) d.tile = 0;
         } else if (tpe > 0) {
           if (tpe > 256 || (tpe & (tpe - 1))) throw std::invalid_argument("tpe: power of 2 <= 256");
           d.tpe = tpe;
         } else {
           d.tpe = 1;                                    // ~S/16 partials per thread (sweep:
-          while (d.tpe < 64 && d.tpe * 16 < S) d.tpe *= 2;   // scripts/red_sweep.py)
+          while (d.tpe < 64 && d.tpe * g_red_lanes < S) d.tpe *= 2;   // scripts/red_sweep.py)
         }
         d.blk0 = t.nblocks;
         const int epb = d.vec4 ? 1024 / d.tpe : 256 / d.tpe;
@@ -307,6 +311,10 @@ PYBIND11_MODULE(_kernels, m) {
       py::arg("type"), py::arg("KH"), py::arg("KW"), py::arg("Cin"), py::arg("Cout"), py::arg("Cs"), py::arg("tpe") = -1);
 
   m.attr("STEP_STATE_BYTES") = (int)sizeof(StepState);
+  m.def("set_red_lanes", [](int n) {
+    if (n < 1 || n > 256) throw std::invalid_argument("red_lanes: 1..256");
+    g_red_lanes = n;
+  });
   static_assert(sizeof(PackRoute) == 56 && offsetof(PackRoute, fwd) == 40, "PackRoute layout (models/plan routes)");
   m.attr("PACK_ROUTE_BYTES") = (int)sizeof(PackRoute);
   m.attr("MAX_ROUTES") = MAX_ROUTES;

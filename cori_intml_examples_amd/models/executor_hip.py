@@ -179,6 +179,7 @@ class HipExecutor(Executor):
     def __init__(self, plan: Plan, store, optimizer, seed: int):
         super().__init__(plan, store, optimizer, seed)
         self.K = kernels()
+        self.K.set_red_lanes(int(tune("red_lanes", 16)))   # slab partials per reduction split-lane
         self.device = store.device
         if self.device.type != "cuda":
             raise RuntimeError("HipExecutor needs a GPU device")
