@@ -476,7 +476,10 @@ __global__ __launch_bounds__(NTH) void conv_stack_kernel(const ConvStackArgs A) 
   lbf16* wlds = (lbf16*)(smem + A.off_w);
   // two argmax-code planes (layer parity): a layer's epilogue writes its plane while slower
   // waves may still copy the previous layer's codes out (no barrier between those phases)
-  LDS uint8_t* codes_pl[2] = {(LDS uint8_t*)(smem + A.off_codes), (LDS uint8_t*)(smem + A.off_codes2)};
+  // (a select, not a 2-entry array: indexed by a non-unrolled layer loop the array went to
+  // scratch in the MNIST instances)
+  LDS uint8_t* const codes_p0 = (LDS uint8_t*)(smem + A.off_codes);
+  LDS uint8_t* const codes_p1 = (LDS uint8_t*)(smem + A.off_codes2);
   const uint32_t step = A.st ? (uint32_t)A.st->t + (uint32_t)A.step_inc : 0u;
   STACK_STAMP(0);
   if (tid < 8) ((LDS uint32_t*)zl)[tid] = 0u;
@@ -673,7 +676,7 @@ __global__ __launch_bounds__(NTH) void conv_stack_kernel(const ConvStackArgs A) 
       obase = A.rows[l + 1][sp][4], OH = A.rows[l + 1][sp][5], ol = N.pad_l, OW = N.Wo + N.KW - 1;
       ORS = N.xrow, OPS = N.xpix;
     }
-    LDS uint8_t* codes = codes_pl[l & 1];
+    LDS uint8_t* codes = (l & 1) ? codes_p1 : codes_p0;
     {
       LDS bf16x8* z = (LDS bf16x8*)out;
       const bf16x8 zero8 = zero_bf16x8();
