@@ -419,16 +419,31 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
       __builtin_amdgcn_wave_barrier();
     } else {
       // unpooled forward and dgrad (mode 1): stage the TM tiles as bf16, then one copy loop
+      // The staged rows are XOR-swizzled by 16-byte chunk: chunk c of row q sits at chunk
+      // c ^ (((q >> 2) << 1) & (LDC / 8 - 1)).  A store instruction's four lane groups write
+      // rows 4 apart, which unswizzled map to the same banks (4-way conflicts at LDC 64).
       bf16* epb = reinterpret_cast<bf16*>(ep);                // [TM*16 pixels][LDC]
       const bool fwd = mode == 0;
+      constexpr int CHM = NTC * 2 - 1;                        // chunk-index mask (LDC / 8 - 1)
+      float bvn[NTC];
+#pragma unroll
+      for (int nt = 0; nt < NTC; ++nt) {
+        const int n = (nt0 + nt) * 16 + r;
+        bvn[nt] = (fwd && a.bias && n < a.N) ? a.bias[n] : 0.f;
+      }
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int p = (tb + t) * 16 + g * 4 + j;
-          const int pc = p < npix ? p : 0;
-          const int pyl = fwo.div(pc);
-          const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (pc - pyl * a.Wo);
+          const int q = t * 16 + g * 4 + j;
+          const int sw = ((q >> 2) << 1) & CHM;
+          size_t m = 0;
+          if (fwd && a.drop_thr) {
+            const int p = (tb + t) * 16 + g * 4 + j;
+            const int pc = p < npix ? p : 0;
+            const int pyl = fwo.div(pc);
+            m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (pc - pyl * a.Wo);
+          }
 #pragma unroll
           for (int nt = 0; nt < NTC; ++nt) {
             const int n = (nt0 + nt) * 16 + r;
@@ -436,14 +451,15 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
             if (fwd) {
               x = 0.f;
               if (n < a.N) {
-                x = acc[t][nt][j] + (a.bias ? a.bias[n] : 0.f);
+                x = acc[t][nt][j] + bvn[nt];
                 if (a.relu) x = fmaxf(x, 0.f);
                 if (a.drop_thr)
                   x = dropout_keep((uint32_t)(m * a.N + n), a.seed, a.stream_id, step, a.drop_thr) ? x * a.drop_scale
                                                                                                  : 0.f;
               }
             }
-            epb[(t * 16 + g * 4 + j) * LDC + nt * 16 + r] = f2bf(x);
+            const int col = nt * 16 + r;
+            epb[q * LDC + (((col >> 3) ^ sw) << 3) + (col & 7)] = f2bf(x);
           }
         }
       }
@@ -454,7 +470,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
         const int p = tb * 16 + pr;
         const int pyl = fwo.div(p);
         const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (p - pyl * a.Wo);
-        const bf16x8 val = *reinterpret_cast<const bf16x8*>(epb + pr * LDC + c8 * 8);
+        const bf16x8 val = *reinterpret_cast<const bf16x8*>(epb + pr * LDC + ((c8 ^ (((pr >> 2) << 1) & CHM)) << 3));
         if (fwd) {
           *reinterpret_cast<bf16x8*>(a.out + m * a.Cs_out + nt0 * 16 + c8 * 8) = val;
         } else {
