@@ -425,6 +425,8 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
       bf16* epb = reinterpret_cast<bf16*>(ep);                // [TM*16 pixels][LDC]
       const bool fwd = mode == 0;
       constexpr int CHM = NTC * 2 - 1;                        // chunk-index mask (LDC / 8 - 1)
+      // the block is whole output rows: pixel p of the block is output pixel mrow0 + p
+      const size_t mrow0 = ((size_t)b * a.Ho + oy0) * a.Wo;
       float bvn[NTC];
 #pragma unroll
       for (int nt = 0; nt < NTC; ++nt) {
@@ -440,9 +442,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
           size_t m = 0;
           if (fwd && a.drop_thr) {
             const int p = (tb + t) * 16 + g * 4 + j;
-            const int pc = p < npix ? p : 0;
-            const int pyl = fwo.div(pc);
-            m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (pc - pyl * a.Wo);
+            m = mrow0 + (size_t)(p < npix ? p : 0);
           }
 #pragma unroll
           for (int nt = 0; nt < NTC; ++nt) {
@@ -467,9 +467,7 @@ __device__ __forceinline__ void conv_halo_body(const ConvMMArgs& a, const int bx
       const int np = max(0, min(TM * 16, npix - tb * 16));
       for (int c = lane; c < np * cch; c += 64) {
         const int pr = fcch.div(c), c8 = c - pr * cch;
-        const int p = tb * 16 + pr;
-        const int pyl = fwo.div(p);
-        const size_t m = ((size_t)b * a.Ho + oy0 + pyl) * a.Wo + (p - pyl * a.Wo);
+        const size_t m = mrow0 + (size_t)(tb * 16 + pr);
         const bf16x8 val = *reinterpret_cast<const bf16x8*>(epb + pr * LDC + ((c8 ^ (((pr >> 2) << 1) & CHM)) << 3));
         if (fwd) {
           *reinterpret_cast<bf16x8*>(a.out + m * a.Cs_out + nt0 * 16 + c8 * 8) = val;

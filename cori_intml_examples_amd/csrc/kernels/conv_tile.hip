@@ -192,10 +192,17 @@ __device__ __forceinline__ void tile_epilogue(const ConvMMArgs& a, const TileRow
       }
       __builtin_amdgcn_wave_barrier();
     } else {
+      // rows staged with their 16-byte chunks XOR-swizzled by row group: chunk c of row q at
+      // c ^ ((q >> 2) * 4 & (chunks - 1)) -- unswizzled, the four lane groups of a store (rows
+      // 4 apart, 1-2 KB apart) hit the same banks
+      constexpr int CHK = NW * 4 - 1;                 // 16-byte chunks per row - 1
 #pragma unroll
       for (int n = 0; n < NW; ++n)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) ep[(g * 4 + j) * LDC + n * 16 + r] = acc[t][n][j];
+        for (int j = 0; j < 4; ++j) {
+          const int col = n * 16 + r, sw = (g * 4) & CHK;   // (row g * 4 + j: (row >> 2) == g)
+          ep[(g * 4 + j) * LDC + (((col >> 2) ^ sw) << 2) + (col & 3)] = acc[t][n][j];
+        }
       __builtin_amdgcn_wave_barrier();
       const int np = (int)min((long long)16, nrows - tile * 16);
       for (int c = lane; c < np * cch; c += 64) {
@@ -207,8 +214,9 @@ __device__ __forceinline__ void tile_epilogue(const ConvMMArgs& a, const TileRow
           m = ((size_t)b * a.Ho + oy) * a.Wo + ox;
         }
         float v[8];
-        *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(ep + pr * LDC + c8 * 8);
-        *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(ep + pr * LDC + c8 * 8 + 4);
+        const int sw = ((pr >> 2) * 4) & CHK;
+        *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(ep + pr * LDC + (((2 * c8) ^ sw) << 2));
+        *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(ep + pr * LDC + (((2 * c8 + 1) ^ sw) << 2));
         const int n0 = cbase + c8 * 8;
         if (a.mode == 1) {
           bwd_through_store8(a.bt, m, n0, v, step);
