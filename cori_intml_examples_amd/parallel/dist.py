@@ -389,7 +389,7 @@ def adaptive_bucket_bytes(groups: Sequence[Tuple[int, int]], size: int = 1) -> i
     return max(16 << 20, total // 4)
 
 
-def data_plane() -> str:
+def data_plane(grad_bytes: Optional[int] = None) -> str:
     """The gradient data plane of the native (captured) reducer, from ``INTML_XGMI``:
     "xgmi" ("1"): the whole gradient on the xGMI plane -- the early (head / dense) range
     all-reduced and updated inside the backward (exchange), the rest by the end-of-backward
@@ -404,7 +404,7 @@ def data_plane() -> str:
         return "hybrid"
     if mode in ("0", "off", "false", "rccl"):
         return "rccl"
-    return auto_plane()
+    return auto_plane(grad_bytes)
 
 
 def device_key(device) -> str:
@@ -418,12 +418,16 @@ def device_key(device) -> str:
     return socket.gethostname() + "/" + ident
 
 
-def auto_plane() -> str:
+def auto_plane(grad_bytes: Optional[int] = None) -> str:
     """The default plane: "xgmi" when every rank has a GPU of its own on ONE node (the xGMI
-    links reach every peer; the all-reduce of the early range overlaps the conv backward), else
-    "rccl".  The xGMI plane is still only used after its collective setup and self-test --
+    links reach every peer; the all-reduce of the early range overlaps the conv backward) and
+    the gradient is small enough for one fused bucket (<= 16 MB, the adaptive single-bucket
+    bound: the 138 MB legacy gradient keeps RCCL buckets forked onto the comm stream, which
+    overlap the backward), else "rccl".  The xGMI plane is still only used after its collective setup and self-test --
     the two-shot kernel and the exchange protocol, on every rank -- pass the vote; otherwise
     the step keeps the RCCL all-reduce (NativeGradReducer._setup_xgmi)."""
+    if grad_bytes is not None and grad_bytes > (16 << 20):
+        return "rccl"
     if is_initialized():
         st = _st()
         if (st.size > 1 and st.local_size == st.size and torch.cuda.is_available()
@@ -466,7 +470,8 @@ class NativeGradReducer:
         return True
 
     def configure(self, groups: Sequence[Tuple[int, int]]) -> List[List[int]]:
-        self.plane = data_plane() if self.comm is not None else "xgmi"
+        self.plane = (data_plane(4 * sum(hi - lo for lo, hi in groups)) if self.comm is not None
+                      else "xgmi")
         bb = self.bucket_bytes
         if self.plane == "xgmi":
             bb = 1 << 62                    # the whole gradient is ONE fused xGMI bucket

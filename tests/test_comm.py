@@ -294,6 +294,7 @@ def test_auto_plane(monkeypatch):
     st.size = st.local_size = 1              # one rank
     assert D.data_plane() == "rccl"
     st.size = st.local_size = 8
+    assert D.data_plane(2 << 20) == "xgmi" and D.data_plane(138 << 20) == "rccl"   # RPV / legacy gradients
     monkeypatch.setenv("INTML_XGMI", "rccl")
     assert D.data_plane() == "rccl"
     monkeypatch.setenv("INTML_XGMI", "xgmi")
