@@ -299,3 +299,78 @@ def test_auto_plane(monkeypatch):
     assert D.data_plane() == "rccl"
     monkeypatch.setenv("INTML_XGMI", "xgmi")
     assert D.data_plane() == "xgmi"
+
+
+def _fake_xgmi(rank=1, size=4, chunk=1024, shared=False):
+    """An XgmiAllreduce with its device buffers replaced by fake addresses (no GPU): for the
+    host-side argument logic of the exchange."""
+    import torch
+    from cori_intml_examples_amd.ops.hip import kernels
+    from cori_intml_examples_amd.parallel import xgmi as X
+    K = kernels()
+    x = object.__new__(X.XgmiAllreduce)
+    x.K, x.rank, x.size, x.chunk, x.n, x.shared = K, rank, size, chunk, chunk * size, shared
+    x.off_f1, x.off_f2, x.off_ab = 0, 4 * X._FLAG_WORDS, 8 * X._FLAG_WORDS
+    x.off_bf1 = X._align(x.off_ab + 256, 256)
+    x.off_bf2 = x.off_bf1 + 4 * X.XCHG_MAX_BLOCKS * 8
+    x.off_in = X._align(x.off_bf2 + 4 * X.XCHG_MAX_BLOCKS * 8, 256)
+    x.off_out = X._align(x.off_in + 4 * chunk * size, 256)
+    x.bases = [(j + 1) << 32 for j in range(size)]
+    x.ctrb = torch.zeros(X.XCHG_MAX_BLOCKS, dtype=torch.int32)
+    x.err = torch.zeros(4, dtype=torch.int32)
+    x.args = K.XgmiArgs()
+    x.args.timeout_ticks = 12345
+    return x, K, X
+
+
+def test_exchange_push_args():
+    """Host side of the exchange (XgmiPush): modes, block-flag slot offsets, looping workgroups
+    only for ranks sharing a GPU, and the capacity / size-1 rules."""
+    x, K, X = _fake_xgmi()
+    p1 = x.push_args(0, mode=1, nblk=10, fbase=5)
+    p2 = x.push_args(0, mode=2, nblk=10, fbase=5)
+    assert (p1.mode, p2.mode, p1.nblk, p2.nblk, p1.nx, p2.nx) == (1, 2, 10, 10, 0, 0)
+    assert p2.ctrb == x.ctrb.data_ptr() + 4 * 5 and p2.err == x.err.data_ptr() and p2.timeout_ticks == 12345
+    assert p1.rank == 1 and p1.size == 4 and p1.chunk == 1024
+    assert x.push_args(0, mode=2, nblk=X.XCHG_MAX_BLOCKS, fbase=1) is None      # past the flag slots
+    assert x.push_args(0).nblk == 0                                            # plain producer push
+    xs, _, _ = _fake_xgmi(shared=True)
+    assert xs.push_args(0, mode=2, nblk=10).nx > 0 and xs.push_args(0, mode=1, nblk=10).nx == 0
+    x1, _, _ = _fake_xgmi(rank=0, size=1)
+    assert x1.push_args(0) is None and x1.push_args(0, mode=3, nblk=4).mode == 3   # size 1: exchange only
+
+
+def test_exchange_arguments_validated_before_launch():
+    """reduce_optim / dual_halo check an XgmiPush against its table on the host (bindings.cpp
+    check_xgmi_push) before anything is launched: mode vs grad_only, block count, float4
+    alignment, the table inside the bucket."""
+    x, K, X = _fake_xgmi(rank=0, size=2, chunk=1024)
+    tab = K.RedTable()
+    tab.add(4096, 256, 2, 16, 0, 256, 2, 1, 1, 16, 16, 16, -1)     # RED_FLATW float4, elements [0, 256)
+    a = K.OptimArgs()
+    a.grad_only = 0
+    xp = x.push_args(0, mode=1, nblk=tab.nblocks)
+    with pytest.raises(ValueError, match="grad_only"):
+        K.reduce_optim(0, tab, a, 0, xp)                   # mode 1 needs a grad_only table
+    xp2 = x.push_args(0, mode=2, nblk=tab.nblocks + 1)
+    with pytest.raises(ValueError, match="nblk"):
+        K.reduce_optim(0, tab, a, 0, xp2)                  # flags sized for another table
+    out = K.RedTable()
+    out.add(4096, 4096, 2, 16, 2048, 256, 2, 1, 1, 16, 16, 16, -1)   # elements past the 2 x 1024 bucket
+    with pytest.raises(ValueError, match="outside"):
+        K.reduce_optim(0, out, a, 0, x.push_args(0, mode=2, nblk=out.nblocks))
+
+
+def test_exchange_launch_choice():
+    """_xchg_launch: the dual launch after the reducing one carries the exchange, unless a
+    launch from there on reads the range's packs (the update rewrites them)."""
+    import types
+    from cori_intml_examples_amd.models.executor_hip import BatchPlan
+    fn = BatchPlan._xchg_launch
+    plan = types.SimpleNamespace(launches=[("head", None), ("dense_bwd", None), ("wgrad_dgrad_conv2", None),
+                                           ("wgrad_dgrad_conv1", None), ("wgrad_conv0", None)],
+                                 pack_readers=[("dense_bwd", 100, 200), ("wgrad_dgrad_conv2", 50, 60)])
+    assert fn(plan, "wgrad_dgrad_conv2", 100, 200) == "wgrad_dgrad_conv1"
+    plan.pack_readers.append(("wgrad_conv0", 150, 160))
+    assert fn(plan, "wgrad_dgrad_conv2", 100, 200) is None
+    assert fn(plan, "wgrad_dgrad_conv1", 0, 10) is None     # no later dual launch
