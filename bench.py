@@ -170,6 +170,7 @@ def probe_data_planes(args, size, dev, g, B, chunk):
       xgmi         the xGMI plane (fit()'s default on one node, dist.auto_plane): the head /
                    dense range pushed to its owners, all-reduced and updated inside the
                    backward (exchange), the conv layers' in the end-of-backward reduction,
+      xgmi_end     the xGMI plane with the exchange as a launch of its own after the backward,
       rccl         the RCCL plane: one all-reduce + optimizer of the whole gradient at the end
                    of the backward (dist.adaptive_bucket_bytes),
       rccl_single  one RCCL all-reduce of the whole gradient at the end of the backward,
@@ -185,7 +186,13 @@ def probe_data_planes(args, size, dev, g, B, chunk):
     if ((size < 2 and not forced) or args.via_fit or "INTML_XGMI" in os.environ
             or "INTML_BUCKET_BYTES" in os.environ):
         return None
-    cands = (("xgmi", {"INTML_XGMI": "xgmi"}), ("rccl", {"INTML_XGMI": "rccl"}),
+    base_tune = os.environ.get("INTML_TUNE", "")
+    end_tune = ",".join(x for x in (base_tune, "xchg_at=end") if x)
+    cands = (("xgmi", {"INTML_XGMI": "xgmi"}),
+             # the exchange as its own launch after the backward: 2 us less fixed cost, the early
+             # range's all-reduce no longer overlapping the conv backward -- the wire decides
+             ("xgmi_end", {"INTML_XGMI": "xgmi", "INTML_TUNE": end_tune}),
+             ("rccl", {"INTML_XGMI": "rccl"}),
              ("rccl_single", {"INTML_XGMI": "rccl", "INTML_BUCKET_BYTES": str(1 << 40)}),
              ("rccl_forked", {"INTML_XGMI": "rccl", "INTML_BUCKET_BYTES": str(1 << 20)}),
              ("hybrid", {"INTML_XGMI": "hybrid", "INTML_BUCKET_BYTES": str(1 << 20)}))
@@ -218,6 +225,8 @@ def probe_data_planes(args, size, dev, g, B, chunk):
         finally:
             for k in env:
                 os.environ.pop(k, None)
+            if base_tune:
+                os.environ["INTML_TUNE"] = base_tune
     best = min(((v, k) for k, v in res.items() if isinstance(v, float)), default=(0, "rccl"))[1]
     os.environ.update(dict(cands)[best])
     res["chosen"] = best
