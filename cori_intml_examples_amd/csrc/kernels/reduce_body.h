@@ -386,8 +386,11 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
     b_hi = min(b_lo + E, d.dst_off + d.numel);
     if (t < E && b_lo + t < b_hi) e = b_lo + t, n = 1;
   }
+  // (the state the update needs is loaded now: its round trip overlaps the waits)
   OptState4 st4{};
   OptState1 st1{};
+  if (n == 4) st4 = load_state4(a, e);
+  else if (n == 1) st1 = load_state1(a, e);
   const int j0 = (int)((b_lo - x.lo) / C), j1 = (int)((b_hi - 1 - x.lo) / C);
   const long long ie = (long long)e - x.lo;     // bucket index
   const int own = n ? (int)(ie / C) : -1;
@@ -426,8 +429,6 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
       xs_put(grad + e, g, n);
     }
   }
-  if (n == 4) st4 = load_state4(a, e);
-  else if (n == 1) st1 = load_state1(a, e);
   if (d.vec4) update_vec4<KIND>(d, a, blk, red, n == 4, e, g, st4);
   else if (n) update_elem<KIND>(a, e, g.x, st1);
   if (a.defer_pack && !a.nroutes && blk == 0 && t == 0) a.st->packs_stale = 1;
