@@ -16,13 +16,25 @@ __global__ __launch_bounds__(256) void dual_halo_kernel(const ConvMMArgs ca, con
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int id = blockIdx.x;
   if (x.n_r) {   // early-bucket reduction + optimizer workgroups
-    const int r = x.rfirst ? id : id - (int)gridDim.x + x.n_r;
+    // rfirst 0: the extras last in the grid; 1: first; 2: interleaved -- workgroup e * q of
+    // the grid (q = grid / n_r) is extra e, so they dispatch spread among the conv workgroups
+    // (interleaving needs q >= 2: with more extras than conv workgroups they go first)
+    const bool inter = x.rfirst == 2 && (int)gridDim.x >= 2 * x.n_r;
+    const bool first = x.rfirst == 1 || (x.rfirst == 2 && !inter);
+    int r;
+    if (inter) {
+      const int q = (int)gridDim.x / x.n_r, e = id / q;
+      r = (id - e * q == 0 && e < x.n_r) ? e : -1;
+      if (r < 0) id -= min(x.n_r, e + 1);
+    } else {
+      r = first ? id : id - (int)gridDim.x + x.n_r;
+    }
     if (r >= 0 && r < x.n_r) {
       if constexpr (XP) xgmi_early_block<false>(x.grad, x.rt, x.ro, r, reinterpret_cast<float*>(smem), x.xp);
       else reduce_optim_block_rt(x.grad, x.rt, x.ro, r, reinterpret_cast<float*>(smem));
       return;
     }
-    if (x.rfirst) id -= x.n_r;
+    if (first) id -= x.n_r;
   }
   // production bodies only: the dgrad epilogue fixed to backward-through (MODE 1), no
   // ablation / stamp code (launch_dual_halo declines args that ask for them; the executor

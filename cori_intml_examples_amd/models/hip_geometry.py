@@ -227,7 +227,8 @@ class GeometryMixin:
         xe = (getattr(self, "early_xchg", None) or {}).get(name)
         kw = {}
         if early is not None:   # this launch also carries an early bucket's reduction (+ optimizer)
-            kw.update(rt=early[0], ro=self._early_ro(early), rgrad=ex.store.grad.data_ptr())
+            kw.update(rt=early[0], ro=self._early_ro(early), rgrad=ex.store.grad.data_ptr(),
+                      rfirst=int(tune("early_rfirst", 0)))   # (0: last in the grid, 1: first, 2: interleaved)
             if xp is not None:
                 kw["xp"] = xp
         elif xe is not None:
