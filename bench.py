@@ -198,10 +198,12 @@ def probe_data_planes(args, size, dev, g, B, chunk):
              ("hybrid", {"INTML_XGMI": "hybrid", "INTML_BUCKET_BYTES": str(1 << 20)}))
     probe = max(chunk * 6, 48)
     res = {}
+    numel = None
     for plane, env in cands:
         os.environ.update(env)
         try:
             model, shape, ncls, *_ = build(args, size, True, dev)
+            numel = model.store.numel
             hvd.broadcast_global_variables(0, model=model)
             data = synthetic(max(args.samples, B * 4), shape, ncls, model._executor, dev, g)
             e, _ = time_steps(model, data, B, probe, min(args.warmup, 16), chunk, g, dev,
@@ -230,6 +232,12 @@ def probe_data_planes(args, size, dev, g, B, chunk):
     best = min(((v, k) for k, v in res.items() if isinstance(v, float)), default=(0, "rccl"))[1]
     os.environ.update(dict(cands)[best])
     res["chosen"] = best
+    # persist the measured choice for fit()'s auto plane on this host / world size / gradient
+    # size class (dist.auto_plane: without a verdict, auto means RCCL)
+    if numel and any(isinstance(v, float) for v in res.values()) and (not hvd.is_initialized() or hvd.rank() == 0):
+        from cori_intml_examples_amd.parallel import dist as D
+        res["verdict_file"] = D.record_verdict(size, 4 * numel, best,
+                                               {k: v for k, v in res.items() if isinstance(v, float)})
     return res
 
 
@@ -565,8 +573,8 @@ def main():
                            if xk is not None else
                            "rccl-native" if comm is not None else ("torch-" + str(st.backend))),
             # what a fit() / train_rpv run without the probe uses (INTML_XGMI unset)
-            "default_plane": (("xgmi" if auto_plane() == "xgmi" else "rccl-native") if comm is not None
-                              else ("torch-" + str(st.backend))),
+            "default_plane": ((lambda p: "rccl-native" if p == "rccl" else p)(auto_plane(4 * model.store.numel))
+                              if comm is not None else ("torch-" + str(st.backend))),
             "env_plane": data_plane(),
             "rccl_nranks": comm.nranks if comm is not None else None,
             "world_size": size,

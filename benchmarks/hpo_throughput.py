@@ -149,15 +149,16 @@ def run_cray(a, n_gpu):
     hist = ev.history
     ok = [h for h in hist if h["ok"]]
     per_hour = len(ok) / wall * 3600
+    # the data plane every evaluation's DP training reported (train_rpv's History.data_plane)
+    planes = sorted({h.get("data_plane") or "none reported" for h in ok})
     return {
         "metric": "HPO evaluations/hour (CrayHPO_rpv genetic, %d-rank DP train_rpv per evaluation, %d epochs, "
                   "%d train / %d valid, batch %d/rank)" % (per, a.epochs, a.n_train, a.n_valid, a.batch_size),
         "value": round(per_hour, 1), "unit": "evaluations/hour", "n_gpus": n_gpu,
         "slots": len(ev.slots), "gpus_per_eval": per,
         "oversubscribed": any(ev.oversubscribed(sl) for sl in ev.slots),
-        "data_plane": ("gloo (cpu)" if not n_gpu else
-                       "gloo (ranks share a GPU)" if any(ev.oversubscribed(sl) for sl in ev.slots) else
-                       "rccl" if per > 1 else "none (1 rank)"),
+        "data_plane": planes,
+        "concurrent_evals": len(ev.slots),
         "evaluations": len(ok), "failed": len(hist) - len(ok), "wall_s": round(wall, 2),
         "mean_eval_s": round(sum(h["seconds"] for h in ok) / max(1, len(ok)), 2),
         "best_fom": min((h["fom"] for h in ok), default=None),

@@ -370,7 +370,8 @@ struct XgmiPush {
   long long lo = 0;                      // first flat element of the all-reduce bucket
   float* inbox[XGMI_MAX_RANKS] = {};     // rank j's inbox [P][chunk] (as mapped here)
   int mode = 1;                          // 1 reduce + push (+ block flags), 2 exchange + update,
-                                         // 3 both in one launch (the end-of-backward bucket)
+                                         // 3 both in one launch (the end-of-backward bucket),
+                                         // 4 / 5 the owner / finish halves of 2 (reduce_body.h)
   float* outbox[XGMI_MAX_RANKS] = {};    // rank j's outbox [P * chunk] (bucket index)
   unsigned* bflag1[XGMI_MAX_RANKS] = {}; // rank j's per-block push flags [nblk][P] (null: no flags)
   unsigned* bflag2[XGMI_MAX_RANKS] = {}; // rank j's per-block owner-sum flags [nblk][P]
@@ -383,6 +384,10 @@ struct XgmiPush {
   int p1 = 0;                            // size 1, mode 3: 1 = keep the exchange structure (push /
                                          // flag / re-read: a measurement of its fixed cost); 0 =
                                          // reduce + update in place (no peers: nothing to exchange)
+  int b_lo = 0, b_hi = 0;                // mode 4: the table blocks [b_lo, b_hi) its workgroups cover
+  int fence = 1;                         // 1: system-scope release before a flag store, acquire after
+                                         // a poll (HIP memory model); 3: none (uncached payload:
+                                         // drained stores + sc1 loads; opt-in, xgmi.hip header)
 };
 
 // Optional extra workgroups of the dual conv backward launch: the fused reduction + optimizer
@@ -415,8 +420,8 @@ struct XgmiArgs {
   int sub = 0;                   // elements per workgroup slice of a chunk (multiple of 4)
   long long timeout_ticks = 0;   // bounded waits: give up after this many wall_clock64 ticks (100 MHz)
   int mode = 1;                  // 0: sum only (reduced gradient -> grad); 1: + optimizer
-  int fence = 3;                 // fences around the flags: 3 none + sc1 payload loads, 2 agent acquire,
-                                 // 1 system release + acquire, 0 none (xgmi.hip)
+  int fence = 1;                 // fences around the flags: 1 system release + acquire (default),
+                                 // 3 none + sc1 payload loads, 2 agent acquire, 0 none (xgmi.hip)
   // bucket elements [skip_lo, skip_hi) were pushed to their owners already (XgmiPush, in the
   // backward): phase 1 skips every float4 wholly inside; skip_mode 2: they were also
   // all-reduced and updated there (exchange), so no phase touches them

@@ -47,6 +47,8 @@ int conv_stack_tabn();
 void launch_prologue(const PrologueArgs& a, const PackTable& tab, hipStream_t s);
 int gather_gx(int R);
 void launch_slab_reduce(float* grad, int lo, int hi, const RedTable& tab, hipStream_t s);
+void launch_reduce_optim_end(float* grad, const RedTable& tc, const OptimArgs& a, const XgmiPush& xc,
+                             const RedTable& te, const XgmiPush& xe, hipStream_t s);
 void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, hipStream_t s,
                          const XgmiPush* xp = nullptr);
 void launch_optim(const OptimArgs& a, const PackTable& tab, hipStream_t s);
@@ -82,7 +84,9 @@ static int g_red_lanes = 16;
 static void check_xgmi_push(const XgmiPush& x, const RedTable& t, const OptimArgs& a) {
   if (x.size < 1 || x.size > XGMI_MAX_RANKS || x.rank < 0 || x.rank >= x.size || x.chunk <= 0 || x.chunk % 4)
     throw std::invalid_argument("xgmi push: ranks / chunk");
-  if (x.mode < 1 || x.mode > 3) throw std::invalid_argument("xgmi push: mode");
+  if (x.mode < 1 || x.mode > 5) throw std::invalid_argument("xgmi push: mode");
+  if (x.mode == 4 && (x.b_lo < 0 || x.b_hi > t.nblocks || x.b_lo > x.b_hi))
+    throw std::invalid_argument("xgmi push: mode-4 block range");
   if (x.size == 1 && x.mode == 1 && !x.bflag1[0]) throw std::invalid_argument("xgmi push: nothing to push");
   if ((x.mode == 1) != (a.grad_only != 0))
     throw std::invalid_argument("xgmi push: mode 1 needs a grad_only table, mode 2 an updating one");
@@ -274,6 +278,23 @@ PYBIND11_MODULE(_kernels, m) {
       .def(py::init([]() { RedTable t; memset(&t, 0, sizeof(t)); return t; }))
       .def_readonly("n", &RedTable::n)
       .def_readonly("nblocks", &RedTable::nblocks)
+      .def("owned_blocks", [](const RedTable& t, long long lo, int chunk, int rank) {
+        // [b_lo, b_hi): the table blocks some element of which falls in owner chunk `rank` of
+        // the bucket starting at flat element lo (the blocks a mode-4 launch must cover) --
+        // the element map of reduce_body.h (vec4: 1024 / tpe elements per block, else 256 / tpe)
+        int b_lo = t.nblocks, b_hi = 0;
+        const long long c_lo = lo + (long long)rank * chunk, c_hi = c_lo + chunk;
+        for (int i = 0; i < t.n; ++i) {
+          const RedDesc& d = t.d[i];
+          const int epb = d.vec4 ? 1024 / d.tpe : 256 / d.tpe;
+          const int nb = (d.numel + epb - 1) / epb;
+          for (int k = 0; k < nb; ++k) {
+            const long long e0 = d.dst_off + (long long)k * epb, e1 = std::min<long long>(e0 + epb, d.dst_off + d.numel);
+            if (e0 < c_hi && e1 > c_lo) b_lo = std::min(b_lo, d.blk0 + k), b_hi = std::max(b_hi, d.blk0 + k + 1);
+          }
+        }
+        return b_hi > b_lo ? std::make_pair(b_lo, b_hi) : std::make_pair(0, 0);
+      })
       .def("add", [](RedTable& t, uintptr_t slab, long long stride_s, int S, int ld, int dst_off, int numel,
                       int type, int KH, int KW, int Cin, int Cout, int Cs, int tpe) {
         if (t.n >= MAX_RED) throw std::runtime_error("RedTable full");
@@ -354,6 +375,13 @@ PYBIND11_MODULE(_kernels, m) {
     launch_prologue(a, t, S(s)); check_last("prologue"); });
   m.def("gather_gx", &gather_gx);
   m.def("head_epi_max", &head_epi_max);
+  m.def("reduce_optim_end", [](uintptr_t grad, const RedTable& tc, const OptimArgs& a, uintptr_t s,
+                               const XgmiPush& xc, const RedTable& te, const XgmiPush& xe) {
+    if (!xc.on || !xe.on || xc.mode != 3 || xe.mode != 5) throw std::invalid_argument("reduce_optim_end: modes 3 + 5");
+    check_xgmi_push(xc, tc, a);
+    check_xgmi_push(xe, te, a);
+    launch_reduce_optim_end(reinterpret_cast<float*>(grad), tc, a, xc, te, xe, S(s)); check_last("reduce_optim_end"); },
+    "the end-of-backward table (mode 3) and the early range's finish part (mode 5) in one launch");
   m.def("reduce_optim", [](uintptr_t grad, const RedTable& t, const OptimArgs& a, uintptr_t s, const XgmiPush* xp) {
     if (xp && xp->on) check_xgmi_push(*xp, t, a);
     launch_reduce_optim(reinterpret_cast<float*>(grad), t, a, S(s), xp); check_last("reduce_optim"); },
@@ -383,6 +411,8 @@ PYBIND11_MODULE(_kernels, m) {
             check_xgmi_push(*xp, *rt, *ro);
             x.xp = *xp;
             if (xp->mode >= 2 && xp->nx) x.n_r = xp->nx;   // (workgroups looping over the blocks)
+            else if (xp->mode == 4) x.n_r = xp->b_hi - xp->b_lo;   // (the blocks it may own a part of)
+            if (xp->mode == 3 || xp->mode == 5) throw std::invalid_argument("dual_halo: exchange modes 1 / 2 / 4 only");
           }
         }
         const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, x, S(s));
@@ -412,7 +442,7 @@ PYBIND11_MODULE(_kernels, m) {
   py::class_<XgmiPush>(m, "XgmiPush")
       .def(py::init<>())
       RW(XgmiPush, on) RW(XgmiPush, rank) RW(XgmiPush, size) RW(XgmiPush, chunk) RW(XgmiPush, lo)
-      RW(XgmiPush, mode) RW(XgmiPush, nblk) RW(XgmiPush, nx) RW(XgmiPush, p1) RW(XgmiPush, timeout_ticks)
+      RW(XgmiPush, mode) RW(XgmiPush, nblk) RW(XgmiPush, nx) RW(XgmiPush, p1) RW(XgmiPush, fence) RW(XgmiPush, b_lo) RW(XgmiPush, b_hi) RW(XgmiPush, timeout_ticks)
       PTR(XgmiPush, ctrb) PTR(XgmiPush, err)
       .def("set_inbox", [](XgmiPush& x, int j, uintptr_t p) {
         if (j < 0 || j >= XGMI_MAX_RANKS) throw std::out_of_range("peer index");

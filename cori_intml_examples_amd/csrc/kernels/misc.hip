@@ -371,11 +371,32 @@ __global__ __launch_bounds__(256) void xgmi_early_kernel(float* __restrict__ gra
   xgmi_early_block<true>(grad, tab, a, blockIdx.x, red, xp);
 }
 
+// the end-of-backward launch of the split exchange: the conv layers' table (mode 3: reduce,
+// push, exchange, update) in workgroups [0, nc) and the early range's finish part (mode 5:
+// wait for its owners' sums -- pushed by the owner part in an earlier backward launch -- read
+// them, update) in workgroups [nc, nc + ne): one launch, no workgroup waits on its own launch
+__global__ __launch_bounds__(256) void xgmi_end_kernel(float* __restrict__ grad, const RedTable tc, const OptimArgs a,
+                                                       const XgmiPush xc, const RedTable te, const XgmiPush xe, int nc) {
+  __shared__ __attribute__((aligned(16))) float red[1024];
+  const int b = blockIdx.x;
+  if (b < nc) xgmi_early_block<true>(grad, tc, a, b, red, xc);
+  else xgmi_early_block<true>(grad, te, a, b - nc, red, xe);
+}
+
+void launch_reduce_optim_end(float* grad, const RedTable& tc, const OptimArgs& a, const XgmiPush& xc,
+                             const RedTable& te, const XgmiPush& xe, hipStream_t s) {
+  const int nc = tc.nblocks <= 0 ? 0 : (xc.nx ? xc.nx : tc.nblocks);
+  const int ne = te.nblocks <= 0 ? 0 : (xe.nx ? xe.nx : te.nblocks);
+  if (nc + ne == 0) return;
+  hipLaunchKernelGGL(xgmi_end_kernel, dim3(nc + ne), dim3(256), 0, s, grad, tc, a, xc, te, xe, nc);
+}
+
 void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, hipStream_t s,
                          const XgmiPush* xp) {
   if (tab.nblocks <= 0) return;
   if (xp && xp->on) {
-    const int grid = xp->mode >= 2 && xp->nx ? xp->nx : tab.nblocks;
+    const int grid = xp->mode >= 2 && xp->nx ? xp->nx : (xp->mode == 4 ? xp->b_hi - xp->b_lo : tab.nblocks);
+    if (grid <= 0) return;
     hipLaunchKernelGGL(xgmi_early_kernel, dim3(grid), dim3(256), 0, s, grad, tab, a, *xp);
     return;
   }

@@ -281,8 +281,9 @@ __device__ __forceinline__ void reduce_optim_block(float* __restrict__ grad, con
 
 // ---------------------------------------------------------------- xGMI early-bucket exchange
 // (XgmiPush, args.h).  The peer buffers are uncached device memory: the protocol is xgmi.hip's
-// (payload stores drained before a relaxed system-scope flag store; bounded relaxed polls; the
-// payload read with sc1 loads that bypass this CU's L1) -- see that file's header.
+// (payload stores drained, then -- fence 1, the default -- a system-scope release before the
+// relaxed system-scope flag store; bounded relaxed polls followed by a system-scope acquire;
+// the payload read with sc1 loads) -- see that file's header.
 __device__ __forceinline__ unsigned xs_load(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -308,6 +309,12 @@ __device__ __forceinline__ float4 xs_local(const float* p, int n) {
 __device__ __forceinline__ void xs_put(float* p, const float4& v, int n) {
   if (n == 4) *reinterpret_cast<float4*>(p) = v;
   else *p = v.x;
+}
+// system-scope release before a flag store (XgmiPush::fence 1): the payload stores before it
+// are visible to every agent before the flag is (the drain before it already completed them)
+__device__ __forceinline__ void xs_release() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 __device__ __forceinline__ void xs_drain_sync() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -342,7 +349,8 @@ __device__ __forceinline__ bool xs_wait(const XgmiPush& x, const unsigned* flags
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (keeps the sc1 loads below the poll)
+    if (x.fence == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");        // system-scope acquire
+    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (keeps the sc1 loads below the poll)
   }
   __syncthreads();
   return *s_ok != 0;
@@ -360,16 +368,28 @@ __device__ __forceinline__ void reduce_push_block(float* __restrict__ grad, cons
   const unsigned seq = xp.ctrb[blk] + 1u;
   xs_drain_sync();
   const int t = threadIdx.x;
-  if (t < xp.size && t != xp.rank) xs_store(xp.bflag1[t] + (size_t)blk * xp.size + xp.rank, seq);
+  if (t < xp.size && t != xp.rank) {
+    if (xp.fence == 1) xs_release();
+    xs_store(xp.bflag1[t] + (size_t)blk * xp.size + xp.rank, seq);
+  }
 }
 
 // mode 2: finish the all-reduce of table block `blk` (pushed by mode 1 of an earlier launch on
 // every rank) and apply its Keras update.  Element ownership and summation order are the fused
 // all-reduce kernel's (owner chunks of x.chunk bucket elements; rows summed in rank order, the
 // owner's own row from grad), so the sums are those the end-of-step kernel would produce.
+// parts (bit mask): 1 = the OWNER part (wait for every sender's push flag, sum the rows, write
+// the own elements' sums to grad, push them into every peer's outbox, raise bflag2); 2 = the
+// FINISH part (wait for the block's other owners, read their sums, apply the update, advance
+// the block's sequence counter).  Mode 2 / 3 run both in one launch; mode 4 runs the owner
+// part in a backward launch and mode 5 the finish part in the end-of-backward launch, so no
+// workgroup ever waits on a flag raised in its own launch.  Carried state (mode 3, one block
+// per workgroup): `pre` -- the optimizer state loaded before the slab reduction -- and `gin`
+// -- this thread's reduced partial, so the owner sum does not re-read it from memory.
 template <int KIND>
 __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a, int blk,
-                                  float* red, const XgmiPush& x) {
+                                  float* red, const XgmiPush& x, int parts = 3, const OptState4* pre4 = nullptr,
+                                  const OptState1* pre1 = nullptr, const float4* gin = nullptr) {
   const RedDesc& d = tab.d[red_desc(tab, blk)];
   const int P = x.size, me = x.rank, t = threadIdx.x, C = x.chunk;
   const unsigned seq = x.ctrb[blk] + 1u;
@@ -386,18 +406,24 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
     b_hi = min(b_lo + E, d.dst_off + d.numel);
     if (t < E && b_lo + t < b_hi) e = b_lo + t, n = 1;
   }
+  const int j0 = (int)((b_lo - x.lo) / C), j1 = (int)((b_hi - 1 - x.lo) / C);
+  const bool owner = me >= j0 && me <= j1;
+  if (parts == 1 && (P == 1 || !owner)) return;   // (mode 4: nothing of this block is mine to sum)
   // (the state the update needs is loaded now: its round trip overlaps the waits)
   OptState4 st4{};
   OptState1 st1{};
-  if (n == 4) st4 = load_state4(a, e);
-  else if (n == 1) st1 = load_state1(a, e);
-  const int j0 = (int)((b_lo - x.lo) / C), j1 = (int)((b_hi - 1 - x.lo) / C);
+  if (parts & 2) {
+    if (pre4) st4 = *pre4;
+    else if (pre1) st1 = *pre1;
+    else if (n == 4) st4 = load_state4(a, e);
+    else if (n == 1) st1 = load_state1(a, e);
+  }
   const long long ie = (long long)e - x.lo;     // bucket index
   const int own = n ? (int)(ie / C) : -1;
   float4 g = {0.f, 0.f, 0.f, 0.f};
   if (P == 1) {                                 // (no peers: the reduced gradient is final)
-    if (n) g = xs_local(grad + e, n);
-  } else if (me >= j0 && me <= j1) {
+    if (n) g = gin ? *gin : xs_local(grad + e, n);
+  } else if ((parts & 1) && owner) {
     // the owner part: every sender's row of the block is in my inbox
     if (!xs_wait(x, x.bflag1[me] + (size_t)blk * P, ~(1u << me), seq, 4, s_ok)) return;
     if (own == me) {
@@ -405,7 +431,7 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
       float4 v[XGMI_MAX_RANKS];
 #pragma unroll
       for (int q = 0; q < XGMI_MAX_RANKS; ++q)
-        if (q < P) v[q] = q == me ? xs_local(grad + e, n) : xs_peer(x.inbox[me], (size_t)q * C + k, n);
+        if (q < P) v[q] = q == me ? (gin ? *gin : xs_local(grad + e, n)) : xs_peer(x.inbox[me], (size_t)q * C + k, n);
       g = v[0];
 #pragma unroll
       for (int q = 1; q < XGMI_MAX_RANKS; ++q)
@@ -416,8 +442,14 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
         if (j < P && j != me) xs_put(x.outbox[j] + ie, g, n);
     }
     xs_drain_sync();
-    if (t < P && t != me) xs_store(x.bflag2[t] + (size_t)blk * P + me, seq);
+    if (t < P && t != me) {
+      if (x.fence == 1) xs_release();
+      xs_store(x.bflag2[t] + (size_t)blk * P + me, seq);
+    }
+  } else if (n && own == me) {
+    g = xs_local(grad + e, n);                  // (mode 5: my own sums, written by the owner part)
   }
+  if (!(parts & 2)) return;
   // the other owners' sums of this block's elements are in my outbox
   unsigned need = 0;
   for (int j = j0; j <= j1 && P > 1; ++j)
@@ -435,11 +467,61 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
   if (t == 0) x.ctrb[blk] = seq;
 }
 
+// mode 3 with one block per workgroup: the slab reduction, the producer push and the exchange
+// of ONE block with the optimizer state loaded before the slab loads and the reduced partial
+// kept in registers for the owner sum (no memory round trip between the phases)
+template <int KIND>
+__device__ __forceinline__ void xchg_fused_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
+                                                 int blk, float* red, const XgmiPush& x) {
+  const RedDesc& dsc = tab.d[red_desc(tab, blk)];
+  const int t = threadIdx.x;
+  float4 g4 = {0.f, 0.f, 0.f, 0.f};
+  if (dsc.vec4) {
+    OptState4 st{};
+    const int G = 256 / dsc.tpe, le = ((blk - dsc.blk0) * G + t % G) * 4;
+    if (t < G && le < dsc.numel) st = load_state4(a, dsc.dst_off + le);
+    int e;
+    const bool mine = slab_reduce_vec4(dsc, blk, red, e, g4);
+    if (mine) *reinterpret_cast<float4*>(grad + e) = g4;
+    if (mine && x.size > 1) xpush4(x, e, g4);
+    if (x.size > 1) {
+      xs_drain_sync();
+      if (t < x.size && t != x.rank) {
+        if (x.fence == 1) xs_release();
+        xs_store(x.bflag1[t] + (size_t)blk * x.size + x.rank, x.ctrb[blk] + 1u);
+      }
+    }
+    __syncthreads();   // (red is reused)
+    xchg_update_block<KIND>(grad, tab, a, blk, red, x, 3, &st, nullptr, &g4);
+  } else {
+    OptState1 st{};
+    const int E = 256 / dsc.tpe, le = (blk - dsc.blk0) * E + t;
+    if (t < E && le < dsc.numel) st = load_state1(a, dsc.dst_off + le);
+    int e;
+    float g;
+    const bool mine = slab_reduce_elem(tab, blk, red, e, g);
+    if (mine) grad[e] = g;
+    if (mine && x.size > 1) xpush1(x, e, g);
+    if (x.size > 1) {
+      xs_drain_sync();
+      if (t < x.size && t != x.rank) {
+        if (x.fence == 1) xs_release();
+        xs_store(x.bflag1[t] + (size_t)blk * x.size + x.rank, x.ctrb[blk] + 1u);
+      }
+    }
+    __syncthreads();
+    g4.x = g;
+    xchg_update_block<KIND>(grad, tab, a, blk, red, x, 3, nullptr, &st, &g4);
+  }
+}
+
 // workgroup r of a data-parallel table launch: mode 1 (reduce + push) one table block each;
 // mode 2 (exchange + update) and mode 3 (both, one launch: the end-of-backward bucket) one
 // block each, or x.nx workgroups looping over the blocks in order (ranks sharing a GPU; mode 3
-// then pushes all of its blocks before its first wait).  M3: mode 3 compiled in -- the
-// standalone launch only: in the dual conv launch (modes 1 / 2) its extra code made the
+// then pushes all of its blocks before its first wait); mode 4 / 5: the owner / finish part
+// of mode 2 (xchg_update_block), block b_lo + r (mode 4: blocks [b_lo, b_hi) of the table,
+// those no part of which this rank owns exit at once).  M3: mode 3 compiled in -- the
+// standalone launch only: in the dual conv launch (modes 1 / 2 / 4) its extra code made the
 // compiler copy the whole by-value DualExtra argument to scratch (1.7 KB per lane)
 template <bool M3>
 __device__ __forceinline__ void xgmi_early_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
@@ -452,7 +534,9 @@ __device__ __forceinline__ void xgmi_early_block(float* __restrict__ grad, const
     if (threadIdx.x == 0) xs_set_err(x.err, 3);
     return;
   }
-  const int step = x.nx ? x.nx : x.nblk;
+  const int step = x.nx ? x.nx : (x.mode == 4 ? x.b_hi - x.b_lo : x.nblk);
+  const int b0 = x.mode == 4 ? x.b_lo : 0, b1 = x.mode == 4 ? x.b_hi : x.nblk;
+  const int parts = x.mode == 4 ? 1 : (x.mode == 5 ? 2 : 3);
   if constexpr (M3) {
   if (x.mode == 3 && x.size == 1 && !x.p1) {   // no peers: the single-GPU reduction + update
     for (int b = r; b < x.nblk; b += step) {
@@ -467,6 +551,16 @@ __device__ __forceinline__ void xgmi_early_block(float* __restrict__ grad, const
     }
     return;
   }
+  if (x.mode == 3 && !x.nx) {                  // one block per workgroup: fused phases
+    switch (a.kind) {
+      case OPT_ADAM: xchg_fused_block<OPT_ADAM>(grad, tab, a, r, red, x); break;
+      case OPT_NADAM: xchg_fused_block<OPT_NADAM>(grad, tab, a, r, red, x); break;
+      case OPT_ADADELTA: xchg_fused_block<OPT_ADADELTA>(grad, tab, a, r, red, x); break;
+      case OPT_RMSPROP: xchg_fused_block<OPT_RMSPROP>(grad, tab, a, r, red, x); break;
+      default: xchg_fused_block<OPT_SGD>(grad, tab, a, r, red, x); break;
+    }
+    return;
+  }
   if (x.mode == 3) {
     for (int b = r; b < x.nblk; b += step) {
       reduce_push_block(grad, tab, a, b, red, x);
@@ -475,13 +569,13 @@ __device__ __forceinline__ void xgmi_early_block(float* __restrict__ grad, const
     if (x.size == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   }
-  for (int b = r; b < x.nblk; b += step) {
+  for (int b = b0 + r; b < b1; b += step) {
     switch (a.kind) {
-      case OPT_ADAM: xchg_update_block<OPT_ADAM>(grad, tab, a, b, red, x); break;
-      case OPT_NADAM: xchg_update_block<OPT_NADAM>(grad, tab, a, b, red, x); break;
-      case OPT_ADADELTA: xchg_update_block<OPT_ADADELTA>(grad, tab, a, b, red, x); break;
-      case OPT_RMSPROP: xchg_update_block<OPT_RMSPROP>(grad, tab, a, b, red, x); break;
-      default: xchg_update_block<OPT_SGD>(grad, tab, a, b, red, x); break;
+      case OPT_ADAM: xchg_update_block<OPT_ADAM>(grad, tab, a, b, red, x, parts); break;
+      case OPT_NADAM: xchg_update_block<OPT_NADAM>(grad, tab, a, b, red, x, parts); break;
+      case OPT_ADADELTA: xchg_update_block<OPT_ADADELTA>(grad, tab, a, b, red, x, parts); break;
+      case OPT_RMSPROP: xchg_update_block<OPT_RMSPROP>(grad, tab, a, b, red, x, parts); break;
+      default: xchg_update_block<OPT_SGD>(grad, tab, a, b, red, x, parts); break;
     }
     __syncthreads();   // (the next block reuses red)
   }

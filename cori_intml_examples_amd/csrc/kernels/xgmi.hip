@@ -11,12 +11,14 @@
 //             relaxed system-scope flag store (the drained stores are complete: nothing is left
 //             in any cache to write back -- the write-through publish of Guideline 16 R1);
 //   consumer: relaxed system-scope poll (bounded) -> acquire -> barrier -> loads.
-// a.fence selects the fences around the flags: 3 (default) = none, and every load of a peer's
-// payload (inbox / outbox) is an sc1 buffer load that bypasses this CU's L1 (Guideline 16: a
-// hand-off stored write-through and drained, read with sc1 loads, needs no acquire); 2 = an
-// agent-scope acquire (drops this CU's L1 lines of the reused inbox / outbox addresses:
-// ~4 us per phase-wait here); 1 = system-scope release + acquire (the original form: the
-// release writes back the XCD's whole L2, the acquire invalidates it); 0 = none, plain loads.
+// a.fence selects the fences around the flags: 1 (default) = system-scope release before every
+// flag store + system-scope acquire after every poll -- the HIP memory model's hand-off between
+// agents (the release writes back the XCD's L2, the acquire invalidates it); 3 (opt-in,
+// INTML_TUNE=xgmi_fence=3) = none, and every load of a peer's payload (inbox / outbox) is an sc1
+// buffer load (Guideline 16: a hand-off stored to uncached memory and drained, read with sc1
+// loads, needs no fence -- correct for MTYPE UC memory on this ISA, but outside the language
+// memory model, so it is not the default until a multi-GPU run shows parity); 2 = an
+// agent-scope acquire; 0 = none, plain loads.
 #include <cstring>
 #include <stdexcept>
 #include <string>

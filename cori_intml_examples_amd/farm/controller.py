@@ -54,6 +54,19 @@ class _EngineRec:
         self.stats: Dict[str, Any] = {}     # last resource telemetry from the engine
 
 
+def _remap_gpu(idx: str) -> str:
+    """The physical device behind logical GPU ``idx``: ``INTML_FARM_GPU_REMAP`` ("1:0,2:0" or
+    "*:0") remaps indices at the very last step, the engine's HIP_VISIBLE_DEVICES -- the
+    one-GPU rehearsal of a one-engine-per-GPU farm (every other decision, the engines' DP
+    environment included, sees distinct GPUs).  Unset: the identity."""
+    spec = os.environ.get("INTML_FARM_GPU_REMAP", "")
+    for item in filter(None, (x.strip() for x in spec.split(","))):
+        src, _, dst = item.partition(":")
+        if dst and (src == "*" or src == idx):
+            return dst
+    return idx
+
+
 class Controller:
     def __init__(self, cluster_id: str, n_engines: int, gpus: Optional[List[str]] = None,
                  engine_env: Optional[Dict[str, str]] = None, abort_grace: float = 10.0,
@@ -83,7 +96,7 @@ class Controller:
         env = dict(os.environ)
         env.update(self.engine_env)
         if self.gpus is not None:
-            env["HIP_VISIBLE_DEVICES"] = str(self.gpus[eid % len(self.gpus)])
+            env["HIP_VISIBLE_DEVICES"] = _remap_gpu(str(self.gpus[eid % len(self.gpus)]))
         # DP rank environment: %%px + hvd.init() turns the engines into one RCCL job
         env.update({"RANK": str(eid), "WORLD_SIZE": str(self.n), "LOCAL_RANK": "0",
                     "LOCAL_WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(self.dp_port),

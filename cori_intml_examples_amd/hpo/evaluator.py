@@ -15,8 +15,11 @@ that names one GPU more than once runs that many ranks on it (oversubscription: 
 box can still run a 2-rank nested evaluation); RCCL needs distinct devices per rank, so
 such a slot's ranks select the RCCL-free xGMI data plane on their own (``dist.init``: more
 local ranks than visible GPUs) -- the same fused all-reduce + optimizer kernel over
-IPC-mapped peer memory that a multi-GPU job uses, captured into the step graph.  ``slots_per_gpu`` > 1 repeats every slot that many times
-(several small evaluations share a GPU concurrently, as the farm's engines-per-GPU do).
+IPC-mapped peer memory that a multi-GPU job uses, captured into the step graph.
+``slots_per_gpu`` > 1 repeats every slot that many times (several small evaluations share a
+GPU concurrently, as the farm's engines-per-GPU do); multi-rank evaluations on a GPU shared by
+concurrent slots use the gloo data plane (``_env_for``: the xGMI plane's spinning workgroups
+are bounded per job, not across jobs).
 
 An evaluation whose command fails or prints no ``FoM:`` line scores ``inf`` (worst);
 ``retries`` re-runs it first.  Each run's stdout/stderr goes to ``log_dir`` if given.
@@ -35,6 +38,8 @@ import threading
 import time
 from typing import Any, Dict, List, Optional, Sequence
 
+# the gradient data plane an evaluation's training ran on (train_rpv prints History.data_plane)
+_PLANE = re.compile(r"gradient reducer ([^\n]+)")
 _FOM = re.compile(r"FoM:\s*([-+]?(?:\d+\.?\d*(?:[eE][-+]?\d+)?|\.\d+(?:[eE][-+]?\d+)?|inf|nan))")
 
 
@@ -138,6 +143,14 @@ class Evaluator:
         if log_dir:
             os.makedirs(log_dir, exist_ok=True)
 
+    def shared_across_slots(self, slot) -> bool:
+        """True if a GPU of ``slot`` also belongs to another slot (evaluations that run
+        concurrently on one GPU)."""
+        if slot is None:
+            return False
+        mine = set(slot)
+        return sum(1 for sl in self.slots if sl is not None and mine & set(sl)) > 1
+
     @property
     def num_slots(self) -> int:
         return len(self.slots)
@@ -175,7 +188,14 @@ class Evaluator:
             uniq = list(dict.fromkeys(slot))
             env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in uniq)
             # (ranks sharing a GPU -- LOCAL_RANK % visible devices -- take the RCCL-free xGMI
-            # plane: dist.init sees more local ranks than devices)
+            # plane: dist.init sees more local ranks than devices.)  A GPU that several
+            # CONCURRENT evaluations share (slots_per_gpu > 1, or overlapping slots) is
+            # different: each job caps its spinning all-reduce workgroups from its own ranks
+            # only, so jobs could starve each other's launches of CUs -- their
+            # multi-rank evaluations keep the gloo data plane, which does not spin on the GPU
+            if self.per_eval > 1 and self.shared_across_slots(slot):
+                env["INTML_COMM"] = "torch"
+                env["INTML_DP_BACKEND"] = "gloo"
         else:
             env.setdefault("INTML_DEVICE", "cpu")
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -195,8 +215,10 @@ class Evaluator:
                 out = self._rank_output(tmp, 0) + out
                 shutil.rmtree(tmp, ignore_errors=True)
             fom = parse_fom(out) if rc == 0 else None
+            plane = _PLANE.search(out)
             rec.update(cmd=cmd, rc=rc, seconds=time.time() - t0, attempt=attempt,
-                       fom=float("inf") if fom is None else fom, ok=fom is not None)
+                       fom=float("inf") if fom is None else fom, ok=fom is not None,
+                       data_plane=plane.group(1).strip() if plane else None)
             if self.log_dir:
                 with self._lock:
                     self._count += 1

@@ -1002,7 +1002,7 @@ class BatchPlan(GeometryMixin):
         reducer = ex.reducer
         dp_early = []
         self.early_push, self.pushed, self.early_xchg, self.exchanged = {}, None, {}, False
-        self.bucket_xchg, self.xchg_end = {}, None
+        self.bucket_xchg, self.xchg_end, self.xchg_fin = {}, None, None
         if reducer is not None:
             bucket_groups = reducer.configure(groups)
             # one bucket at the end of the backward (the adaptive plan for gradients <= 16 MB):
@@ -1026,6 +1026,9 @@ class BatchPlan(GeometryMixin):
                 # applies its update in extra workgroups of its own, so the fused kernel after
                 # the backward is left with the conv layers only
                 if tune("xgmi_push", True) and not solo:
+                    # every early table would start at block-flag slot 0 (fbase) and the pushed /
+                    # exchanged range is ONE span: _early_groups caps them at one dual launch
+                    assert len(self.early_red) <= 1, "exchange: one early table per step (flag slots, pushed range)"
                     for nm, (tab_, (elo, ehi), go) in self.early_red.items():
                         if not go:
                             continue
@@ -1034,6 +1037,22 @@ class BatchPlan(GeometryMixin):
                         at_end = tune("xchg_at", "dual") == "end"
                         nxt = (("end" if at_end else self._xchg_launch(nm, elo, ehi))
                                if tune("xgmi_xchg", True) else None)
+                        # split exchange (default): the owner half (wait for the senders, sum,
+                        # push the sums back: mode 4) in extra workgroups of the next dual launch,
+                        # covering only the table blocks this rank owns part of (none at one
+                        # rank), and the finish half (wait for the other owners, update: mode 5)
+                        # beside the end-of-backward table in ONE launch -- every wait is on a
+                        # flag raised in an EARLIER launch, and no conv-sized workgroup holds a
+                        # CU slot for the update (xchg_split=0: both halves in the dual launch)
+                        if nxt and not at_end and tune("xchg_split", True):
+                            trip = reducer.exchange_args(elo, ehi, tab_.nblocks, table=tab_)
+                            if trip is not None:
+                                self.early_push[nm] = trip[0]
+                                if trip[1].b_hi > trip[1].b_lo:
+                                    self.early_xchg[nxt] = (tab_, trip[1])
+                                self.xchg_fin = (tab_, trip[2])
+                                self.pushed, self.exchanged = (elo, ehi), True
+                                continue
                         pair = reducer.exchange_args(elo, ehi, tab_.nblocks) if nxt else None
                         if pair is not None:
                             self.early_push[nm] = pair[0]
@@ -1104,8 +1123,10 @@ class BatchPlan(GeometryMixin):
             tab_n = sum(self.red_groups[i][1] - self.red_groups[i][0]
                         for i in bucket_groups[xk] if i not in dp_early)
             if btab.nblocks > 0 and early_n + tab_n == rhi - rlo:
-                fb = sum(t.nblocks for t in [e[0] for e in self.early_xchg.values()]
-                         + ([self.xchg_end[0]] if self.xchg_end else []))
+                # (the early table's flag slots [0, its nblocks) -- one early table, asserted above)
+                fb = sum(t.nblocks for t in {id(t): t for t in [e[0] for e in self.early_xchg.values()]
+                                             + ([self.xchg_end[0]] if self.xchg_end else [])
+                                             + ([self.xchg_fin[0]] if self.xchg_fin else [])}.values())
                 x3 = reducer.exchange_args(blo, bhi, btab.nblocks, fbase=fb, fused=True)
                 if x3 is not None:
                     self.bucket_xchg[xk] = x3
@@ -1129,6 +1150,13 @@ class BatchPlan(GeometryMixin):
             extra.append(("xchg_early_b%d", lambda k: None if (k != xk or self.xchg_end is None) else
                           (lambda s: K.reduce_optim(ex.store.grad.data_ptr(), self.xchg_end[0],
                                                     ex._optim_args(False, defer_pack=True), s, self.xchg_end[1])),
+                          "main"))
+            # (the split exchange's finish half rides in the end-of-backward table launch; a launch
+            # of its own only when that table is not exchanged)
+            extra.append(("xchg_fin_b%d", lambda k: None if (k != xk or self.xchg_fin is None
+                                                            or k in self.bucket_xchg) else
+                          (lambda s: K.reduce_optim(ex.store.grad.data_ptr(), self.xchg_fin[0],
+                                                    ex._optim_args(False, defer_pack=True), s, self.xchg_fin[1])),
                           "main"))
             extra.append(("xgmi_allreduce_optim_b%d", lambda k: None if (k != xk or k in self.bucket_xchg) else
                           (lambda s: reducer.launch_fused(ex.store.grad, ex._optim_args(False, defer_pack=True), s,
@@ -1247,7 +1275,11 @@ class BatchPlan(GeometryMixin):
         lo, hi, tab = self.bucket_tables[k]
         ex = self.ex
         xp = (getattr(self, "bucket_xchg", None) or {}).get(k)
-        if xp is not None:       # reduction + all-reduce (exchange) + Keras update in one launch
+        fin = getattr(self, "xchg_fin", None)
+        if xp is not None and fin is not None:   # + the early range's exchange finish (mode 5)
+            ex.K.reduce_optim_end(ex.store.grad.data_ptr(), tab, ex._optim_args(False, defer_pack=True), s, xp,
+                                  fin[0], fin[1])
+        elif xp is not None:     # reduction + all-reduce (exchange) + Keras update in one launch
             ex.K.reduce_optim(ex.store.grad.data_ptr(), tab, ex._optim_args(False, defer_pack=True), s, xp)
         elif self.optim_fused:     # gradient reduction + Keras update in one launch (re-pack deferred)
             ex.K.reduce_optim(ex.store.grad.data_ptr(), tab, ex._optim_args(False, defer_pack=True), s)

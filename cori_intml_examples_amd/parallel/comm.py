@@ -214,7 +214,8 @@ def establish(rank: int, size: int, device: torch.device, timeout_s: float = 600
       2. every rank builds its communicator in a worker thread with a deadline
          (``INTML_RCCL_INIT_TIMEOUT``, default 120 s): a rank that never joins (it failed
          before ``ncclCommInitRank``) leaves its peers blocked inside RCCL, but their main
-         threads give up waiting and go on to the vote (the blocked thread is abandoned);
+         threads give up waiting and go on to the vote (the blocked thread goes to a reaper
+         that aborts + closes the communicator if it still comes up: ``_reap_late_init``);
       3. the numeric self-test (``NativeComm.self_test``: eager + graph-captured, closed-form);
       4. ONE all_gather of every rank's verdict; any failure anywhere -> every rank aborts its
          communicator and falls back.
@@ -258,6 +259,7 @@ def establish(rank: int, size: int, device: torch.device, timeout_s: float = 600
         th.join(init_timeout_s)
         if th.is_alive():
             why = "communicator not up within %.0f s (a peer never joined)" % init_timeout_s
+            _reap_late_init(th, res)
         elif "err" in res:
             why = res["err"]
         else:
@@ -279,6 +281,38 @@ def establish(rank: int, size: int, device: torch.device, timeout_s: float = 600
             comm.close()
         return None, bad
     return comm, None
+
+
+# communicator-init threads abandoned at their deadline, and what became of them: "pending",
+# "failed: ..." or "closed" (a late communicator is aborted + closed by the reaper, never used)
+abandoned_inits: list = []
+
+
+def _reap_late_init(th, res: dict) -> None:
+    """An init thread that missed its deadline may still complete inside ncclCommInitRank
+    later (its peers joined late).  By then the job has voted onto the RCCL-free plane, so a
+    late communicator must not live on with its watchdog: a daemon reaper joins the thread and
+    aborts + closes whatever it produced.  The outcome is recorded in ``abandoned_inits``."""
+    import threading
+    rec = {"thread": th.name, "state": "pending"}
+    abandoned_inits.append(rec)
+
+    def reap():
+        th.join()
+        c = res.get("comm")
+        if c is None:
+            rec["state"] = "failed: %s" % res.get("err", "no communicator")
+            return
+        try:
+            c.abort("communicator came up after the init deadline; the job runs without RCCL")
+        except Exception:   # noqa: BLE001
+            pass
+        try:
+            c.close()
+        finally:
+            rec["state"] = "closed"
+
+    threading.Thread(target=reap, name="rccl-init-reaper", daemon=True).start()
 
 
 def comm_mode(use_gpu: bool, backend: Optional[str], local_size: Optional[int] = None,

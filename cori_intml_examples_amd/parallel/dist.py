@@ -29,6 +29,11 @@ from . import state as S
 from ..utils.env import tune
 
 
+class DataParallelDivergence(RuntimeError):
+    """The ranks of a data-parallel job hold different weights (fit()'s per-epoch digest check,
+    train.loop.dp_consistency_check): raised on every rank at the same epoch end."""
+
+
 # ------------------------------------------------------------------------------ bootstrap
 def init(shard_data: Optional[bool] = None, backend: Optional[str] = None,
          bucket_bytes: Optional[int] = None) -> S.DPState:
@@ -418,21 +423,93 @@ def device_key(device) -> str:
     return socket.gethostname() + "/" + ident
 
 
+# ------------------------------------------------------------------------------ plane verdicts
+# A measured data-plane choice, persisted: bench.py's probe (probe_data_planes) times every
+# plane on the job itself, checks the ranks' weights bit-identical after each, and rank 0
+# records the winner here, keyed by (host, world size, gradient size class).  auto_plane reads
+# it: without a verdict for the job's key, "auto" means RCCL (nothing but a
+# measurement on the real fabric admits the xGMI plane).
+VERDICT_PLANES = ("xgmi", "hybrid", "rccl")
+
+
+def verdict_path() -> str:
+    return os.environ.get("INTML_PLANE_VERDICTS") or os.path.join(
+        os.path.expanduser("~"), ".cache", "cori_intml_examples_amd", "plane_verdicts.json")
+
+
+def verdict_key(world: int, grad_bytes: int, host: Optional[str] = None) -> str:
+    """(host, world size, gradient size class): the class is the power of two at or above
+    the gradient's bytes, so a verdict measured on one model applies to models of the same
+    order of gradient size (the quantity the planes' relative cost depends on)."""
+    import socket
+    cls = 1 << max(0, int(grad_bytes) - 1).bit_length()
+    return "%s/P%d/%dB" % (host or socket.gethostname(), int(world), cls)
+
+
+def plane_family(plane: str) -> str:
+    """A probe candidate's plane family as auto_plane uses it ("xgmi_end" -> "xgmi",
+    "rccl_single" / "rccl_forked" -> "rccl")."""
+    return "xgmi" if plane.startswith("xgmi") else ("hybrid" if plane == "hybrid" else "rccl")
+
+
+def _read_verdicts(path: str) -> dict:
+    import json
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d if isinstance(d, dict) else {}
+    except (OSError, ValueError):
+        return {}
+
+
+def record_verdict(world: int, grad_bytes: int, plane: str, probe: Optional[dict] = None) -> Optional[str]:
+    """Persist a measured plane choice (rank 0 of the measuring job).  Atomic replace; returns
+    the file written, or None if it could not be (a read-only home: auto stays on RCCL)."""
+    import json
+    import tempfile
+    import time
+    path = verdict_path()
+    fam = plane_family(plane)
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        d = _read_verdicts(path)
+        d[verdict_key(world, grad_bytes)] = {
+            "plane": fam, "probe_choice": plane, "grad_bytes": int(grad_bytes), "time": time.time(),
+            "probe_ms_per_step": {k: v for k, v in (probe or {}).items() if isinstance(v, (float, int))}}
+        fd, tmp = tempfile.mkstemp(dir=os.path.dirname(path), prefix=".verdicts.")
+        with os.fdopen(fd, "w") as f:
+            json.dump(d, f, indent=1, sort_keys=True)
+        os.replace(tmp, path)
+        return path
+    except OSError:
+        return None
+
+
+def lookup_verdict(world: int, grad_bytes: int) -> Optional[str]:
+    """The recorded plane family for this job's key, or None."""
+    v = _read_verdicts(verdict_path()).get(verdict_key(world, grad_bytes))
+    plane = v.get("plane") if isinstance(v, dict) else None
+    return plane if plane in VERDICT_PLANES else None
+
+
 def auto_plane(grad_bytes: Optional[int] = None) -> str:
-    """The default plane: "xgmi" when every rank has a GPU of its own on ONE node (the xGMI
-    links reach every peer; the all-reduce of the early range overlaps the conv backward) and
-    the gradient is small enough for one fused bucket (<= 16 MB, the adaptive single-bucket
-    bound: the 138 MB legacy gradient keeps RCCL buckets forked onto the comm stream, which
-    overlap the backward), else "rccl".  The xGMI plane is still only used after its collective setup and self-test --
-    the two-shot kernel and the exchange protocol, on every rank -- pass the vote; otherwise
-    the step keeps the RCCL all-reduce (NativeGradReducer._setup_xgmi)."""
+    """The default plane.  "rccl", unless a MEASURED verdict for this job's (host, world size,
+    gradient size class) says otherwise (``record_verdict``, written by bench.py's plane probe
+    after it checked every plane's ranks bit-identical).  The xGMI / hybrid verdicts apply only
+    where those planes can run: every rank a GPU of its own on ONE node and a gradient small
+    enough for one fused bucket (<= 16 MB; the 138 MB legacy gradient keeps RCCL buckets
+    forked onto the comm stream).  Even then the xGMI plane is used only after its collective
+    setup and stressed self-test pass the vote on every rank, else the step keeps RCCL
+    (NativeGradReducer._setup_xgmi).  The caller makes the choice collective (rank 0's)."""
     if grad_bytes is not None and grad_bytes > (16 << 20):
         return "rccl"
     if is_initialized():
         st = _st()
         if (st.size > 1 and st.local_size == st.size and torch.cuda.is_available()
-                and torch.cuda.device_count() >= st.local_size):
-            return "xgmi"
+                and torch.cuda.device_count() >= st.local_size and grad_bytes is not None):
+            v = lookup_verdict(st.size, grad_bytes)
+            if v is not None:
+                return v
     return "rccl"
 
 
@@ -472,6 +549,10 @@ class NativeGradReducer:
     def configure(self, groups: Sequence[Tuple[int, int]]) -> List[List[int]]:
         self.plane = (data_plane(4 * sum(hi - lo for lo, hi in groups)) if self.comm is not None
                       else "xgmi")
+        if self.comm is not None and self.size > 1 and _active():
+            # one plane for the job: rank 0's (a verdict file written between two ranks' reads
+            # must not split the job between planes)
+            self.plane = broadcast_object(self.plane, 0)
         bb = self.bucket_bytes
         if self.plane == "xgmi":
             bb = 1 << 62                    # the whole gradient is ONE fused xGMI bucket
@@ -519,9 +600,10 @@ class NativeGradReducer:
             keys = allgather(device_key(self.device))
             shared = len(set(keys)) < len(keys) or _st().local_size > max(1, torch.cuda.device_count())
             max_wg = int(tune("xgmi_shared_wg", 8)) if shared else None
-            self.xgmi = X.create(self.rank, self.size, n, self.device, allgather, max_wg=max_wg)
+            # (shared goes into create(): the admission self-test runs the exchange geometry --
+            # looping or one workgroup per block -- that training will use)
+            self.xgmi = X.create(self.rank, self.size, n, self.device, allgather, max_wg=max_wg, shared=shared)
             if self.xgmi is not None:
-                self.xgmi.shared = shared
                 self._xgmi_err_host = torch.zeros(4, dtype=torch.int32).pin_memory()
         if self.xgmi is not None:
             self.xgmi_bucket = k
@@ -546,19 +628,27 @@ class NativeGradReducer:
         blo = self._xgmi_lo(lo, hi)
         return None if blo is None else self.xgmi.push_args(blo)
 
-    def exchange_args(self, lo: int, hi: int, nblk: int, fbase: int = 0, fused: bool = False):
+    def exchange_args(self, lo: int, hi: int, nblk: int, fbase: int = 0, fused: bool = False, table=None):
         """(push, exchange) XgmiPush pair for an early range [lo, hi) whose reduction table has
         ``nblk`` blocks: the launch that reduces it pushes + flags (mode 1), a later backward
         launch finishes its all-reduce and applies its update (mode 2).  ``fused``: ONE
         XgmiPush doing both in one launch (mode 3, the end-of-backward table).  ``fbase``: the
         table's first block-flag slot.  None when the range is not in the xGMI bucket or the
-        flags cannot cover the table."""
+        flags cannot cover the table.  ``table`` (the split exchange): returns (mode 1, mode 4,
+        mode 5) -- the owner half of the exchange in the next backward launch over the table
+        blocks this rank owns part of (``table.owned_blocks``; none at size 1), the finish half
+        beside the end-of-backward table."""
         blo = self._xgmi_lo(lo, hi)
         if blo is None:
             return None
         if fused:
             return self.xgmi.push_args(blo, mode=3, nblk=nblk, fbase=fbase)
         x1 = self.xgmi.push_args(blo, mode=1, nblk=nblk, fbase=fbase)
+        if table is not None:
+            own = tuple(table.owned_blocks(blo, self.xgmi.chunk, self.rank)) if self.size > 1 else (0, 0)
+            x4 = self.xgmi.push_args(blo, mode=4, nblk=nblk, fbase=fbase, blocks=own)
+            x5 = self.xgmi.push_args(blo, mode=5, nblk=nblk, fbase=fbase)
+            return None if x1 is None or x4 is None or x5 is None else (x1, x4, x5)
         x2 = self.xgmi.push_args(blo, mode=2, nblk=nblk, fbase=fbase)
         return None if x1 is None or x2 is None else (x1, x2)
 

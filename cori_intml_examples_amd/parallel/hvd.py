@@ -1,6 +1,6 @@
 """Drop-in for ``import horovod.keras as hvd`` (``train_rpv.py:10``, ``rpv.py:64,82``)."""
 from . import callbacks
-from .dist import (Compression, DistributedOptimizer, allgather, allreduce, barrier, broadcast,
+from .dist import (Compression, DataParallelDivergence, DistributedOptimizer, allgather, allreduce, barrier, broadcast,
                    broadcast_model_state, broadcast_object, init, is_initialized, local_rank,
                    local_size, rank, shutdown, size)
 
@@ -12,4 +12,5 @@ def broadcast_global_variables(root_rank=0, model=None):
 
 __all__ = ["init", "shutdown", "rank", "size", "local_rank", "local_size", "allreduce",
            "allgather", "broadcast", "broadcast_object", "barrier", "DistributedOptimizer",
-           "Compression", "callbacks", "broadcast_global_variables", "is_initialized"]
+           "Compression", "callbacks", "broadcast_global_variables", "is_initialized",
+           "DataParallelDivergence"]

@@ -124,9 +124,10 @@ class XgmiAllreduce:
         self.timeout_s = float(timeout_s or default_timeout_s())
         a.timeout_ticks = int(self.timeout_s * _TICKS_PER_S)
         a.ctr, a.err = self.ctr.data_ptr(), self.err.data_ptr()
-        # 3: no fences, sc1 payload loads; 2: agent-scope acquire; 1: system-scope release +
-        # acquire; 0: none (xgmi.hip header; uncached payload never needs a release)
-        a.fence = int(tune("xgmi_fence", 3))
+        # 1 (default): system-scope release + acquire around every flag (the HIP memory model;
+        # the fence-free form 3 -- sc1 payload loads only -- stays opt-in until a
+        # multi-GPU run shows parity); 2: agent-scope acquire; 0: none (xgmi.hip header)
+        a.fence = int(tune("xgmi_fence", 1))
         if err is None:
             for j, b in enumerate(bases):
                 a.set_peer(j, b + self.off_in, b + self.off_out, b + self.off_f1, b + self.off_f2, b + self.off_ab)
@@ -135,7 +136,7 @@ class XgmiAllreduce:
         self.setup_error = err
 
     # ------------------------------------------------------------------ launches
-    def push_args(self, lo: int = 0, mode: int = 1, nblk: int = 0, fbase: int = 0):
+    def push_args(self, lo: int = 0, mode: int = 1, nblk: int = 0, fbase: int = 0, blocks=None):
         """XgmiPush for the kernels that finalise part of this all-reduce's bucket inside the
         backward (the early head / dense reduction).  mode 1: they store each reduced element
         straight into its owner's inbox row -- phase 1 of the all-reduce, overlapping the rest
@@ -144,7 +145,10 @@ class XgmiAllreduce:
         and send the sums back, and every rank applies the update -- the range's whole
         all-reduce + optimizer inside the backward (args.h XgmiPush); mode 3: both in one
         launch (the end-of-backward bucket's table).  ``lo``: the bucket's first flat element;
-        ``fbase``: the table's first block-flag slot (tables of one step use disjoint slots).  None past the flag capacity, or at size 1 without an exchange
+        ``fbase``: the table's first block-flag slot (tables of one step use disjoint slots);
+        mode 4 / 5 (the split exchange): the owner half of mode 2 in a backward launch over the
+        table ``blocks`` = (b_lo, b_hi) this rank owns part of, and the finish half (waits for
+        the other owners + update) in the end-of-backward launch.  None past the flag capacity, or at size 1 without an exchange
         (nothing to push; at size 1 the exchange is the range's update in the later launch --
         the same structure, no peer traffic)."""
         if not self.bases or fbase + nblk > XCHG_MAX_BLOCKS or (self.size < 2 and not nblk):
@@ -167,7 +171,12 @@ class XgmiAllreduce:
             # xchg_nx (A/B): as many looping workgroups on separate GPUs too
             x.nx = int(tune("xgmi_xchg_wg", 4)) if self.shared else int(tune("xchg_nx", 0))
             x.nx = x.nx if mode >= 2 else 0
+            if mode == 4:
+                x.b_lo, x.b_hi = blocks if blocks is not None else (0, nblk)
+                if x.nx:
+                    x.nx = min(x.nx, max(1, x.b_hi - x.b_lo))
             x.p1 = int(tune("xchg_p1", False))
+            x.fence = 3 if self.args.fence == 3 else 1    # the exchange: release/acquire or none
         return x
 
     def launch(self, grad: int, stream: int, opt=None, skip=(0, 0), exchanged: bool = False) -> None:
@@ -191,8 +200,24 @@ class XgmiAllreduce:
         if e[0]:
             raise RuntimeError(describe_error(*e))
 
-    def selftest(self) -> Optional[str]:
-        """Two launches on closed-form data (exact in fp32); None if correct on this rank."""
+    def _skew(self, it: int) -> None:
+        """A rank-dependent device-side busy delay before launch ``it`` of a stressed self-test
+        (0-40 us, different on every rank and launch): back-to-back launches then meet their
+        peers out of phase, so a flag seen before its payload -- an ordering bug -- shows up
+        as a wrong sum instead of hiding behind lockstep timing."""
+        cyc = ((it * 7 + self.rank * 13) % 5) * 20000
+        if cyc:
+            try:
+                torch.cuda._sleep(cyc)
+            except Exception:         # noqa: BLE001 -- (no delay kernel: unskewed)
+                pass
+
+    def selftest(self, stress: Optional[int] = None) -> Optional[str]:
+        """Closed-form data (exact in fp32) through the two-shot kernel and the exchange
+        protocol; None if correct on this rank.  Two synchronised launches, then ``stress``
+        (default: up to 64, bounded to 256 MB of buffers) back-to-back launches on distinct
+        buffers with rank-dependent busy delays in front of each (``_skew``), every result
+        checked after one synchronisation."""
         if self.setup_error:
             return self.setup_error
         n, P, r = self.n, self.size, self.rank
@@ -209,14 +234,37 @@ class XgmiAllreduce:
             if not torch.equal(g, want):
                 bad = int((g != want).sum())
                 return "selftest: %d of %d elements wrong" % (bad, n)
-        return self._xchg_selftest()
+        if stress is None:
+            stress = int(tune("xgmi_selftest_stress", 64))
+        k = max(0, min(int(stress), (256 << 20) // max(1, 4 * n)))
+        if k:
+            gs = []
+            for it in range(k):
+                g = pat * float(r + 1 + (it % 11))
+                self._skew(it)
+                self.launch(g.data_ptr(), stream)
+                gs.append(g)
+            torch.cuda.synchronize(self.device)
+            if int(self.err[0].item()):
+                return "stressed selftest: " + describe_error(*self.err.tolist())
+            for it, g in enumerate(gs):
+                want = pat * float(sum(q + 1 + (it % 11) for q in range(P)))
+                if not torch.equal(g, want):
+                    return "stressed selftest: launch %d of %d: %d of %d elements wrong" % (
+                        it, k, int((g != want).sum()), n)
+            del gs
+        return self._xchg_selftest(stress=min(k, 16))
 
-    def _xchg_selftest(self) -> Optional[str]:
+    def _xchg_selftest(self, stress: int = 0) -> Optional[str]:
         """The exchange protocol the training step uses (XgmiPush mode 3: per-block flags,
         owner sums pushed back through the outboxes) on a closed-form table -- a float4 and a
-        split-lane descriptor over a window straddling the first owner boundary -- twice (the
-        block sequence numbers advance); every rank must read back the exact sums.  Uses the
-        top block-flag slots, which no training table reaches."""
+        split-lane descriptor over a window straddling the first owner boundary -- as mode 3 (one
+        launch) and as the split exchange (modes 1 -> 4 -> 5, three launches), twice each (the
+        block sequence numbers advance), then ``stress`` more launches back to back alternating
+        the two, with rank-dependent delays (``_skew``); every rank must read back the exact sums.  The
+        geometry is training's (one workgroup per block on separate GPUs, looping workgroups
+        when ranks share one: ``shared``).  Uses the top block-flag slots, which no training
+        table reaches."""
         K, P, r, dev = self.K, self.size, self.rank, self.device
         lo = max(0, min(self.n, self.chunk) - 2048) // 4 * 4
         hi = min(self.n, lo + 4096) // 4 * 4
@@ -229,7 +277,7 @@ class XgmiAllreduce:
         st = torch.zeros(K.STEP_STATE_BYTES, dtype=torch.uint8, device=dev)   # lr 0: the update is a no-op
         p = torch.zeros(self.n, dtype=torch.float32, device=dev)
         ramp = lambda m: torch.remainder(torch.arange(m, device=dev, dtype=torch.float32), 7.0) * 0.25
-        for it in range(2):
+        def launch(it, split=False):
             f = float(r + 1 + it)
             sv = torch.stack([ramp(nv) * f * (s + 1) for s in range(S)])
             sb = torch.stack([ramp(max(nb, 1)) * f * (s + 1) for s in range(S)])
@@ -239,19 +287,63 @@ class XgmiAllreduce:
                 tab.add(sb.data_ptr(), max(nb, 1), S, nb, lo + nv, nb, 1, 1, 1, 1, nb, nb, tpe)   # RED_BIAS
             a = K.OptimArgs()
             a.p, a.n, a.st, a.kind = p.data_ptr(), self.n, st.data_ptr(), 0
+            g = torch.zeros(self.n, dtype=torch.float32, device=dev)
+            if split:
+                # the split exchange the training step runs: mode 1 (reduce + push, a grad-only
+                # table), mode 4 (owner half, the blocks this rank owns part of), mode 5 (finish
+                # half) -- three launches, in the flag slots below mode 3's
+                fb = XCHG_MAX_BLOCKS - 2 * tab.nblocks
+                own = tuple(tab.owned_blocks(0, self.chunk, r)) if P > 1 else (0, 0)
+                x1 = self.push_args(0, mode=1, nblk=tab.nblocks, fbase=fb)
+                x4 = self.push_args(0, mode=4, nblk=tab.nblocks, fbase=fb, blocks=own)
+                x5 = self.push_args(0, mode=5, nblk=tab.nblocks, fbase=fb)
+                if x1 is None or x4 is None or x5 is None:
+                    return None
+                a.grad_only = 1
+                if P > 1 or x1.bflag1[0]:
+                    K.reduce_optim(g.data_ptr(), tab, a, stream, x1)
+                else:
+                    K.reduce_optim(g.data_ptr(), tab, a, stream)
+                a.grad_only = 0
+                K.reduce_optim(g.data_ptr(), tab, a, stream, x4)
+                K.reduce_optim(g.data_ptr(), tab, a, stream, x5)
+                return g, (sv, sb)
             xp = self.push_args(0, mode=3, nblk=tab.nblocks, fbase=XCHG_MAX_BLOCKS - tab.nblocks)
             if xp is None:
-                return "exchange selftest: no flag slots"
-            g = torch.zeros(self.n, dtype=torch.float32, device=dev)
+                return None
             K.reduce_optim(g.data_ptr(), tab, a, stream, xp)
-            torch.cuda.synchronize(self.device)
-            if int(self.err[0].item()):
-                return "exchange selftest: " + describe_error(*self.err.tolist())
+            return g, (sv, sb)            # (the slabs stay alive until the check)
+
+        def check(g, it, what):
             k = sum(q + 1 + it for q in range(P)) * S * (S + 1) / 2
             want = torch.cat([ramp(nv), ramp(nb)[:nb]]) * k
             if not torch.equal(g[lo:lo + nv + nb], want):
                 bad = int((g[lo:lo + nv + nb] != want).sum())
-                return "exchange selftest: %d of %d elements wrong" % (bad, nv + nb)
+                return "%s: %d of %d elements wrong" % (what, bad, nv + nb)
+            return None
+
+        for it in range(4):
+            out = launch(it, split=it >= 2)
+            if out is None:
+                return "exchange selftest: no flag slots"
+            torch.cuda.synchronize(self.device)
+            if int(self.err[0].item()):
+                return "exchange selftest: " + describe_error(*self.err.tolist())
+            why = check(out[0], it, "exchange selftest")
+            if why:
+                return why
+        outs = []
+        for it in range(4, 4 + stress):
+            self._skew(it)
+            outs.append(launch(it, split=bool(it & 1)))
+        if outs:
+            torch.cuda.synchronize(self.device)
+            if int(self.err[0].item()):
+                return "stressed exchange selftest: " + describe_error(*self.err.tolist())
+            for it, out in enumerate(outs, start=4):
+                why = check(out[0], it, "stressed exchange selftest (launch %d)" % it)
+                if why:
+                    return why
         return None
 
     def close(self) -> None:
@@ -275,12 +367,16 @@ def describe_error(e: int, seq: int = 0, seen: int = 0, where: int = 0) -> str:
 
 
 def create(rank: int, size: int, n: int, device: torch.device, allgather,
-           timeout_s: Optional[float] = None, max_wg: Optional[int] = None) -> Optional[XgmiAllreduce]:
+           timeout_s: Optional[float] = None, max_wg: Optional[int] = None,
+           shared: bool = False) -> Optional[XgmiAllreduce]:
     """Build + self-test collectively; returns the object only if EVERY rank passed both
-    the setup and the self-test (same decision on every rank: the votes are gathered)."""
+    the setup and the (stressed) self-test (same decision on every rank: the votes are
+    gathered).  ``shared``: the ranks share a GPU -- set BEFORE the self-test, so it runs the
+    exchange geometry (looping workgroups) that training will use."""
     x, why = None, None
     try:
         x = XgmiAllreduce(rank, size, n, device, allgather, timeout_s=timeout_s, max_wg=max_wg)
+        x.shared = bool(shared)
         why = x.setup_error
     except Exception as e:            # noqa: BLE001
         why = "error: %s" % e

@@ -84,6 +84,12 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
     do_val = val is not None
 
     model.history = cbks.History()
+    # DP consistency guard (the reference's own multi-rank check is identical test loss on every
+    # rank, DistTrain_mnist.ipynb:526-527): a cross-rank digest of the weights at every epoch end
+    check_dp = (shard is not None or (dp is not None and dp.size > 1
+                                       and getattr(model.optimizer, "distributed", False)))
+    check_dp = check_dp and os.environ.get("INTML_DP_CHECK", "1") not in ("0", "false", "False")
+    model.history.dp_consistency = [] if check_dp else None
     progbar = cbks.ProgbarLogger() if verbose else None
     cb_list = ([progbar] if progbar else []) + list(callbacks or []) + [model.history]
     cb = cbks.CallbackList(cb_list)
@@ -162,12 +168,48 @@ def fit_loop(model, x, y, batch_size, epochs, verbose, callbacks, validation_spl
             epoch_logs["val_loss"] = vloss
             if model.metrics:
                 epoch_logs["val_acc"] = vacc
+        if check_dp:
+            # before the callbacks: a checkpoint / early-stop decision never sees diverged ranks
+            model.history.dp_consistency.append(dp_consistency_check(model, epoch))
         cb.on_epoch_end(epoch, epoch_logs)
         if model.stop_training:
             break
     cb.on_train_end()
     model.history.data_plane = data_plane_of(ex, dp)
     return model.history
+
+
+def weight_digest(model) -> list:
+    """(sum, sum |w|, sum w^2) of the flat fp32 master weights, accumulated in fp64: equal on
+    every rank iff (to fp64 rounding of identical inputs, i.e. exactly) the ranks agree."""
+    m = model.store.master[:model.store.numel].detach().double()
+    return [float(m.sum()), float(m.abs().sum()), float((m * m).sum())]
+
+
+def dp_consistency_check(model, epoch: int) -> dict:
+    """One allgather of 3 doubles per epoch: every rank's weight digest.  Raises
+    ``DataParallelDivergence`` on EVERY rank (they all see the same gathered list) if any rank
+    differs -- a data-plane ordering bug, a dropped bucket or a rank that skipped a step would
+    otherwise train on silently, diverged.  Returns the History record."""
+    from ..parallel import dist as _dist
+    d = weight_digest(model)
+    digests = _dist.allgather(d)
+    ok = all(x == digests[0] for x in digests)
+    rec = {"epoch": int(epoch), "digest": d, "identical": ok}
+    if not ok:
+        bad = [i for i, x in enumerate(digests) if x != digests[0]]
+        rec["ranks_differing"] = bad
+        model.history.dp_consistency.append(rec)
+        raise _dist.DataParallelDivergence(
+            "data-parallel ranks diverged at the end of epoch %d: weight digests of ranks %s differ "
+            "from rank 0's (%s vs %s); data plane %s" % (epoch, bad, digests[bad[0]], digests[0],
+                                                           data_plane_of(model._executor, _dp_state())))
+    return rec
+
+
+def _dp_state():
+    from ..parallel import state as dp_state
+    return dp_state.current()
 
 
 def data_plane_of(ex, dp) -> Optional[str]:

@@ -6,6 +6,7 @@ vote the whole job onto the RCCL-free plane -- no rank raises, no rank hangs:
   one_init  only rank 1's construction raises (its peers' constructions succeed)
   uid       rank 0 cannot create the unique id (the others learn it from rank 0's broadcast)
   hang      rank 1's construction never returns (INTML_RCCL_INIT_TIMEOUT bounds the wait)
+  late      rank 1's construction returns AFTER the deadline: the reaper aborts + closes it
   selftest  rank 1's numeric self-test fails (wrong sum in the captured all-reduce)
   ok        everything succeeds: the job keeps its communicator
 """
@@ -33,12 +34,15 @@ class _FakeModule:
 
 class _FakeComm:
     aborted = []
+    closed = 0
 
     def __init__(self, rank, size, device, timeout_s, uid=None):
         if SCENARIO == "all_init" or (SCENARIO == "one_init" and rank == 1):
             raise RuntimeError("ncclCommInitRank: unhandled system error (injected)")
         if SCENARIO == "hang" and rank == 1:
             time.sleep(3600)
+        if SCENARIO == "late" and rank == 1:
+            time.sleep(float(os.environ.get("INTML_RCCL_INIT_TIMEOUT", 4)) + 2.0)
         self.rank, self.size = rank, size
 
     def self_test(self, timeout_s=60.0):
@@ -50,7 +54,7 @@ class _FakeComm:
         _FakeComm.aborted.append(why)
 
     def close(self):
-        pass
+        _FakeComm.closed += 1
 
 
 def main(outdir):
@@ -61,6 +65,13 @@ def main(outdir):
     st = dist.init()
     rep = {"rank": st.rank, "size": st.size, "xgmi_only": bool(st.xgmi_only), "comm": st.comm is not None,
            "plane": st.plane, "aborted": len(_FakeComm.aborted), "init_s": time.time() - t0}
+    if SCENARIO == "late":
+        # the late communicator must be aborted + closed by the reaper once it comes up
+        deadline = time.time() + 20
+        while time.time() < deadline and any(r["state"] == "pending" for r in C.abandoned_inits):
+            time.sleep(0.1)
+        rep["abandoned"] = [r["state"] for r in C.abandoned_inits]
+        rep["aborted"], rep["closed"] = len(_FakeComm.aborted), _FakeComm.closed
     with open(os.path.join(outdir, "fb%d.json" % st.rank), "w") as f:
         json.dump(rep, f)
     if st.comm is not None:

@@ -34,6 +34,12 @@ from cori_intml_examples_amd.parallel import dist, hvd  # noqa: E402
 from cori_intml_examples_amd.utils import set_random_seed  # noqa: E402
 
 GLOBAL_B, STEPS, SPG, N = 128, 24, 8, 4096
+# DPX_SMALL=1: a small RPV-shaped model (32x32x3, conv [8,16,16], fc [32]) whose exchange tables
+# have a handful of blocks -- small enough that the separate-GPU geometry (one workgroup per
+# table block, INTML_TUNE=xgmi_xchg_wg=0) cannot fill the shared card with spinning workgroups
+SMALL = os.environ.get("DPX_SMALL", "0") == "1"
+SHAPE = (32, 32, 3) if SMALL else (64, 64, 3)
+ARCH = dict(conv_sizes=[8, 16, 16], fc_sizes=[32]) if SMALL else dict(conv_sizes=[16, 32, 64], fc_sizes=[128])
 
 
 def flat(m):
@@ -52,13 +58,13 @@ def run(opt, lr, outdir, r, P, dev):
     """One DP training of the bench model with `opt`; rank 0 also trains the single-process
     twin.  Returns this rank's report."""
     rep = {}
-    kw = dict(conv_sizes=[16, 32, 64], fc_sizes=[128], dropout=0.0, optimizer=opt, lr=lr, device="cuda:0")
+    kw = dict(dropout=0.0, optimizer=opt, lr=lr, device="cuda:0", **ARCH)
     set_random_seed(1 + r)                       # different on purpose: the broadcast must fix it
-    m = zoo.rpv_cnn((64, 64, 3), use_horovod=True, **kw)
+    m = zoo.rpv_cnn(SHAPE, use_horovod=True, **kw)
     hvd.broadcast_global_variables(0, model=m)
     w0 = m.get_weights()
     ex = m._executor
-    data = synth.synth_device("rpv", N, (64, 64, 3), 1, ex.in_Cs, 7, dev)
+    data = synth.synth_device("rpv", N, SHAPE, 1, ex.in_Cs, 7, dev)
     g = torch.Generator(device=dev).manual_seed(11)
     perm = torch.randperm(N, device=dev, generator=g)[:STEPS * GLOBAL_B]
     b = GLOBAL_B // P
@@ -88,13 +94,18 @@ def run(opt, lr, outdir, r, P, dev):
     rep["pushed"] = list(getattr(plan, "pushed", None) or [])
     rep["xchg_launches"] = sorted((getattr(plan, "early_xchg", None) or {}).keys())
     rep["exchanged"] = bool(getattr(plan, "exchanged", False))
+    rep["xchg_fin"] = getattr(plan, "xchg_fin", None) is not None     # split exchange: finish half at the end
     rep["bucket_xchg"] = sorted((getattr(plan, "bucket_xchg", None) or {}).keys())
+    # exchange geometry: looping workgroups (nx > 0, ranks sharing a GPU) or one per block (0)
+    rep["xchg_nx"] = sorted({int(v[1].nx) for v in (getattr(plan, "early_xchg", None) or {}).values()}
+                            | {int(v.nx) for v in (getattr(plan, "bucket_xchg", None) or {}).values()})
+    rep["shared"] = bool(red.xgmi.shared) if red.xgmi is not None else None
     rep["err"] = int(red.xgmi.err[0].item()) if red.xgmi is not None else -1
     rep["digest"] = hashlib.sha256(w.tobytes()).hexdigest()
     rep["finite"] = bool(np.isfinite(w).all())
     rep["moved"] = float(np.abs(w - np.concatenate([a.reshape(-1) for a in w0])).max())
     if r == 0:
-        single = zoo.rpv_cnn((64, 64, 3), use_horovod=False, **kw)
+        single = zoo.rpv_cnn(SHAPE, use_horovod=False, **kw)
         single.set_weights(w0)
         ws = train(single, data, perm.contiguous(), GLOBAL_B)
         d = np.abs(w - ws)

@@ -15,6 +15,7 @@ from cori_intml_examples_amd.parallel import hvd  # noqa: E402
 
 @pytest.fixture
 def probe_env(monkeypatch):
+    monkeypatch.setenv("INTML_PLANE_VERDICTS", "/nonexistent-dir/verdicts.json")   # (unwritable: no file)
     for k in ("INTML_XGMI", "INTML_BUCKET_BYTES", "INTML_PLANE_PROBE"):
         # setenv first so teardown restores the original state even though the probe itself
         # writes these variables
@@ -32,7 +33,7 @@ def probe_env(monkeypatch):
         x = (types.SimpleNamespace(err=[types.SimpleNamespace(item=lambda: 0)]) if plane() in ("xgmi", "hybrid")
              else None)
         m = types.SimpleNamespace(_executor=types.SimpleNamespace(reducer=types.SimpleNamespace(xgmi=x)),
-                                  plane=plane())
+                                  plane=plane(), store=types.SimpleNamespace(numel=547841))
         return m, (64, 64, 3), 1, "cfg", "metric", None
 
     monkeypatch.setattr(bench, "build", build)
@@ -60,6 +61,21 @@ def test_probe_picks_fastest_and_sets_env(probe_env):
     assert os.environ["INTML_XGMI"] == "rccl" and os.environ["INTML_BUCKET_BYTES"] == str(1 << 20)
 
 
+def test_probe_records_verdict(probe_env, monkeypatch, tmp_path):
+    """The probe's choice is persisted (rank 0) for fit()'s auto plane: the plane family under
+    the job's (host, world size, gradient size class) key."""
+    import json
+    from cori_intml_examples_amd.parallel import dist as D
+    cost, _, args = probe_env
+    monkeypatch.setenv("INTML_PLANE_VERDICTS", str(tmp_path / "v.json"))
+    cost.update(xgmi=9.0)
+    r = bench.probe_data_planes(args, 2, None, None, 128, 8)
+    assert r["chosen"] == "xgmi" and r["verdict_file"] == str(tmp_path / "v.json")
+    d = json.load(open(tmp_path / "v.json"))
+    (k, v), = d.items()
+    assert k == D.verdict_key(2, 4 * 547841) and v["plane"] == "xgmi" and v["probe_ms_per_step"]["xgmi"] > 0
+
+
 def test_probe_can_pick_hybrid(probe_env):
     cost, _, args = probe_env
     cost.update(xgmi=12.0, rccl=11.0, rccl_forked=10.5, hybrid=9.0)
@@ -68,12 +84,14 @@ def test_probe_can_pick_hybrid(probe_env):
     assert os.environ["INTML_XGMI"] == "hybrid" and os.environ["INTML_BUCKET_BYTES"] == str(1 << 20)
 
 
-def test_default_plane_is_rccl(monkeypatch):
-    """Without a probe (fit(), train_rpv) the data plane is RCCL: nothing but a measurement
-    admits xGMI."""
+def test_default_plane_is_rccl(monkeypatch, tmp_path):
+    """Without a probe verdict (fit(), train_rpv) the data plane is RCCL: nothing but a
+    measurement admits xGMI (ADVICE r2 / r5; the verdict path is tests/test_comm.py::
+    test_auto_plane)."""
     from cori_intml_examples_amd.parallel.dist import data_plane
     monkeypatch.delenv("INTML_XGMI", raising=False)
-    assert data_plane() == "rccl"
+    monkeypatch.setenv("INTML_PLANE_VERDICTS", str(tmp_path / "none.json"))
+    assert data_plane() == "rccl" and data_plane(4 * 547841) == "rccl"
     for v, want in (("auto", "rccl"), ("0", "rccl"), ("1", "xgmi"), ("xgmi", "xgmi"), ("hybrid", "hybrid")):
         monkeypatch.setenv("INTML_XGMI", v)
         assert data_plane() == want

@@ -215,14 +215,49 @@ def test_xgmi_only_reducer_is_one_fused_bucket():
 
 
 @pytest.mark.gpu
+def test_dp_step_xgmi_separate_gpu_geometry(tmp_path):
+    """the exchange geometry of SEPARATE GPUs -- one workgroup per table block
+    (no looping workgroups), the two-shot kernel's full workgroup count -- executed at P = 2 on
+    one card (INTML_TUNE=xgmi_xchg_wg=0,xgmi_shared_wg=256) with a model small enough that the
+    spinning workgroups cannot starve the peer's launches.  Same invariants as the shared-GPU
+    rehearsal: no wait times out, bit-identical ranks, close to the single-process run."""
+    env = dict(os.environ, PYTHONPATH=ROOT, INTML_DP_TIMEOUT="60", DPX_SMALL="1",
+               INTML_TUNE="xgmi_xchg_wg=0,xgmi_shared_wg=256")
+    for k in ("WORLD_SIZE", "RANK", "INTML_DP_BACKEND", "INTML_COMM", "INTML_XGMI", "INTML_BUCKET_BYTES"):
+        env.pop(k, None)
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "tests", "dp_xgmi_worker_gpu.py"), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    reps = [json.load(open(tmp_path / ("dpx%d.json" % i))) for i in range(2)]
+    for top in reps:
+        for opt in ("Adam", "SGD"):
+            rep = top[opt]
+            assert rep["shared"] and rep["xchg_nx"] == [0], rep          # shared card, separate-GPU geometry
+            assert rep["exchanged"] and rep["xchg_fin"] and rep["bucket_xchg"] == [0], rep
+            assert rep["err"] == 0 and rep["finite"] and rep["moved"] > 1e-4, rep
+    for opt in ("Adam", "SGD"):
+        assert len({top[opt]["digest"] for top in reps}) == 1
+    vs = reps[0]["SGD"]["vs_single"]
+    assert vs["max"] < 2e-3 and vs["rel"] < 0.05, vs
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("P", [2, 4, 8])
 def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
     """the 8-GPU data-parallel step end to end on one GPU.  P ranks (torchrun,
     all on GPU 0, so the RCCL-free plane is chosen on its own) train 24 captured steps (3
     replays x 8) at per-rank batch 128/P through the fused xGMI all-reduce + optimizer
     kernel, with Adam and with SGD -- the head / dense gradient pushed to its owners by the
-    first dual backward launch (producer push) and all-reduced + updated by the
-    next one (exchange), the rest by the end-of-backward reduction launch (mode-3 exchange): no wait times out, every rank ends with bit-identical weights, and those match a
+    first dual backward launch (producer push), summed by its owners in the next
+    one and updated beside the rest in the end-of-backward reduction launch (split exchange,
+    modes 4 / 5 + mode 3): no wait times out, every rank ends with bit-identical weights, and those match a
     single-process run at global batch 128 from the same weights and permutation (SGD within
     fp32 reordering; Adam within its sign-flip bound)."""
     env = dict(os.environ, PYTHONPATH=ROOT, INTML_DP_TIMEOUT="60")
@@ -255,9 +290,10 @@ def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
             assert rep["err"] == 0 and rep["finite"] and rep["moved"] > 1e-4, rep
             # the dense / head gradient was pushed to its owners from inside the backward
             assert rep["push_launches"] == ["wgrad_dgrad_conv2"] and rep["pushed"][1] > rep["pushed"][0], rep
-            # ... and all-reduced + updated by the next one (exchange): the fused kernel after the
-            # backward only had the conv layers left
-            assert rep["xchg_launches"] == ["wgrad_dgrad_conv1"] and rep["exchanged"], rep
+            # ... and all-reduced by the next one (split exchange: the owner half -- on every rank,
+            # each owns part of the RPV dense range at P <= 8) and updated with the end-of-backward
+            # table (the finish half): the fused kernel is not launched
+            assert rep["xchg_launches"] == ["wgrad_dgrad_conv1"] and rep["exchanged"] and rep["xchg_fin"], rep
     for opt in ("Adam", "SGD"):
         assert len({top[opt]["digest"] for top in reps}) == 1, [top[opt]["digest"] for top in reps]
     # SGD: linear in the gradient -- the per-rank partial sums and the all-reduce reorder the
@@ -273,32 +309,48 @@ def test_dp_step_xgmi_ranks_one_gpu(tmp_path, P):
     assert vs["max"] < 2.4e-2 and vs["rel"] < 0.1, vs
 
 
-def test_auto_plane(monkeypatch):
-    """fit()'s default data plane: xGMI (exchange inside the backward) when every rank has a GPU
-    of its own on one node, RCCL across nodes, with shared GPUs, or when pinned."""
+def test_auto_plane(monkeypatch, tmp_path):
+    """fit()'s default data plane: RCCL unless a MEASURED verdict
+    (bench.py's probe, record_verdict) exists for the job's (host, world size, gradient size
+    class); a verdict applies only where its plane can run (every rank its own GPU on one node,
+    a gradient <= 16 MB); pinned planes override."""
     import types
     from cori_intml_examples_amd.parallel import dist as D
     monkeypatch.delenv("INTML_XGMI", raising=False)
+    monkeypatch.setenv("INTML_PLANE_VERDICTS", str(tmp_path / "verdicts.json"))
     st = types.SimpleNamespace(size=8, local_size=8)
     monkeypatch.setattr(D, "is_initialized", lambda: True)
     monkeypatch.setattr(D, "_st", lambda: st)
     monkeypatch.setattr(D.torch.cuda, "is_available", lambda: True)
     monkeypatch.setattr(D.torch.cuda, "device_count", lambda: 8)
-    assert D.data_plane() == "xgmi"
-    st.local_size = 4                        # two nodes
-    assert D.data_plane() == "rccl"
+    rpv = 4 * 547841
+    assert D.data_plane(rpv) == "rccl"                   # no verdict: RCCL
+    assert D.record_verdict(8, rpv, "xgmi_end", {"xgmi_end": 0.1, "rccl": 0.11}) is not None
+    assert D.lookup_verdict(8, rpv) == "xgmi" and D.data_plane(rpv) == "xgmi"
+    assert D.data_plane(rpv + 1000) == "xgmi"            # same size class
+    assert D.data_plane(rpv // 4) == "rccl"              # another size class: not measured
+    st.size = st.local_size = 4
+    assert D.data_plane(rpv) == "rccl"                   # another world size: not measured
+    st.size = st.local_size = 8
+    st.local_size = 4                                    # two nodes
+    assert D.data_plane(rpv) == "rccl"
     st.local_size = 8
     monkeypatch.setattr(D.torch.cuda, "device_count", lambda: 1)   # ranks share a GPU
-    assert D.data_plane() == "rccl"
+    assert D.data_plane(rpv) == "rccl"
     monkeypatch.setattr(D.torch.cuda, "device_count", lambda: 8)
-    st.size = st.local_size = 1              # one rank
-    assert D.data_plane() == "rccl"
-    st.size = st.local_size = 8
-    assert D.data_plane(2 << 20) == "xgmi" and D.data_plane(138 << 20) == "rccl"   # RPV / legacy gradients
+    assert D.data_plane(138 << 20) == "rccl"             # legacy gradient: RCCL buckets
+    D.record_verdict(8, rpv, "rccl_forked")              # a later measurement overrides
+    assert D.data_plane(rpv) == "rccl"
+    D.record_verdict(8, rpv, "hybrid")
+    assert D.data_plane(rpv) == "hybrid"
     monkeypatch.setenv("INTML_XGMI", "rccl")
-    assert D.data_plane() == "rccl"
+    assert D.data_plane(rpv) == "rccl"
     monkeypatch.setenv("INTML_XGMI", "xgmi")
-    assert D.data_plane() == "xgmi"
+    assert D.data_plane(rpv) == "xgmi"
+    # a corrupt / unreadable verdict file means no verdict
+    monkeypatch.delenv("INTML_XGMI")
+    (tmp_path / "verdicts.json").write_text("{not json")
+    assert D.data_plane(rpv) == "rccl"
 
 
 def _fake_xgmi(rank=1, size=4, chunk=1024, shared=False):
@@ -374,3 +426,45 @@ def test_exchange_launch_choice():
     plan.pack_readers.append(("wgrad_conv0", 150, 160))
     assert fn(plan, "wgrad_dgrad_conv2", 100, 200) is None
     assert fn(plan, "wgrad_dgrad_conv1", 0, 10) is None     # no later dual launch
+
+
+def test_split_exchange_args():
+    """The split exchange (default): mode 1 in the reducing launch, mode 4 (owner half) over
+    exactly the table blocks this rank owns part of -- none at one rank -- and mode 5 (finish
+    half) for the end-of-backward launch; the owned block range follows the reduction map
+    (vec4: 1024 / tpe elements per block)."""
+    x, K, X = _fake_xgmi(rank=1, size=4, chunk=1024)
+    tab = K.RedTable()
+    tab.add(4096, 4096, 2, 16, 0, 4096, 2, 1, 1, 256, 16, 256, -1)     # RED_FLATW float4: elements [0, 4096)
+    assert tab.nblocks > 0
+    b = tuple(tab.owned_blocks(0, 1024, 1))
+    epb = 4096 // tab.nblocks                                          # elements per block
+    assert b == (1024 // epb, 2048 // epb)                             # rank 1 owns [1024, 2048)
+    assert tuple(tab.owned_blocks(0, 1024, 3)) == (3072 // epb, tab.nblocks)
+    assert tuple(tab.owned_blocks(8192, 1024, 0)) == (0, 0)            # the table is outside chunk 0
+    x4 = x.push_args(0, mode=4, nblk=tab.nblocks, blocks=b)
+    x5 = x.push_args(0, mode=5, nblk=tab.nblocks)
+    assert (x4.mode, x4.b_lo, x4.b_hi, x5.mode, x4.fence, x5.fence) == (4, b[0], b[1], 5, 1, 1)
+    a = K.OptimArgs()
+    with pytest.raises(ValueError, match="block range"):
+        bad = x.push_args(0, mode=4, nblk=tab.nblocks, blocks=(0, tab.nblocks + 1))
+        K.reduce_optim(0, tab, a, 0, bad)
+    with pytest.raises(ValueError, match="modes 3 \\+ 5"):
+        K.reduce_optim_end(0, tab, a, 0, x4, tab, x5)
+    # the reducer hands the executor (mode 1, mode 4, mode 5); at one rank mode 4 owns nothing
+    import types
+    from cori_intml_examples_amd.parallel.dist import NativeGradReducer
+    for size, want in ((4, b), (1, (0, 0))):
+        xx, _, _ = _fake_xgmi(rank=1 if size > 1 else 0, size=size, chunk=1024 if size > 1 else 4096)
+        red = types.SimpleNamespace(xgmi=xx, xgmi_bucket=0, buckets=[(0, 4096)], rank=xx.rank, size=size)
+        red._xgmi_lo = types.MethodType(NativeGradReducer._xgmi_lo, red)
+        trip = NativeGradReducer.exchange_args(red, 0, 4096, tab.nblocks, table=tab)
+        assert [t.mode for t in trip] == [1, 4, 5] and (trip[1].b_lo, trip[1].b_hi) == want
+
+
+def test_fence_defaults():
+    """the xGMI plane's flags are fenced by default (system-scope release + acquire,
+    the HIP memory model) -- the fence-free form is opt-in (INTML_TUNE=xgmi_fence=3)."""
+    from cori_intml_examples_amd.ops.hip import kernels
+    K = kernels()
+    assert K.XgmiArgs().fence == 1 and K.XgmiPush().fence == 1

@@ -106,7 +106,7 @@ def test_shard_indices_disjoint_cover_and_reshard():
     assert np.array_equal(shard_indices(10, 1, 3, False, 0, 0).numpy(), np.arange(3, 6))
 
 
-@pytest.mark.parametrize("scenario", ["all_init", "one_init", "uid", "hang", "selftest", "ok"])
+@pytest.mark.parametrize("scenario", ["all_init", "one_init", "uid", "hang", "late", "selftest", "ok"])
 def test_rccl_failure_falls_back_collectively(tmp_path, scenario):
     """A multi-GPU job whose RCCL data plane fails to come up -- in any phase (unique id,
     communicator construction, a rank that never joins, the numeric self-test), on every rank
@@ -125,3 +125,29 @@ def test_rccl_failure_falls_back_collectively(tmp_path, scenario):
         assert reps[0]["aborted"] == 1, reps        # rank 0's healthy communicator was aborted
     if scenario == "hang":
         assert all(rep["init_s"] < 60 for rep in reps), reps
+    if scenario == "late":
+        # rank 1's communicator came up after the deadline: the reaper aborted and closed it
+        # (no live communicator + watchdog left behind on the RCCL-free plane)
+        assert reps[1]["abandoned"] == ["closed"] and reps[1]["aborted"] == 1 and reps[1]["closed"] == 1, reps
+        assert reps[0]["abandoned"] == [] and reps[0]["aborted"] == 1, reps
+
+
+@pytest.mark.parametrize("scenario", ["ok", "diverge"])
+def test_fit_detects_divergent_rank(tmp_path, scenario):
+    """fit()'s per-epoch cross-rank weight digest: identical ranks record one
+    identical digest per epoch; a rank that diverged (injected on rank 1 at epoch 1) makes
+    fit() raise DataParallelDivergence on EVERY rank at that epoch's end, with the failing
+    record in History.dp_consistency (2 gloo ranks)."""
+    r = _torchrun(2, [os.path.join(ROOT, "tests", "dp_diverge_worker.py"), str(tmp_path), scenario], timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    reps = [json.load(open(tmp_path / ("div%d.json" % i))) for i in range(2)]
+    if scenario == "ok":
+        for rep in reps:
+            assert rep["raised"] is None and rep["epochs_done"] == 3, rep
+            assert [x["epoch"] for x in rep["records"]] == [0, 1, 2] and all(x["identical"] for x in rep["records"])
+        assert reps[0]["records"] == reps[1]["records"]
+        return
+    for rep in reps:
+        assert rep["raised"] and "epoch 1" in rep["raised"] and "[1]" in rep["raised"], rep
+        assert [x["identical"] for x in rep["records"]] == [True, False], rep
+        assert rep["records"][-1]["ranks_differing"] == [1]

@@ -189,3 +189,44 @@ def test_dist_train_px_engines_gpu():
             assert len(vl[0]) == 2 and vl[0] == vl[1] and np.all(np.isfinite(vl[0])), vl
     finally:
         cl.stop()
+
+
+def test_farm_engines_distinct_gpus_remapped(monkeypatch):
+    """farm engines pinned to DISTINCT GPU indices (the one-engine-per-GPU layout
+    of an 8-GPU node: no shared-GPU environment, every engine a one-rank-per-node RCCL
+    candidate), rehearsed on one card by remapping the indices to GPU 0 only in the engines'
+    HIP_VISIBLE_DEVICES.  %%px + hvd.init() over the two engines must come up collectively --
+    RCCL refuses two ranks on one physical device, so the phased bring-up votes both ranks onto
+    the RCCL-free plane -- and train in lockstep."""
+    from cori_intml_examples_amd import farm
+    from cori_intml_examples_amd.farm import magics
+    monkeypatch.setenv("INTML_FARM_GPU_REMAP", "*:0")
+    monkeypatch.setenv("INTML_RCCL_INIT_TIMEOUT", "30")
+    cl = farm.start_cluster(2, cluster_id="gpu_remap_%d" % os.getpid(), gpus=[0, 1], timeout=300)
+    try:
+        with cl.client() as c:
+            ar = magics.px(
+                "import os\n"
+                "import numpy as np\n"
+                "from cori_intml_examples_amd.parallel import hvd\n"
+                "from cori_intml_examples_amd.apps.rpv import build_model, train_model\n"
+                "from cori_intml_examples_amd.io.datasets import synthetic_rpv\n"
+                "shared_env = os.environ.get('INTML_COMM')\n"
+                "st = hvd.init()\n"
+                "x, y, _ = synthetic_rpv(1024, channels=1, seed=3)\n"
+                "model = build_model(x.shape[1:], conv_sizes=[8, 16, 16], fc_sizes=[32], dropout=0.2,\n"
+                "                    optimizer='Adam', lr=0.001 * hvd.size(), use_horovod=True)\n"
+                "history = train_model(model, x, y, None, None, batch_size=64, n_epochs=2, use_horovod=True, verbose=0)\n"
+                "wsum = float(sum(np.abs(w).sum() for w in model.get_weights()))\n"
+                "world = hvd.size(); plane = history.data_plane; note = st.plane\n"
+                "checks = [r['identical'] for r in history.dp_consistency]\n",
+                client=c, verbose=False, block=True)
+            dv = c[:]
+            assert dv.pull("shared_env") == [None, None]          # the distinct-GPU environment
+            assert dv.pull("world") == [2, 2]
+            ws = dv.pull("wsum")
+            assert ws[0] == ws[1], (ws, dv.pull("plane"), dv.pull("note"))
+            assert dv.pull("checks") == [[True, True], [True, True]], dv.pull("checks")
+            assert all("NativeGradReducer" in p for p in dv.pull("plane")), dv.pull("plane")
+    finally:
+        cl.stop()

@@ -183,13 +183,22 @@ def test_evaluator_timeout_kills_whole_process_group(tmp_path):
 def test_evaluator_explicit_and_shared_gpu_slots(monkeypatch):
     """Explicit slots; a slot naming one GPU twice runs 2 ranks on it (they select the RCCL-free
     xGMI data plane themselves: more local ranks than visible GPUs -- no gloo override);
-    slots_per_gpu repeats slots (several evaluations per GPU)."""
+    slots_per_gpu repeats slots (several evaluations per GPU) -- and then the GPU's concurrent
+    multi-rank evaluations use gloo (the xGMI plane bounds its spinning workgroups
+    per job, not across jobs)."""
     monkeypatch.delenv("INTML_DP_BACKEND", raising=False)
+    monkeypatch.delenv("INTML_COMM", raising=False)
+    one = hpo.Evaluator("python -c pass", gpus_per_eval=2, slots=[[0, 0]])
+    env = one._env_for([0, 0])
+    assert env["HIP_VISIBLE_DEVICES"] == "0" and "INTML_DP_BACKEND" not in env and "INTML_COMM" not in env
     ev = hpo.Evaluator("python -c pass", gpus_per_eval=2, slots=[[0, 0]], slots_per_gpu=3)
     assert ev.num_slots == 3 and ev.gpus == [0]
     assert ev.oversubscribed([0, 0]) and not ev.oversubscribed([0, 1])
+    assert ev.shared_across_slots([0, 0]) and not one.shared_across_slots([0, 0])
     env = ev._env_for([0, 0])
-    assert env["HIP_VISIBLE_DEVICES"] == "0" and "INTML_DP_BACKEND" not in env
+    assert env["HIP_VISIBLE_DEVICES"] == "0" and env["INTML_DP_BACKEND"] == "gloo" and env["INTML_COMM"] == "torch"
+    two = hpo.Evaluator("python -c pass", gpus_per_eval=2, slots=[[0, 1], [1, 2]])   # overlapping slots
+    assert two._env_for([0, 1])["INTML_DP_BACKEND"] == "gloo"
     env = hpo.Evaluator("python -c pass", gpus_per_eval=2, slots=[[2, 3]])._env_for([2, 3])
     assert env["HIP_VISIBLE_DEVICES"] == "2,3" and "INTML_DP_BACKEND" not in env
     cmd = ev.command_for(["--lr", "0.1"], [0, 0])

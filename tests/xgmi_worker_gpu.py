@@ -34,7 +34,7 @@ def adam_args(K, p, g, m, v, st, n, P):
 
 def full(r, P, dev, K, X, rep):
     n = 100003                                  # not a multiple of anything
-    x = X.create(r, P, n, dev, allgather)
+    x = X.create(r, P, n, dev, allgather, shared=True)
     rep["created"] = x is not None
     if x is None:
         return
@@ -74,7 +74,7 @@ def full(r, P, dev, K, X, rep):
     # a bucket [lo, hi) of a larger flat gradient (hybrid plane: the conv bucket)
     N, lo = 50021, 12345
     hi = N
-    xb = X.create(r, P, hi - lo, dev, allgather)
+    xb = X.create(r, P, hi - lo, dev, allgather, shared=True)
     rep["range_created"] = xb is not None
     if xb is None:
         return
@@ -101,7 +101,7 @@ def full(r, P, dev, K, X, rep):
 
 def delay(r, P, dev, K, X, rep):
     n = 4099
-    x = X.create(r, P, n, dev, allgather, timeout_s=2.0)
+    x = X.create(r, P, n, dev, allgather, timeout_s=2.0, shared=True)
     rep["created"] = x is not None
     if x is None:
         return
