@@ -138,9 +138,10 @@ def run_cray(a, n_gpu):
     cmd = ("python -m cori_intml_examples_amd.apps.train_rpv --synthetic --n-epochs %d --n-train %d "
            "--n-valid %d --batch-size %d --fom best --verbose 0" % (a.epochs, a.n_train, a.n_valid, a.batch_size))
     logd = tempfile.mkdtemp(prefix="cray-bench-")
+    # verbose: one stderr line per finished evaluation (progress for long searches)
     ev = hpo.Evaluator(cmd, gpus_per_eval=per, slots=slots, slots_per_gpu=a.evals_per_slot,
                        timeout=a.eval_timeout, cpu_slots=2 if not n_gpu else None, cwd=ROOT,
-                       env={"INTML_DEVICE": "cpu"} if not n_gpu else None)
+                       env={"INTML_DEVICE": "cpu"} if not n_gpu else None, verbose=True)
     opt = hpo.GeneticOptimizer(ev, generations=a.generations, num_demes=a.demes, pop_size=a.pop_size,
                                log_fn=os.path.join(logd, "rpv_hpo.log"), seed=0)
     t0 = time.time()

@@ -383,11 +383,54 @@ __global__ __launch_bounds__(256) void xgmi_end_kernel(float* __restrict__ grad,
   else xgmi_early_block<true>(grad, te, a, b - nc, red, xe);
 }
 
+// mode 3 with one workgroup per block (xchg_fused_block), and with END the early range's
+// finish part (mode 5) in workgroups [nc, grid) -- the optimizer kind a template parameter
+template <int KIND, bool END>
+__global__ __launch_bounds__(256) void xchg_fused_kernel(float* __restrict__ grad, const RedTable tc, const OptimArgs a,
+                                                         const XgmiPush xc, const RedTable te, const XgmiPush xe,
+                                                         int nc) {
+  __shared__ __attribute__((aligned(16))) float red[1024];
+  const int b = blockIdx.x;
+  if (!END || b < nc) {
+    if (xs_aborted(xc)) return;
+    xchg_fused_block<KIND>(grad, tc, a, b, red, xc);
+  } else {
+    if (xs_aborted(xe)) return;
+    xchg_update_block<KIND>(grad, te, a, b - nc, red, xe, 2);
+  }
+}
+
+template <bool END>
+static void launch_fused(float* grad, const RedTable& tc, const OptimArgs& a, const XgmiPush& xc, const RedTable& te,
+                         const XgmiPush& xe, int nc, int ne, hipStream_t s) {
+  const dim3 g(nc + ne), b(256);
+  switch (a.kind) {
+    case OPT_ADAM: hipLaunchKernelGGL((xchg_fused_kernel<OPT_ADAM, END>), g, b, 0, s, grad, tc, a, xc, te, xe, nc); break;
+    case OPT_NADAM: hipLaunchKernelGGL((xchg_fused_kernel<OPT_NADAM, END>), g, b, 0, s, grad, tc, a, xc, te, xe, nc); break;
+    case OPT_ADADELTA:
+      hipLaunchKernelGGL((xchg_fused_kernel<OPT_ADADELTA, END>), g, b, 0, s, grad, tc, a, xc, te, xe, nc);
+      break;
+    case OPT_RMSPROP:
+      hipLaunchKernelGGL((xchg_fused_kernel<OPT_RMSPROP, END>), g, b, 0, s, grad, tc, a, xc, te, xe, nc);
+      break;
+    default: hipLaunchKernelGGL((xchg_fused_kernel<OPT_SGD, END>), g, b, 0, s, grad, tc, a, xc, te, xe, nc); break;
+  }
+}
+
+// mode 3 goes through the fused kernel when it runs one workgroup per block and has the
+// exchange structure (peers, or xchg_p1); looping workgroups (ranks sharing a GPU) and the
+// single-GPU reduction keep the generic table kernels
+static bool fused_mode3(const XgmiPush& x) { return x.mode == 3 && !x.nx && (x.size > 1 || x.p1); }
+
 void launch_reduce_optim_end(float* grad, const RedTable& tc, const OptimArgs& a, const XgmiPush& xc,
                              const RedTable& te, const XgmiPush& xe, hipStream_t s) {
   const int nc = tc.nblocks <= 0 ? 0 : (xc.nx ? xc.nx : tc.nblocks);
   const int ne = te.nblocks <= 0 ? 0 : (xe.nx ? xe.nx : te.nblocks);
   if (nc + ne == 0) return;
+  if (fused_mode3(xc) && !xe.nx) {
+    launch_fused<true>(grad, tc, a, xc, te, xe, nc, ne, s);
+    return;
+  }
   hipLaunchKernelGGL(xgmi_end_kernel, dim3(nc + ne), dim3(256), 0, s, grad, tc, a, xc, te, xe, nc);
 }
 
@@ -397,6 +440,10 @@ void launch_reduce_optim(float* grad, const RedTable& tab, const OptimArgs& a, h
   if (xp && xp->on) {
     const int grid = xp->mode >= 2 && xp->nx ? xp->nx : (xp->mode == 4 ? xp->b_hi - xp->b_lo : tab.nblocks);
     if (grid <= 0) return;
+    if (fused_mode3(*xp)) {
+      launch_fused<false>(grad, tab, a, *xp, tab, *xp, grid, 0, s);
+      return;
+    }
     hipLaunchKernelGGL(xgmi_early_kernel, dim3(grid), dim3(256), 0, s, grad, tab, a, *xp);
     return;
   }

@@ -469,7 +469,10 @@ __device__ __forceinline__ void xchg_update_block(float* __restrict__ grad, cons
 
 // mode 3 with one block per workgroup: the slab reduction, the producer push and the exchange
 // of ONE block with the optimizer state loaded before the slab loads and the reduced partial
-// kept in registers for the owner sum (no memory round trip between the phases)
+// kept in registers for the owner sum (no memory round trip between the phases).  Its own
+// kernel (misc.hip xchg_fused_kernel, optimizer kind a template parameter): compiled into
+// xgmi_early_kernel beside the other modes it made the compiler copy the by-value RedTable /
+// XgmiPush arguments to scratch (1.6 KB per lane)
 template <int KIND>
 __device__ __forceinline__ void xchg_fused_block(float* __restrict__ grad, const RedTable& tab, const OptimArgs& a,
                                                  int blk, float* red, const XgmiPush& x) {
@@ -515,6 +518,15 @@ __device__ __forceinline__ void xchg_fused_block(float* __restrict__ grad, const
   }
 }
 
+// sticky abort (an earlier wait timed out on some rank): true = touch nothing
+__device__ __forceinline__ bool xs_aborted(const XgmiPush& x) {
+  if (x.size > 1 && xs_load(x.abort_[x.rank])) {
+    if (threadIdx.x == 0) xs_set_err(x.err, 3);
+    return true;
+  }
+  return false;
+}
+
 // workgroup r of a data-parallel table launch: mode 1 (reduce + push) one table block each;
 // mode 2 (exchange + update) and mode 3 (both, one launch: the end-of-backward bucket) one
 // block each, or x.nx workgroups looping over the blocks in order (ranks sharing a GPU; mode 3
@@ -548,16 +560,6 @@ __device__ __forceinline__ void xgmi_early_block(float* __restrict__ grad, const
         default: reduce_optim_block<OPT_SGD>(grad, tab, a, b, red); break;
       }
       __syncthreads();
-    }
-    return;
-  }
-  if (x.mode == 3 && !x.nx) {                  // one block per workgroup: fused phases
-    switch (a.kind) {
-      case OPT_ADAM: xchg_fused_block<OPT_ADAM>(grad, tab, a, r, red, x); break;
-      case OPT_NADAM: xchg_fused_block<OPT_NADAM>(grad, tab, a, r, red, x); break;
-      case OPT_ADADELTA: xchg_fused_block<OPT_ADADELTA>(grad, tab, a, r, red, x); break;
-      case OPT_RMSPROP: xchg_fused_block<OPT_RMSPROP>(grad, tab, a, r, red, x); break;
-      default: xchg_fused_block<OPT_SGD>(grad, tab, a, r, red, x); break;
     }
     return;
   }
