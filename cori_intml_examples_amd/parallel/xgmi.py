@@ -300,10 +300,7 @@ class XgmiAllreduce:
                 if x1 is None or x4 is None or x5 is None:
                     return None
                 a.grad_only = 1
-                if P > 1 or x1.bflag1[0]:
-                    K.reduce_optim(g.data_ptr(), tab, a, stream, x1)
-                else:
-                    K.reduce_optim(g.data_ptr(), tab, a, stream)
+                K.reduce_optim(g.data_ptr(), tab, a, stream, x1)
                 a.grad_only = 0
                 K.reduce_optim(g.data_ptr(), tab, a, stream, x4)
                 K.reduce_optim(g.data_ptr(), tab, a, stream, x5)
