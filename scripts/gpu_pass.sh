@@ -8,7 +8,8 @@
 #   SMOKE=1                   __graft_entry__.smoke()
 #   DRIVER=1                  the driver's exact bench command (bench.py --gpus 1 --steps 20 --warmup 5)
 #   AB="a|b|c"                interleaved bench A/B of INTML_TUNE variants ("" = defaults), with
-#                             AB_MODEL (rpv), AB_STEPS (600), AB_ROUNDS (3), AB_ENV (extra env);
+#                             AB_MODEL (rpv), AB_STEPS (600), AB_ROUNDS (3), AB_ENV (extra env),
+#                             AB_ARGS (extra bench.py flags, e.g. "--batch 1024");
 #                             a variant "ENV=v ENV2=w;tune" also sets environment for that arm
 #   BENCH="<bench args>"      one bench.py line (BENCH_ENV: extra env)
 #   PROF="rpv mnist ..."      rocprofv3 kernel stats of each model's bench step (PROF_ENV)
@@ -45,7 +46,7 @@ if [ -n "$AB" ]; then
     for v in "${VARIANTS[@]}"; do
       venv=""; tv="$v"
       if [[ "$v" == *";"* ]]; then venv="${v%%;*}"; tv="${v#*;}"; fi
-      env $AB_ENV $venv INTML_TUNE="$tv" $T 200 python bench.py --model ${AB_MODEL:-rpv} --steps ${AB_STEPS:-600} --warmup 80 --no-hpo --no-dp-delta \
+      env $AB_ENV $venv INTML_TUNE="$tv" $T 200 python bench.py --model ${AB_MODEL:-rpv} --steps ${AB_STEPS:-600} --warmup 80 --no-hpo --no-dp-delta $AB_ARGS \
         > ${O}_ab.tmp 2>&1 || { tail -n 30 ${O}_ab.tmp; exit 1; }
       line ${O}_ab.tmp "r$i [${v:-default}]" | tee -a ${O}_ab.txt
     done
