@@ -42,7 +42,8 @@ size_t wgrad_halo_lds_bytes(const WgradArgs& a, int MT, int NTT) {
   const size_t x_elems = (size_t)(((R_in * XR * XP) + 7) & ~7);
   const size_t npb32 = (size_t)((a.R * a.Wo + 31) & ~31);
   // (>= the write-through slab squares, 4 x 16 x WH_SQ floats, which reuse the buffer)
-  return std::max<size_t>(x_elems * 2 + npb32 * ldb * 2 + 64 + (size_t)(MT * 4 + 4) * 4, 4 * 16 * WH_SQ * 4);
+  // (+ 64 B of zeros and 64 B of ones: the padding / bias-tile A operands of the fragment reads)
+  return std::max<size_t>(x_elems * 2 + npb32 * ldb * 2 + 128 + (size_t)(MT * 4 + 4) * 4, 4 * 16 * WH_SQ * 4);
 }
 
 template <int MTW, int NTT, bool CS4>

@@ -48,9 +48,13 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   const int x_elems = ((R_in * XR * XP) + 7) & ~7;
   bf16* dyl = xl + x_elems;
   bf16* zl = dyl + (size_t)npb32 * ldb;             // 64 B of zeros
-  int* ktab = reinterpret_cast<int*>(zl + 32);      // [MT*4] halo offsets of k column blocks
+  bf16* ol = zl + 32;                               // 64 B of bf16 ones (the bias tile's A operand)
+  int* ktab = reinterpret_cast<int*>(zl + 64);      // [MT*4] halo offsets of k column blocks
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, i = lane & 15, g = lane >> 4;
+  // (wave via readfirstlane: the per-m-tile conditions below are then wave-uniform scalars --
+  // as per-lane values they turned the k loop into exec-masked blocks, one lgkmcnt(0) per tile)
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, i = lane & 15,
+            g = lane >> 4;
   const int mt0 = bz * MT;
   const int nt0 = by * NTT;
   const int KHW = a.KH * a.KW;
@@ -58,7 +62,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   const int MTb = MT + (do_bias ? 1 : 0);          // pseudo m-tile MT = bias (ones operand)
 
   WH_STAMP(0);
-  if (tid < 32) reinterpret_cast<uint32_t*>(zl)[tid] = 0u;
+  if (tid < 32) reinterpret_cast<uint32_t*>(zl)[tid] = tid < 16 ? 0u : 0x3F803F80u;
   for (int c = tid; c < MT * 4; c += 256) {
     const int k = (mt0 + c / 4) * 16 + 4 * (c & 3);
     const int tap = k / Cs;
@@ -82,9 +86,6 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
     tbias[u] = mt == MT && do_bias;
     ko[u] = (mt < MT) ? ktab[mt * 4 + (i & 3)] : -1;
   }
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = f2bf(1.f);
 
   f32x4 acc[MTW][NTT];
 #pragma unroll
@@ -200,9 +201,11 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
         }
   #pragma unroll
         for (int u = 0; u < MTW; ++u) {
-          const bf16* pa0 = ko[u] >= 0 ? xl + off0 + ko[u] : zl;
-          const bf16* pa1 = ko[u] >= 0 ? xl + off1 + ko[u] : zl;
-          afr[u] = tbias[u] ? ones : __builtin_shufflevector(tr_read_h(pa0), tr_read_h(pa1), 0, 1, 2, 3, 4, 5, 6, 7);
+          // branch-free: padding k columns read the zero block, the bias tile the ones block
+          const bf16* pz = tbias[u] ? ol : zl;
+          const bf16* pa0 = ko[u] >= 0 ? xl + off0 + ko[u] : pz;
+          const bf16* pa1 = ko[u] >= 0 ? xl + off1 + ko[u] : pz;
+          afr[u] = __builtin_shufflevector(tr_read_h(pa0), tr_read_h(pa1), 0, 1, 2, 3, 4, 5, 6, 7);
         }
       };
       auto mmas = [&](const bf16x8 (&afr)[MTW], const bf16x8 (&bfr)[NTT]) {
