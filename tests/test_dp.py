@@ -151,3 +151,17 @@ def test_fit_detects_divergent_rank(tmp_path, scenario):
         assert rep["raised"] and "epoch 1" in rep["raised"] and "[1]" in rep["raised"], rep
         assert [x["identical"] for x in rep["records"]] == [True, False], rep
         assert rep["records"][-1]["ranks_differing"] == [1]
+
+
+@pytest.mark.parametrize("scenario", ["rank0", "rank1"])
+def test_plane_choice_is_rank0s(tmp_path, scenario):
+    """One data plane per job (2 gloo ranks): only one rank sees an xGMI verdict for the job's
+    key; NativeGradReducer.configure broadcasts rank 0's choice, so both ranks run xGMI when
+    rank 0 has the verdict and both stay on RCCL when only rank 1 does."""
+    r = _torchrun(2, [os.path.join(ROOT, "tests", "plane_vote_worker.py"), str(tmp_path), scenario], timeout=180)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    reps = [json.load(open(tmp_path / ("vote%d.json" % i))) for i in range(2)]
+    holder = 1 if scenario == "rank1" else 0
+    assert reps[holder]["local_view"] == "xgmi" and reps[1 - holder]["local_view"] == "rccl", reps
+    want = "xgmi" if holder == 0 else "rccl"
+    assert [x["plane"] for x in reps] == [want, want], reps
