@@ -413,6 +413,7 @@ PYBIND11_MODULE(_kernels, m) {
             if (xp->mode >= 2 && xp->nx) x.n_r = xp->nx;   // (workgroups looping over the blocks)
             else if (xp->mode == 4) x.n_r = xp->b_hi - xp->b_lo;   // (the blocks it may own a part of)
             if (xp->mode == 3 || xp->mode == 5) throw std::invalid_argument("dual_halo: exchange modes 1 / 2 / 4 only");
+            // (mode 2: launch_dual_halo declines it -- the caller runs the three launches apart)
           }
         }
         const bool ok = launch_dual_halo(ca, ntc, wa, MT, NTT, splits, x, S(s));

@@ -31,6 +31,9 @@ bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT
   const size_t lds = std::max(conv_halo_lds_bytes(ca, ntc), wgrad_halo_lds_bytes(wa, MT, NTT));
   if (lds > 160 * 1024 || (x.n_r && lds < 2048)) return false;   // (the reduce body stages <= 2 KB)
   if (x.n_r && x.xp.on && x.xp.mode >= 2 && lds < 4096) return false;   // (+ the exchange's wait word)
+  // extras run the exchange's modes 1 (reduce + push) and 4 (owner half) only; a mode-2 table
+  // (the unsplit exchange, xchg_split=0) goes to the caller's separate launches
+  if (x.n_r && x.xp.on && x.xp.mode != 1 && x.xp.mode != 4) return false;
   // dgrad m-tiles per wave per pass: the TM in {4, 2} that minimises the busiest wave's
   // tile count over the block (ties -> larger TM: more fragment reuse); TM = 1 only when
   // the block has <= 4 tiles (measured: TM 1 loses its fragment reuse on longer blocks)

@@ -548,6 +548,16 @@ __device__ __forceinline__ void xgmi_early_block(float* __restrict__ grad, const
   }
   const int step = x.nx ? x.nx : (x.mode == 4 ? x.b_hi - x.b_lo : x.nblk);
   const int b0 = x.mode == 4 ? x.b_lo : 0, b1 = x.mode == 4 ? x.b_hi : x.nblk;
+  if constexpr (!M3) {
+    // the dual conv launch's extras run modes 1 and 4 only (launch_dual_halo declines the
+    // others): the owner half updates nothing, so one instantiation serves every optimizer --
+    // the five optimizer kinds of mode 2 compiled in raised the dual kernel's SGPR spills
+    for (int b = b0 + r; b < b1; b += step) {
+      xchg_update_block<OPT_SGD>(grad, tab, a, b, red, x, 1);
+      __syncthreads();
+    }
+    return;
+  }
   const int parts = x.mode == 4 ? 1 : (x.mode == 5 ? 2 : 3);
   if constexpr (M3) {
   if (x.mode == 3 && x.size == 1 && !x.p1) {   // no peers: the single-GPU reduction + update

@@ -76,14 +76,15 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   __syncthreads();
   WH_STAMP(8);
 
-  // per-wave m-tile descriptors (constant over blocks and k-steps)
+  // per-wave m-tile descriptors (constant over blocks and k-steps).  Wave-uniform state as two
+  // scalars -- the wave's valid m-tiles are u < nval, the bias tile is u == ubias -- rather than
+  // per-u flag arrays (each a 64-bit lane mask in SGPRs: they pushed the dual kernel's SGPR spills)
   int ko[MTW];
-  bool tbias[MTW], tval[MTW];
+  const int nval = max(0, min(MTW, (MTb - wave + 3) >> 2));
+  const int ubias = (do_bias && MT >= wave && ((MT - wave) & 3) == 0) ? (MT - wave) >> 2 : -1;
 #pragma unroll
   for (int u = 0; u < MTW; ++u) {
     const int mt = wave + 4 * u;
-    tval[u] = mt < MTb;
-    tbias[u] = mt == MT && do_bias;
     ko[u] = (mt < MT) ? ktab[mt * 4 + (i & 3)] : -1;
   }
 
@@ -174,6 +175,9 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       const bool rowal = (a.Wo & 31) == 0 && (npix & 31) == 0 && !(a.kperm & 2);
       const int la0 = dP0 * s * XP, la1 = dP1 * s * XP;
       int y = 0, x0 = 0;
+      // (a row-divisor form of the scalar k-step base -- widths dividing 32, RPV conv2's 16-wide
+      // rows -- measured equal, 0.0999-0.1003 vs 0.0999-0.1004 ms/step (profiles/r6_wgrad_ab.txt),
+      // and cost the dual kernels SGPR spills: not kept)
       // k-step ks's fragments (the row-aligned path's scalar position (y, x0) advances)
       auto frags = [&](const int ks, bf16x8 (&afr)[MTW], bf16x8 (&bfr)[NTT]) {
         // per-lane pixel rows of the two transposed reads (h = 0, 1).  MFMA k index 8g + j
@@ -202,7 +206,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
   #pragma unroll
         for (int u = 0; u < MTW; ++u) {
           // branch-free: padding k columns read the zero block, the bias tile the ones block
-          const bf16* pz = tbias[u] ? ol : zl;
+          const bf16* pz = u == ubias ? ol : zl;
           const bf16* pa0 = ko[u] >= 0 ? xl + off0 + ko[u] : pz;
           const bf16* pa1 = ko[u] >= 0 ? xl + off1 + ko[u] : pz;
           afr[u] = __builtin_shufflevector(tr_read_h(pa0), tr_read_h(pa1), 0, 1, 2, 3, 4, 5, 6, 7);
@@ -211,7 +215,7 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
       auto mmas = [&](const bf16x8 (&afr)[MTW], const bf16x8 (&bfr)[NTT]) {
   #pragma unroll
         for (int u = 0; u < MTW; ++u)
-          if (tval[u]) {
+          if (u < nval) {
   #pragma unroll
             for (int v = 0; v < NTT; ++v) acc[u][v] = mfma16(afr[u], bfr[v], acc[u][v]);
           }
@@ -469,11 +473,11 @@ __device__ __forceinline__ void wgrad_halo_body(const WgradArgs& a, const int MT
 #pragma unroll
   for (int u = 0; u < MTW; ++u) {
     const int mt = wave + 4 * u;
-    if (!tval[u]) continue;
+    if (u >= nval) continue;
 #pragma unroll
     for (int v = 0; v < NTT; ++v) {
       if (nt0 + v >= a.NT) continue;
-      if (tbias[u]) {   // bias tile: every row holds the column sums; row 0 lives in lanes 0..15
+      if (u == ubias) {   // bias tile: every row holds the column sums; row 0 lives in lanes 0..15
         if (g == 0) a.bslab[(size_t)bx * ld + (nt0 + v) * 16 + i] = acc[u][v][0];
         continue;
       }

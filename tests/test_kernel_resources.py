@@ -25,7 +25,12 @@ def test_dual_kernels_no_scratch():
     assert len(dual) == 4, [r["name"] for r in rows]
     assert all(r.get("scratch", 0) == 0 for r in dual), [(r["name"], r.get("scratch")) for r in dual]
     prod = [r for r in dual if "Lb0E" in r["name"]]
-    assert all(r.get("occ", 0) >= 2 and r.get("sgpr_spill", 0) <= 170 for r in prod), prod
+    # round 6: 163 (round 5: 165-167; the wgrad MFMA loop's per-tile state now two wave-uniform
+    # scalars instead of per-tile lane masks); the xGMI push / owner-half instances 208 (round 5:
+    # 297; their extras compile modes 1 and 4 only, one owner-half instantiation)
+    assert all(r.get("occ", 0) >= 2 and r.get("sgpr_spill", 0) <= 165 for r in prod), prod
+    xp = [r for r in dual if "Lb1E" in r["name"]]
+    assert all(r.get("occ", 0) >= 2 and r.get("sgpr_spill", 0) <= 215 for r in xp), xp
 
 
 def test_reduction_kernels_no_scratch():
