@@ -13,6 +13,8 @@ namespace py = pybind11;
 void launch_conv_halo(const ConvMMArgs& a, int ntc, hipStream_t s);
 size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc);
 void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s, bool big);
+bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s);
+bool conv_hs_ok(const ConvMMArgs& a, int ntc);
 long long conv_tile_big_blocks(const ConvMMArgs& a, int ntc);
 size_t conv_tile_lds_bytes(int ntc);
 void launch_wgrad_tile(const WgradArgs& a, int ntc, hipStream_t s);
@@ -357,6 +359,11 @@ PYBIND11_MODULE(_kernels, m) {
     launch_conv_tile(a, ntc, S(s), big); check_last("conv_tile"); }, py::arg("a"), py::arg("ntc"), py::arg("s"),
     py::arg("big") = false);
   m.def("conv_tile_big_blocks", &conv_tile_big_blocks);
+  m.def("conv_hs_ok", &conv_hs_ok);
+  m.def("conv_hs", [](const ConvMMArgs& a, int ntc, uintptr_t s) {
+    const bool ok = launch_conv_hs(a, ntc, S(s)); check_last("conv_hs"); return ok; },
+    py::arg("a"), py::arg("ntc"), py::arg("s"),
+    "halo-staged wide conv (stride 1, 3x3 'same', W | 256); false (nothing launched) for other shapes");
   m.def("wgrad_tile_lds_bytes", &wgrad_tile_lds_bytes);
   m.def("wgrad_tile", [](const WgradArgs& a, int ntc, uintptr_t s) {
     launch_wgrad_tile(a, ntc, S(s)); check_last("wgrad_tile"); });

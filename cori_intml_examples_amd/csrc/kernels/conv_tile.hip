@@ -354,6 +354,150 @@ __global__ __launch_bounds__(64 * NWV) void conv_gl_kernel(const ConvMMArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Halo-staged wide conv (stride 1, 3x3, 'same' padding, no pool, Cs_in % 32 == 0: the legacy
+// model's 32x32 conv3 forward and its dgrad).  conv_gl gathers the A operand per k-step --
+// every input pixel is DMA'd once per TAP (9x), and the per-CU LDS-DMA rate bounds the launch
+// (profiles/r3_legacy_ab_big_tiles.txt, r6_legacy_sequence.txt).  Here a block is RB = 256 / W
+// whole output rows of one image; for each 32-channel chunk the (RB + 2) x (W + 2) input halo is
+// DMA'd ONCE (double-buffered across chunks) and the nine taps read their A fragments from it at
+// tap-shifted offsets; only the weight fragments go through the per-k-step ring.  Per k-step the
+// DMA volume drops from 16 KB (A) + NTC KB (B) to ~2.4 KB + NTC KB.
+//   halo LDS layout: flat halo pixel fp = hr * (W + 2) + hc, 64 B per pixel (32 channels),
+//   16-byte chunk c stored at position c ^ ((fp >> 2) & 3) -- any 16 consecutive pixels (an
+//   m-tile's rows at any tap shift) then cover all 64 banks once per lane group;
+//   k order: chunk-major, tap-minor (pack index tap * cps + chunk).
+// Waves: 8 = 4 (64-row groups) x 2 (n halves), as conv_gl<NTC, 8>; the epilogue is the shared one.
+namespace {
+constexpr int HS_NBUF = 4;                 // weight ring slots (3 k-steps of DMA in flight)
+constexpr int HS_HALO_INSTR = 3;           // halo DMA instructions per wave per chunk (24 KB)
+constexpr int HS_HALO_BYTES = 8 * HS_HALO_INSTR * 1024;
+
+__device__ __forceinline__ void hs_wait(int n) {   // s_waitcnt vmcnt(n), n in [0, 8]
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
+}  // namespace
+
+template <int NTC>
+__global__ __launch_bounds__(512) void conv_hs_kernel(const ConvMMArgs a) {
+  constexpr int NWV = 8, WM = 4, NW = NTC / 2;
+  constexpr int PB = NTC / NWV;                        // weight DMA instructions per wave per k-step
+  constexpr int B_BYTES = NTC * 1024;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const ring = smem;                             // [HS_NBUF][B_BYTES]
+  char* const halo = smem + HS_NBUF * B_BYTES;         // [2][HS_HALO_BYTES]
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int W = a.W, HW = W + 2, RB = 256 / W;
+  const int nyb = a.Ho / RB;
+  const int b = (int)blockIdx.x / nyb, y0 = ((int)blockIdx.x - b * nyb) * RB;
+  const int nt0 = blockIdx.y * NTC;
+  const int cps = a.Cs_in >> 5, KS = 9 * cps;
+  const int npix_h = (RB + 2) * HW;                    // halo pixels per chunk
+  const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
+  const bf16* zero = a.zero;
+  const bf16* ximg = a.x + (size_t)b * a.H * W * a.Cs_in;
+
+  // halo chunk c -> buffer c & 1: instruction j of wave w covers flat pixels 16 (w*3 + j) ...
+  auto issue_halo = [&](int c) {
+    char* hb = halo + (c & 1) * HS_HALO_BYTES;
+#pragma unroll
+    for (int j = 0; j < HS_HALO_INSTR; ++j) {
+      const int ins = wave * HS_HALO_INSTR + j;
+      const int fp = ins * 16 + (lane >> 2);
+      const int lc = (lane & 3) ^ ((fp >> 2) & 3);       // logical chunk this lane's slot holds
+      const int hr = fp / HW, hc = fp - hr * HW;
+      const int iy = y0 - 1 + hr, ix = hc - 1;
+      const bool ok = fp < npix_h && iy >= 0 && iy < a.H && ix >= 0 && ix < W;
+      const bf16* src = ok ? ximg + ((size_t)iy * W + ix) * a.Cs_in + c * 32 + lc * 8 : zero;
+      __builtin_amdgcn_global_load_lds(src, hb + ins * 1024, 16, 0, 0);
+    }
+  };
+  // weight fragments of k-step k (chunk k / 9, tap k % 9) -> ring slot k % HS_NBUF
+  auto issue_b = [&](int k) {
+    const int c = k / 9, tap = k - c * 9;
+    const int kp = tap * cps + c;
+    char* sb = ring + (k % HS_NBUF) * B_BYTES;
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int n = wave + NWV * j;
+      const int nt = min(nt0 + n, a.NT - 1);
+      __builtin_amdgcn_global_load_lds(a.wpk + ((size_t)(kp * a.NT + nt) * 64 + lane) * 8, sb + n * 1024, 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][NW];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < NW; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // this lane's output pixel of m-tile t: block row wm * 64 + t * 16 + r -> (y, x); its halo
+  // pixel at tap (0, 0) is (y, x) (the halo starts one row / column before the image)
+  int fp0[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int pr = wm * 64 + t * 16 + r, y = pr / W, x = pr - y * W;
+    fp0[t] = y * HW + x;
+  }
+
+  // prologue: halo 0, weights of k-steps 0..2
+  issue_halo(0);
+#pragma unroll
+  for (int k = 0; k < HS_NBUF - 1; ++k)
+    if (k < KS) issue_b(k);
+  for (int st = 0; st < KS; ++st) {
+    const int c = st / 9, tap = st - c * 9;
+    // vector-memory instructions issued after B(st) by now: B(st+1), B(st+2) and the next halo
+    // if it was issued at the stage of one of them (tap 0 of a chunk: H(c+1) precedes B(st+3))
+    const int later = min(2, KS - 1 - st);
+    int younger = later * PB;
+    if (later >= 1 && (st - 2) >= 0 && (st - 2) % 9 == 0 && (st - 2) / 9 + 1 < cps) younger += HS_HALO_INSTR;
+    if (later >= 2 && (st - 1) >= 0 && (st - 1) % 9 == 0 && (st - 1) / 9 + 1 < cps) younger += HS_HALO_INSTR;
+    hs_wait(younger);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // (the barrier retired every reader of stage st-1's ring slot and, at tap 0, of chunk c-1's
+    // halo buffer: refill them)
+    if (tap == 0 && c + 1 < cps) issue_halo(c + 1);
+    if (st + HS_NBUF - 1 < KS) issue_b(st + HS_NBUF - 1);
+    const char* Bb = ring + (st % HS_NBUF) * B_BYTES;
+    const char* H = halo + (c & 1) * HS_HALO_BYTES;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    const int toff = ky * HW + kx;
+    bf16x8 af[4], bfr[NW];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int fp = fp0[t] + toff;
+      af[t] = *reinterpret_cast<const bf16x8*>(H + fp * 64 + ((g ^ ((fp >> 2) & 3)) << 4));
+    }
+#pragma unroll
+    for (int n = 0; n < NW; ++n)
+      bfr[n] = *reinterpret_cast<const bf16x8*>(Bb + ((wn * NW + n) * 64 + lane) * 16);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int n = 0; n < NW; ++n) acc[t][n] = mfma16(af[t], bfr[n], acc[t][n]);
+  }
+  __syncthreads();                                    // ring / halo reads done: epilogue scratch
+  TileRows tr;
+  tr.pool = false;
+  tr.dil = 1, tr.cy = 0, tr.cx = 0, tr.Hc = a.Ho, tr.Wc = a.Wo;
+  tr.nrows = (long long)a.B * a.Ho * a.Wo;
+  const long long row0 = ((long long)b * a.Ho + y0) * a.Wo;
+  tile_epilogue<NTC, WM>(a, tr, acc, smem, row0, nt0, step);
+}
+
+// ------------------------------------------------------------------------------------------
 // Register-staged path (unpool-on-load input).
 template <int NTC>
 __global__ __launch_bounds__(256) void conv_tile_kernel(const ConvMMArgs a) {
@@ -516,6 +660,34 @@ static void launch_t(const ConvMMArgs& a, hipStream_t s) {
     }
   }
   hipLaunchKernelGGL(conv_tile_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), conv_tile_lds_bytes(NTC), s, a);
+}
+
+// halo-staged path (conv_hs_kernel): the shapes it serves, its LDS bytes and launch
+bool conv_hs_ok(const ConvMMArgs& a, int ntc) {
+  return (ntc == 8 || ntc == 16) && a.zero != nullptr && a.in_code == nullptr && a.stride == 1 && a.in_dil == 1 &&
+         a.KH == 3 && a.KW == 3 && a.pad_t == 1 && a.pad_l == 1 && a.H == a.Ho && a.W == a.Wo && a.W >= 16 &&
+         a.W <= 64 && 256 % a.W == 0 && a.Ho % (256 / a.W) == 0 && (a.Cs_in & 31) == 0 &&
+         a.KS == 9 * (a.Cs_in >> 5) && !(a.mode == 0 && a.pool) && (256 / a.W + 2) * (a.W + 2) <= 8 * HS_HALO_INSTR * 16;
+}
+
+size_t conv_hs_lds_bytes(int ntc) {
+  const size_t ring = (size_t)HS_NBUF * ntc * 1024 + 2 * HS_HALO_BYTES;
+  const size_t ep = epilogue_bytes(ntc) * 2;          // 8 waves
+  return ring > ep ? ring : ep;
+}
+
+bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s) {
+  if (!conv_hs_ok(a, ntc)) return false;
+  const dim3 grid(a.B * (a.Ho / (256 / a.W)), (a.NT + ntc - 1) / ntc);
+  const size_t lds = conv_hs_lds_bytes(ntc);
+  if (ntc == 16) {
+    (void)hipFuncSetAttribute((const void*)conv_hs_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(conv_hs_kernel<16>, grid, dim3(512), lds, s, a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)conv_hs_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(conv_hs_kernel<8>, grid, dim3(512), lds, s, a);
+  }
+  return true;
 }
 
 // ntc: n-tiles per block; big: 256-row blocks of 8 waves (LDS-DMA path only; the host picks

@@ -208,6 +208,11 @@ class GeometryMixin:
                         if NT >= nb and K.conv_tile_big_blocks(a, nb) >= tune("conv_big_min", 512):
                             ntc, big = nb, True
                             break
+                # stride-1 3x3 'same' layers with whole-row blocks: the halo-staged kernel (each
+                # input pixel DMA'd once per 32-channel chunk instead of once per tap)
+                hs = 16 if NT >= 16 else 8
+                if tune("conv_hs", True) and NT >= 8 and K.conv_hs_ok(a, hs):
+                    return lambda s, a=a, n=hs: K.conv_hs(a, n, s)
             return lambda s, a=a, n=ntc, b=big: K.conv_tile(a, n, s, b)
         ntc = self._halo_cfg(a, NT, pool)
         return lambda s, a=a, n=ntc: K.conv_halo(a, n, s)
