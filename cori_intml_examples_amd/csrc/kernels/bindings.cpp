@@ -12,7 +12,7 @@ namespace py = pybind11;
 
 void launch_conv_halo(const ConvMMArgs& a, int ntc, hipStream_t s);
 size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc);
-void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s, bool big);
+void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s, bool big, int nbuf);
 bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s);
 bool conv_hs_ok(const ConvMMArgs& a, int ntc);
 long long conv_tile_big_blocks(const ConvMMArgs& a, int ntc);
@@ -35,7 +35,7 @@ bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT
                       const DualExtra& x, hipStream_t s);
 bool launch_dense_bwd_dual(const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da,
                            hipStream_t s);
-void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s);
+void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s, int order);
 size_t dense_wgrad_lds_bytes(int kg, int ntt);
 void launch_dense_dx(const DenseFwdArgs& a, int ntc, hipStream_t s);
 void launch_dense_bwd_pair(const WgradArgs& wa, int kg, int ntt, int splits, const DenseFwdArgs& da, int ntc,
@@ -355,9 +355,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("wgrad_halo_resident", &wgrad_halo_resident);
   m.def("head_rows_per_block", &head_rows_per_block, py::arg("fused") = false);
   m.def("conv_tile_lds_bytes", &conv_tile_lds_bytes);
-  m.def("conv_tile", [](const ConvMMArgs& a, int ntc, uintptr_t s, bool big) {
-    launch_conv_tile(a, ntc, S(s), big); check_last("conv_tile"); }, py::arg("a"), py::arg("ntc"), py::arg("s"),
-    py::arg("big") = false);
+  m.def("conv_tile", [](const ConvMMArgs& a, int ntc, uintptr_t s, bool big, int nbuf) {
+    launch_conv_tile(a, ntc, S(s), big, nbuf); check_last("conv_tile"); }, py::arg("a"), py::arg("ntc"), py::arg("s"),
+    py::arg("big") = false, py::arg("nbuf") = 4);
   m.def("conv_tile_big_blocks", &conv_tile_big_blocks);
   m.def("conv_hs_ok", &conv_hs_ok);
   m.def("conv_hs", [](const ConvMMArgs& a, int ntc, uintptr_t s) {
@@ -398,8 +398,9 @@ PYBIND11_MODULE(_kernels, m) {
     check_last("dense_bwd_dual");
     return ok;
   });
-  m.def("dense_wgrad", [](const WgradArgs& a, int kg, int ntt, int splits, uintptr_t s) {
-    launch_dense_wgrad(a, kg, ntt, splits, S(s)); check_last("dense_wgrad"); });
+  m.def("dense_wgrad", [](const WgradArgs& a, int kg, int ntt, int splits, uintptr_t s, int order) {
+    launch_dense_wgrad(a, kg, ntt, splits, S(s), order); check_last("dense_wgrad"); }, py::arg("a"), py::arg("kg"),
+    py::arg("ntt"), py::arg("splits"), py::arg("s"), py::arg("order") = 0);
   m.def("dense_wgrad_lds_bytes", &dense_wgrad_lds_bytes);
   m.def("dense_dx", [](const DenseFwdArgs& a, int ntc, uintptr_t s) {
     launch_dense_dx(a, ntc, S(s)); check_last("dense_dx"); });

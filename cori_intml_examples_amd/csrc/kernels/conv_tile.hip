@@ -692,10 +692,20 @@ bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s) {
 
 // ntc: n-tiles per block; big: 256-row blocks of 8 waves (LDS-DMA path only; the host picks
 // it when the grid still has >= 512 blocks)
-void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s, bool big) {
+void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s, bool big, int nbuf) {
   const bool gl = a.in_code == nullptr && a.zero != nullptr;
-  if (big && gl && ntc == 16) { launch_gl<16, 8>(a, s); return; }   // (a 5-deep ring measured equal)
-  if (big && gl && ntc == 8) { launch_gl<8, 8>(a, s); return; }
+  // nbuf 3: a 3-slot ring (2 k-steps of DMA in flight) -- 72 KB for the 8-tile big block, so two
+  // blocks fit a CU's LDS instead of one
+  if (big && gl && ntc == 16) {
+    if (nbuf == 3) launch_gl<16, 8, 3>(a, s);
+    else launch_gl<16, 8>(a, s);   // (a 5-deep ring measured equal)
+    return;
+  }
+  if (big && gl && ntc == 8) {
+    if (nbuf == 3) launch_gl<8, 8, 3>(a, s);
+    else launch_gl<8, 8>(a, s);
+    return;
+  }
   switch (ntc) {
     case 2: launch_t<2>(a, s); break;
     case 4: launch_t<4>(a, s); break;

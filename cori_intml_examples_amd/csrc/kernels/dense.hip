@@ -128,6 +128,36 @@ __global__ __launch_bounds__(512) void dense_lds_kernel(const DenseFwdArgs a) {
     if (st + 1 < nst) step(w1, w0, st + 1);
     if (st + 2 < nst) step(w2, w1, st + 2);
   }
+  if (a.mode == 1 && a.bt.pCs % 8 == 0) {
+    // dX epilogue: the workgroup's 128 rows x 128 columns go through LDS (the operand buffers
+    // are dead after the loop's last barrier) so that every thread finishes whole 8-column runs
+    // -- one 16-byte load of the saved activation and one 16-byte store per run, 16 threads
+    // covering 256 contiguous bytes of a row (the per-element form stored 32-byte pieces)
+    constexpr int LDE = 8 * 16 + 4;
+    float* ep = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ep[(t * 16 + g * 4 + j) * LDE + wave * 16 + r] = acc[t][j];
+    __syncthreads();
+    const BwdThrough& bt = a.bt;
+    const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
+    const int width = bt.pH * bt.pW * bt.pCs, pix = bt.pH * bt.pW;
+#pragma unroll
+    for (int q = 0; q < DL_ROWS * 16 / 512; ++q) {
+      const int e = tid + 512 * q, rr = e >> 4, c8 = e & 15;
+      const int m = mg * DL_ROWS + rr, n = nb * 128 + c8 * 8;
+      if (m >= a.M || n >= width) continue;
+      float v[8];
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(ep + rr * LDE + c8 * 8);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(ep + rr * LDE + c8 * 8 + 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { v[k] = lo[k]; v[4 + k] = hi[k]; }
+      const int px = n / bt.pCs;
+      bwd_through_store8(bt, (size_t)m * pix + px, n - px * bt.pCs, v, step);
+    }
+    return;
+  }
   if (nt >= a.NT) return;
   if (a.mode == 1) {
     const BwdThrough& bt = a.bt;

@@ -350,10 +350,25 @@ __device__ __forceinline__ void dense_dx_body(const DenseFwdArgs& a, const int b
 
 size_t dense_dx_lds_bytes(int ntc) { return (size_t)4 * 16 * (ntc * 16 + 4) * 4; }
 
+// order 0: grid (splits, feature groups, n groups), feature groups fastest.  order 1 / 2: a 1-D
+// grid with the n groups of one feature group consecutive -- the workgroups resident together
+// then cover whole rows of the [K][N] weight / optimizer-state arrays (contiguous HBM ranges
+// instead of one 16 * NTT * 4-byte strip of every row) and share their x slice; order 2 also
+// hands each XCD (dispatch round-robins workgroup ids over the 8) a contiguous range of tiles,
+// so that x slice is fetched into one L2 (needs a grid that is a multiple of 8)
 template <int KG, int NTT, bool OPT>
-__global__ __launch_bounds__(256) void dense_wgrad_kernel(const WgradArgs a) {
+__global__ __launch_bounds__(256) void dense_wgrad_kernel(const WgradArgs a, const int order) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  dense_wgrad_body<KG, NTT, OPT>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  if (order == 0) {
+    dense_wgrad_body<KG, NTT, OPT>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+    return;
+  }
+  const int ny = (a.Ktiles + KG - 1) / KG, nz = (a.NT + NTT - 1) / NTT;
+  int id = blockIdx.x;
+  if (order == 2) id = (id & 7) * (gridDim.x >> 3) + (id >> 3);
+  const int bz = id % nz;
+  id /= nz;
+  dense_wgrad_body<KG, NTT, OPT>(a, id / ny, id % ny, bz, smem);
 }
 
 template <int NTC>
@@ -408,14 +423,18 @@ static dim3 dense_dx_grid(const DenseFwdArgs& a, int ntc) {
 
 #define DW_CASES(X) X(2, 1) X(2, 2) X(2, 4) X(2, 8)
 
-void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s) {
+void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s, int order) {
   dense_wgrad_check(a, kg, ntt, splits);
-  const dim3 grid = dense_wgrad_grid(a, kg, ntt, splits);
+  dim3 grid = dense_wgrad_grid(a, kg, ntt, splits);
+  const unsigned n = grid.x * grid.y * grid.z;
+  if (order < 0 || order > 2) throw std::runtime_error("dense_wgrad: order");
+  if (order == 2 && n % 8) order = 1;
+  if (order) grid = dim3(n);
   const size_t lds = dense_wgrad_lds_bytes(kg, ntt);
 #define X(KG_, NT_)                                                                         \
   if (kg == KG_ && ntt == NT_) {                                                            \
-    if (a.opt_w >= 0) hipLaunchKernelGGL((dense_wgrad_kernel<KG_, NT_, true>), grid, dim3(256), lds, s, a); \
-    else hipLaunchKernelGGL((dense_wgrad_kernel<KG_, NT_, false>), grid, dim3(256), lds, s, a);             \
+    if (a.opt_w >= 0) hipLaunchKernelGGL((dense_wgrad_kernel<KG_, NT_, true>), grid, dim3(256), lds, s, a, order); \
+    else hipLaunchKernelGGL((dense_wgrad_kernel<KG_, NT_, false>), grid, dim3(256), lds, s, a, order);             \
     return;                                                                                 \
   }
   DW_CASES(X)

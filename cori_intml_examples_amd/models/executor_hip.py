@@ -870,7 +870,8 @@ class BatchPlan(GeometryMixin):
                     if ds.dense.use_bias:
                         wa.bslab = grad + 4 * store.spec(ds.dense, "bias").offset
                         wa.opt_b = store.spec(ds.dense, "bias").offset
-                wl = lambda s, a=wa, c=cfg: K.dense_wgrad(a, c[0], c[1], c[2], s)
+                dw_order = int(tune("dw_order", 0))
+                wl = lambda s, a=wa, c=cfg, o=dw_order: K.dense_wgrad(a, c[0], c[1], c[2], s, o)
             else:
                 wa, cfg, slab, bslab = self._wgrad_args(
                     xin, 1, 1, g.src.width, 1, 1, 1, 1, 1, 0, 0, self.dense_dh[g.j], g.Ns, g.N, bs,

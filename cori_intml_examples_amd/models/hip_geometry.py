@@ -210,10 +210,13 @@ class GeometryMixin:
                             break
                 # stride-1 3x3 'same' layers with whole-row blocks: the halo-staged kernel (each
                 # input pixel DMA'd once per 32-channel chunk instead of once per tap)
-                hs = 16 if NT >= 16 else 8
-                if tune("conv_hs", True) and NT >= 8 and K.conv_hs_ok(a, hs):
+                # (8 n-tiles per block: 116 VGPRs and 80 KB of LDS -- two blocks per CU; the
+                # all-256-channel NTC 16 block, one per CU, measured no faster than conv_gl)
+                hs = int(tune("conv_hs_ntc", 8))
+                if tune("conv_hs", True) and NT >= hs and K.conv_hs_ok(a, hs):
                     return lambda s, a=a, n=hs: K.conv_hs(a, n, s)
-            return lambda s, a=a, n=ntc, b=big: K.conv_tile(a, n, s, b)
+            nbuf = int(tune("conv_gl_nbuf", 3))
+            return lambda s, a=a, n=ntc, b=big, nb=nbuf: K.conv_tile(a, n, s, b, nb)
         ntc = self._halo_cfg(a, NT, pool)
         return lambda s, a=a, n=ntc: K.conv_halo(a, n, s)
 

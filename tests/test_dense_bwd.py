@@ -16,7 +16,7 @@ def cdiv(a, b):
     return (a + b - 1) // b
 
 
-def _wgrad(K, x, dh, N, S):
+def _wgrad(K, x, dh, N, S, order=0):
     dev = x.device
     M, width = x.shape
     NT, Ktiles = cdiv(N, 16), cdiv(width, 16)
@@ -31,15 +31,16 @@ def _wgrad(K, x, dh, N, S):
     a.Ktiles, a.dy, a.Cs_dy, a.NT, a.P = Ktiles, dh.data_ptr(), dh.shape[1], NT, M
     a.px_per_split = pps
     a.slab, a.bslab = slab.data_ptr(), bslab.data_ptr()
-    K.dense_wgrad(a, 2, ntt, S, torch.cuda.current_stream().cuda_stream)
+    K.dense_wgrad(a, 2, ntt, S, torch.cuda.current_stream().cuda_stream, order)
     torch.cuda.synchronize()
     return slab.sum(0)[:width, :N], bslab.sum(0)[:N]
 
 
 @gpu
+@pytest.mark.parametrize("order", [0, 1, 2])
 @pytest.mark.parametrize("M,width,N,S", [(40, 256, 128, 1), (128, 4096, 128, 1), (1024, 4096, 128, 2),
                                          (64, 96, 24, 1), (200, 512, 40, 2), (128, 9216, 128, 1)])
-def test_dense_wgrad_matches_fp32(M, width, N, S):
+def test_dense_wgrad_matches_fp32(M, width, N, S, order):
     from cori_intml_examples_amd.ops.hip import kernels
     K = kernels()
     dev = torch.device("cuda", 0)
@@ -48,7 +49,8 @@ def test_dense_wgrad_matches_fp32(M, width, N, S):
     x = torch.randn(M, width, generator=g).to(torch.bfloat16).to(dev)
     dh = torch.zeros(M, Ns, dtype=torch.bfloat16, device=dev)
     dh[:, :N] = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
-    gw, gb = _wgrad(K, x, dh, N, S)
+    # order 1 / 2: the 1-D grid orders (n groups of a feature group consecutive; XCD ranges)
+    gw, gb = _wgrad(K, x, dh, N, S, order)
     ref = x.float().t() @ dh.float()[:, :N]
     bref = dh.float()[:, :N].sum(0)
     assert torch.isfinite(gw).all() and torch.isfinite(gb).all()

@@ -157,6 +157,19 @@ def test_dense_and_head(kind, drop, cin, hw, n):
         gw = m.store.view(ds.dense, "kernel", grad=True).cpu()
         assert _rel(gw, a.t() @ dh) < 5e-3, "dense %d wgrad" % g.j
         assert _rel(m.store.view(ds.dense, "bias", grad=True).cpu(), dh.sum(0)) < 5e-3
+        if g.src.kind == "conv" and g.KSb:
+            # dX of a dense fed by a flattened conv: dH W^T through that conv's dropout / ReLU
+            # masks, stored as its (pooled-resolution) output gradient -- dense_dx_kernel, or
+            # dense_lds_kernel's LDS-staged epilogue for the legacy 65,536-wide layer
+            pg = ex.convs[g.src.idx]
+            xin = _f(bp.conv_out[pg.i])[..., :pg.Cout]
+            dx = (dh @ w.t()).reshape(xin.shape)
+            if pg.rate > 0:
+                dx = dx * _mask(dx.numel(), pg.rate, ex.seed, pg.stream, step).view(dx.shape)
+            if pg.relu:
+                dx = dx * (xin > 0).float()
+            got = _f(bp.conv_dy[pg.i])[..., :pg.Cout]
+            assert _rel(got, dx) < 1e-2, "dense %d dX into conv %d: %.3g" % (g.j, pg.i, _rel(got, dx))
     # head: grads from the saved head input
     hd = ex.plan.head
     a = src_val(ex.head_src)
