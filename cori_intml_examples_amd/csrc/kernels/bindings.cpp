@@ -13,8 +13,8 @@ namespace py = pybind11;
 void launch_conv_halo(const ConvMMArgs& a, int ntc, hipStream_t s);
 size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc);
 void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s, bool big, int nbuf);
-bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s);
-bool conv_hs_ok(const ConvMMArgs& a, int ntc);
+bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s, int nwv);
+bool conv_hs_ok(const ConvMMArgs& a, int ntc, int nwv);
 long long conv_tile_big_blocks(const ConvMMArgs& a, int ntc);
 size_t conv_tile_lds_bytes(int ntc);
 void launch_wgrad_tile(const WgradArgs& a, int ntc, hipStream_t s);
@@ -35,7 +35,7 @@ bool launch_dual_halo(const ConvMMArgs& ca, int ntc, const WgradArgs& wa, int MT
                       const DualExtra& x, hipStream_t s);
 bool launch_dense_bwd_dual(const WgradArgs& wa, int ktw, int ntt, int splits, const DenseFwdArgs& da,
                            hipStream_t s);
-void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s, int order);
+void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s, int order, bool late);
 size_t dense_wgrad_lds_bytes(int kg, int ntt);
 void launch_dense_dx(const DenseFwdArgs& a, int ntc, hipStream_t s);
 void launch_dense_bwd_pair(const WgradArgs& wa, int kg, int ntt, int splits, const DenseFwdArgs& da, int ntc,
@@ -359,11 +359,12 @@ PYBIND11_MODULE(_kernels, m) {
     launch_conv_tile(a, ntc, S(s), big, nbuf); check_last("conv_tile"); }, py::arg("a"), py::arg("ntc"), py::arg("s"),
     py::arg("big") = false, py::arg("nbuf") = 4);
   m.def("conv_tile_big_blocks", &conv_tile_big_blocks);
-  m.def("conv_hs_ok", &conv_hs_ok);
-  m.def("conv_hs", [](const ConvMMArgs& a, int ntc, uintptr_t s) {
-    const bool ok = launch_conv_hs(a, ntc, S(s)); check_last("conv_hs"); return ok; },
-    py::arg("a"), py::arg("ntc"), py::arg("s"),
-    "halo-staged wide conv (stride 1, 3x3 'same', W | 256); false (nothing launched) for other shapes");
+  m.def("conv_hs_ok", &conv_hs_ok, py::arg("a"), py::arg("ntc"), py::arg("nwv") = 8);
+  m.def("conv_hs", [](const ConvMMArgs& a, int ntc, uintptr_t s, int nwv) {
+    const bool ok = launch_conv_hs(a, ntc, S(s), nwv); check_last("conv_hs"); return ok; },
+    py::arg("a"), py::arg("ntc"), py::arg("s"), py::arg("nwv") = 8,
+    "halo-staged wide conv (stride 1 or the parity classes of a strided dgrad, whole-row blocks of "
+    "32 * nwv rows); false (nothing launched) for other shapes");
   m.def("wgrad_tile_lds_bytes", &wgrad_tile_lds_bytes);
   m.def("wgrad_tile", [](const WgradArgs& a, int ntc, uintptr_t s) {
     launch_wgrad_tile(a, ntc, S(s)); check_last("wgrad_tile"); });
@@ -398,9 +399,9 @@ PYBIND11_MODULE(_kernels, m) {
     check_last("dense_bwd_dual");
     return ok;
   });
-  m.def("dense_wgrad", [](const WgradArgs& a, int kg, int ntt, int splits, uintptr_t s, int order) {
-    launch_dense_wgrad(a, kg, ntt, splits, S(s), order); check_last("dense_wgrad"); }, py::arg("a"), py::arg("kg"),
-    py::arg("ntt"), py::arg("splits"), py::arg("s"), py::arg("order") = 0);
+  m.def("dense_wgrad", [](const WgradArgs& a, int kg, int ntt, int splits, uintptr_t s, int order, bool late) {
+    launch_dense_wgrad(a, kg, ntt, splits, S(s), order, late); check_last("dense_wgrad"); }, py::arg("a"),
+    py::arg("kg"), py::arg("ntt"), py::arg("splits"), py::arg("s"), py::arg("order") = 0, py::arg("late") = false);
   m.def("dense_wgrad_lds_bytes", &dense_wgrad_lds_bytes);
   m.def("dense_dx", [](const DenseFwdArgs& a, int ntc, uintptr_t s) {
     launch_dense_dx(a, ntc, S(s)); check_last("dense_dx"); });

@@ -354,26 +354,32 @@ __global__ __launch_bounds__(64 * NWV) void conv_gl_kernel(const ConvMMArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Halo-staged wide conv (stride 1, 3x3, 'same' padding, no pool, Cs_in % 32 == 0: the legacy
-// model's 32x32 conv3 forward and its dgrad).  conv_gl gathers the A operand per k-step --
-// every input pixel is DMA'd once per TAP (9x), and the per-CU LDS-DMA rate bounds the launch
-// (profiles/r3_legacy_ab_big_tiles.txt, r6_legacy_sequence.txt).  Here a block is RB = 256 / W
-// whole output rows of one image; for each 32-channel chunk the (RB + 2) x (W + 2) input halo is
-// DMA'd ONCE (double-buffered across chunks) and the nine taps read their A fragments from it at
-// tap-shifted offsets; only the weight fragments go through the per-k-step ring.  Per k-step the
-// DMA volume drops from 16 KB (A) + NTC KB (B) to ~2.4 KB + NTC KB.
-//   halo LDS layout: flat halo pixel fp = hr * (W + 2) + hc, 64 B per pixel (32 channels),
-//   16-byte chunk c stored at position c ^ ((fp >> 2) & 3) -- any 16 consecutive pixels (an
-//   m-tile's rows at any tap shift) then cover all 64 banks once per lane group;
-//   k order: chunk-major, tap-minor (pack index tap * cps + chunk).
+// Halo-staged wide conv (stride 1, Cs_in % 32 == 0, no pool: the legacy model's 32x32 conv3
+// forward and dgrad, and its two strided dgrads).  conv_gl gathers the A operand per k-step --
+// every input pixel is DMA'd once per TAP, and the per-CU LDS-DMA rate bounds the launch
+// (profiles/r3_legacy_ab_big_tiles.txt, r6_legacy_sequence.txt).  Here a block is RB = 256 / Wc
+// whole output rows of one image; for each 32-channel chunk the input halo those rows read is
+// DMA'd ONCE (double-buffered across chunks) and every tap reads its A fragments from it at a
+// tap-shifted offset; only the weight fragments go through the per-k-step ring.
+//   strided dgrad (input dilation d > 1): the output pixels split into d x d parity classes
+//   (grid.z, as conv_gl); within class (cy, cx) only the taps of one lattice contribute and
+//   output pixel (cy + d i, cx + d j) reads input (i + oy0 + ty, j + ox0 + tx) for lattice tap
+//   (ty, tx) -- a stride-1 conv on the dilated input's own grid with an nky x nkx kernel, so
+//   the same halo scheme applies (the dense-dilated form reads each input pixel ~d^2 KH KW / ...
+//   times per chunk, and conv_gl's row gather once per tap).
+//   halo LDS layout: flat halo pixel fp = hr * HWd + hc, 64 B per pixel (32 channels), 16-byte
+//   chunk c stored at position c ^ ((fp >> 2) & 3) -- any 16 consecutive pixels (an m-tile's
+//   rows at any tap shift) then cover all 64 banks once per lane group;
+//   k order: chunk-major, tap-minor.
 // Waves: 8 = 4 (64-row groups) x 2 (n halves), as conv_gl<NTC, 8>; the epilogue is the shared one.
 namespace {
 constexpr int HS_NBUF = 4;                 // weight ring slots (3 k-steps of DMA in flight)
-constexpr int HS_HALO_INSTR = 3;           // halo DMA instructions per wave per chunk (24 KB)
-constexpr int HS_HALO_BYTES = 8 * HS_HALO_INSTR * 1024;
+constexpr int HS_HALO_INSTR = 3;           // halo DMA instructions per wave per chunk (3 KB)
+__host__ __device__ constexpr int hs_halo_bytes(int nwv) { return nwv * HS_HALO_INSTR * 1024; }
+__host__ __device__ constexpr int hs_halo_pix(int nwv) { return nwv * HS_HALO_INSTR * 16; }
 
-__device__ __forceinline__ void hs_wait(int n) {   // s_waitcnt vmcnt(n), n in [0, 8]
-  switch (n) {
+__device__ __forceinline__ void hs_wait(int n) {   // s_waitcnt vmcnt(min(n, 8)) -- never less
+  switch (n) {                                     // than n outstanding is waited for
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
@@ -385,28 +391,50 @@ __device__ __forceinline__ void hs_wait(int n) {   // s_waitcnt vmcnt(n), n in [
     default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
   }
 }
+
+// per-launch geometry of the halo-staged conv (one parity class per grid.z)
+struct HsGeom {
+  int dil, cy, cx, Hc, Wc, RB, ky0, kx0, nky, nkx, oy0, ox0, HWd, HR;
+  __host__ __device__ void init(const ConvMMArgs& a, int cls, int rows) {   // rows: block rows
+    dil = a.in_dil > 1 ? a.in_dil : 1;
+    cy = cls / dil, cx = cls % dil;
+    Hc = (a.Ho - cy + dil - 1) / dil, Wc = (a.Wo - cx + dil - 1) / dil;
+    RB = Wc > 0 && Wc <= rows ? rows / Wc : 0;
+    ky0 = ((a.pad_t - cy) % dil + dil) % dil, kx0 = ((a.pad_l - cx) % dil + dil) % dil;
+    nky = ky0 < a.KH ? (a.KH - ky0 + dil - 1) / dil : 0;
+    nkx = kx0 < a.KW ? (a.KW - kx0 + dil - 1) / dil : 0;
+    oy0 = (cy - a.pad_t + ky0) / dil, ox0 = (cx - a.pad_l + kx0) / dil;   // exact: same parity
+    HWd = Wc + (nkx > 0 ? nkx - 1 : 0), HR = RB + (nky > 0 ? nky - 1 : 0);
+  }
+};
 }  // namespace
 
-template <int NTC>
-__global__ __launch_bounds__(512) void conv_hs_kernel(const ConvMMArgs a) {
-  constexpr int NWV = 8, WM = 4, NW = NTC / 2;
-  constexpr int PB = NTC / NWV;                        // weight DMA instructions per wave per k-step
+// NWV waves: 8 (256-row blocks, two per CU) or 16 (512-row blocks: half the weight DMA per MFMA)
+template <int NTC, int NWV>
+__global__ __launch_bounds__(64 * NWV) void conv_hs_kernel(const ConvMMArgs a) {
+  constexpr int WM = NWV / 2, NW = NTC / 2;
   constexpr int B_BYTES = NTC * 1024;
+  constexpr int HS_HALO_BYTES = hs_halo_bytes(NWV);
+  static_assert(NTC < NWV || NTC % NWV == 0, "uniform weight DMA per wave");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const ring = smem;                             // [HS_NBUF][B_BYTES]
   char* const halo = smem + HS_NBUF * B_BYTES;         // [2][HS_HALO_BYTES]
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WM, wn = wave / WM;
-  const int W = a.W, HW = W + 2, RB = 256 / W;
-  const int nyb = a.Ho / RB;
+  HsGeom q;
+  q.init(a, (int)blockIdx.z, 32 * NWV);
+  const int W = a.W, HWd = q.HWd, RB = q.RB, nkx = q.nkx;
+  const int nyb = q.Hc / RB;
   const int b = (int)blockIdx.x / nyb, y0 = ((int)blockIdx.x - b * nyb) * RB;
   const int nt0 = blockIdx.y * NTC;
-  const int cps = a.Cs_in >> 5, KS = 9 * cps;
-  const int npix_h = (RB + 2) * HW;                    // halo pixels per chunk
+  const int cps = a.Cs_in >> 5, ntap = q.nky * nkx, KS = ntap * cps;
+  const int npix_h = q.HR * HWd;                       // halo pixels per chunk
   const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
   const bf16* zero = a.zero;
   const bf16* ximg = a.x + (size_t)b * a.H * W * a.Cs_in;
+  // weight DMA instructions this wave issues per k-step (NTC 4: waves 0-3 one each)
+  const int nbw = NTC >= NWV ? NTC / NWV : (wave < NTC ? 1 : 0);
 
   // halo chunk c -> buffer c & 1: instruction j of wave w covers flat pixels 16 (w*3 + j) ...
   auto issue_halo = [&](int c) {
@@ -416,23 +444,32 @@ __global__ __launch_bounds__(512) void conv_hs_kernel(const ConvMMArgs a) {
       const int ins = wave * HS_HALO_INSTR + j;
       const int fp = ins * 16 + (lane >> 2);
       const int lc = (lane & 3) ^ ((fp >> 2) & 3);       // logical chunk this lane's slot holds
-      const int hr = fp / HW, hc = fp - hr * HW;
-      const int iy = y0 - 1 + hr, ix = hc - 1;
+      const int hr = fp / HWd, hc = fp - hr * HWd;
+      const int iy = y0 + q.oy0 + hr, ix = q.ox0 + hc;
       const bool ok = fp < npix_h && iy >= 0 && iy < a.H && ix >= 0 && ix < W;
       const bf16* src = ok ? ximg + ((size_t)iy * W + ix) * a.Cs_in + c * 32 + lc * 8 : zero;
       __builtin_amdgcn_global_load_lds(src, hb + ins * 1024, 16, 0, 0);
     }
   };
-  // weight fragments of k-step k (chunk k / 9, tap k % 9) -> ring slot k % HS_NBUF
-  auto issue_b = [&](int k) {
-    const int c = k / 9, tap = k - c * 9;
-    const int kp = tap * cps + c;
+  // weight fragments of k-step k = (chunk c, lattice tap (ty, tx)) -> ring slot k % HS_NBUF
+  auto issue_b = [&](int k, int c, int ty, int tx) {
+    const int kp = ((q.ky0 + ty * q.dil) * a.KW + (q.kx0 + tx * q.dil)) * cps + c;
     char* sb = ring + (k % HS_NBUF) * B_BYTES;
 #pragma unroll
-    for (int j = 0; j < PB; ++j) {
+    for (int j = 0; j < (NTC + NWV - 1) / NWV; ++j) {
       const int n = wave + NWV * j;
-      const int nt = min(nt0 + n, a.NT - 1);
-      __builtin_amdgcn_global_load_lds(a.wpk + ((size_t)(kp * a.NT + nt) * 64 + lane) * 8, sb + n * 1024, 16, 0, 0);
+      if (n < NTC) {
+        const int nt = min(nt0 + n, a.NT - 1);
+        __builtin_amdgcn_global_load_lds(a.wpk + ((size_t)(kp * a.NT + nt) * 64 + lane) * 8, sb + n * 1024, 16, 0,
+                                         0);
+      }
+    }
+  };
+  // k-step walkers (no divisions in the loop): tap-minor, chunk-major
+  auto advance = [&](int& c, int& ty, int& tx) {
+    if (++tx == nkx) {
+      tx = 0;
+      if (++ty == q.nky) { ty = 0; ++c; }
     }
   };
 
@@ -441,39 +478,64 @@ __global__ __launch_bounds__(512) void conv_hs_kernel(const ConvMMArgs a) {
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int n = 0; n < NW; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // this lane's output pixel of m-tile t: block row wm * 64 + t * 16 + r -> (y, x); its halo
-  // pixel at tap (0, 0) is (y, x) (the halo starts one row / column before the image)
+  // this lane's output pixel of m-tile t: block row wm * 64 + t * 16 + r -> class pixel (y, x);
+  // its halo pixel at lattice tap (0, 0) is (y, x) (the halo starts at the tap-(0, 0) input)
   int fp0[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const int pr = wm * 64 + t * 16 + r, y = pr / W, x = pr - y * W;
-    fp0[t] = y * HW + x;
+    const int pr = wm * 64 + t * 16 + r, y = pr / q.Wc, x = pr - y * q.Wc;
+    fp0[t] = y * HWd + x;
   }
 
-  // prologue: halo 0, weights of k-steps 0..2
-  issue_halo(0);
-#pragma unroll
-  for (int k = 0; k < HS_NBUF - 1; ++k)
-    if (k < KS) issue_b(k);
+  // counted waits: `issued` = this wave's vector-memory instructions so far; pb0..pb2 = the
+  // count right after B(st), B(st+1), B(st+2) were issued, phc / phn after H(c) / H(c+1).  Stage
+  // st needs B(st) and H(c): it waits until at most issued - max(pb0, phc) remain outstanding.
+  int issued = 0, pb0 = 0, pb1 = 0, pb2 = 0, phc = 0, phn = 0;
+  int bc = 0, bty = 0, btx = 0;                        // position of the next weight issue
+  if (KS > 0) {
+    issue_halo(0);
+    issued += HS_HALO_INSTR;
+    phc = issued;
+    issue_b(0, bc, bty, btx);
+    advance(bc, bty, btx);
+    issued += nbw;
+    pb0 = issued;
+    if (KS > 1) {
+      issue_b(1, bc, bty, btx);
+      advance(bc, bty, btx);
+      issued += nbw;
+    }
+    pb1 = issued;
+    if (KS > 2) {
+      issue_b(2, bc, bty, btx);
+      advance(bc, bty, btx);
+      issued += nbw;
+    }
+    pb2 = issued;
+  }
+  int c = 0, ty = 0, tx = 0;                           // stage st's k-step
   for (int st = 0; st < KS; ++st) {
-    const int c = st / 9, tap = st - c * 9;
-    // vector-memory instructions issued after B(st) by now: B(st+1), B(st+2) and the next halo
-    // if it was issued at the stage of one of them (tap 0 of a chunk: H(c+1) precedes B(st+3))
-    const int later = min(2, KS - 1 - st);
-    int younger = later * PB;
-    if (later >= 1 && (st - 2) >= 0 && (st - 2) % 9 == 0 && (st - 2) / 9 + 1 < cps) younger += HS_HALO_INSTR;
-    if (later >= 2 && (st - 1) >= 0 && (st - 1) % 9 == 0 && (st - 1) / 9 + 1 < cps) younger += HS_HALO_INSTR;
-    hs_wait(younger);
+    hs_wait(issued - max(pb0, phc));
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     // (the barrier retired every reader of stage st-1's ring slot and, at tap 0, of chunk c-1's
     // halo buffer: refill them)
-    if (tap == 0 && c + 1 < cps) issue_halo(c + 1);
-    if (st + HS_NBUF - 1 < KS) issue_b(st + HS_NBUF - 1);
+    const bool first = ty == 0 && tx == 0, last = ty == q.nky - 1 && tx == nkx - 1;
+    if (first && c + 1 < cps) {
+      issue_halo(c + 1);
+      issued += HS_HALO_INSTR;
+      phn = issued;
+    }
+    if (st + HS_NBUF - 1 < KS) {
+      issue_b(st + HS_NBUF - 1, bc, bty, btx);
+      advance(bc, bty, btx);
+      issued += nbw;
+    }
+    pb0 = pb1, pb1 = pb2, pb2 = issued;
+    if (last) phc = phn;
     const char* Bb = ring + (st % HS_NBUF) * B_BYTES;
     const char* H = halo + (c & 1) * HS_HALO_BYTES;
-    const int ky = tap / 3, kx = tap - ky * 3;
-    const int toff = ky * HW + kx;
+    const int toff = ty * HWd + tx;
     bf16x8 af[4], bfr[NW];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -487,13 +549,15 @@ __global__ __launch_bounds__(512) void conv_hs_kernel(const ConvMMArgs a) {
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int n = 0; n < NW; ++n) acc[t][n] = mfma16(af[t], bfr[n], acc[t][n]);
+    advance(c, ty, tx);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();                                    // ring / halo reads done: epilogue scratch
   TileRows tr;
   tr.pool = false;
-  tr.dil = 1, tr.cy = 0, tr.cx = 0, tr.Hc = a.Ho, tr.Wc = a.Wo;
-  tr.nrows = (long long)a.B * a.Ho * a.Wo;
-  const long long row0 = ((long long)b * a.Ho + y0) * a.Wo;
+  tr.dil = q.dil, tr.cy = q.cy, tr.cx = q.cx, tr.Hc = q.Hc, tr.Wc = q.Wc;
+  tr.nrows = (long long)a.B * q.Hc * q.Wc;
+  const long long row0 = ((long long)b * q.Hc + y0) * q.Wc;
   tile_epilogue<NTC, WM>(a, tr, acc, smem, row0, nt0, step);
 }
 
@@ -662,30 +726,49 @@ static void launch_t(const ConvMMArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(conv_tile_kernel<NTC>, dim3(gx, gy, d * d), dim3(256), conv_tile_lds_bytes(NTC), s, a);
 }
 
-// halo-staged path (conv_hs_kernel): the shapes it serves, its LDS bytes and launch
-bool conv_hs_ok(const ConvMMArgs& a, int ntc) {
-  return (ntc == 8 || ntc == 16) && a.zero != nullptr && a.in_code == nullptr && a.stride == 1 && a.in_dil == 1 &&
-         a.KH == 3 && a.KW == 3 && a.pad_t == 1 && a.pad_l == 1 && a.H == a.Ho && a.W == a.Wo && a.W >= 16 &&
-         a.W <= 64 && 256 % a.W == 0 && a.Ho % (256 / a.W) == 0 && (a.Cs_in & 31) == 0 &&
-         a.KS == 9 * (a.Cs_in >> 5) && !(a.mode == 0 && a.pool) && (256 / a.W + 2) * (a.W + 2) <= 8 * HS_HALO_INSTR * 16;
+// halo-staged path (conv_hs_kernel): the shapes it serves, its LDS bytes and launch.  Every
+// parity class must tile into whole (32 * nwv)-row blocks and fit its halo in the DMA slots.
+bool conv_hs_ok(const ConvMMArgs& a, int ntc, int nwv) {
+  if (!(ntc == 4 || ntc == 8 || ntc == 16) || !(nwv == 8 || nwv == 16) || (nwv == 16 && ntc == 16) || a.zero == nullptr ||
+      a.in_code != nullptr || a.stride != 1 || (a.Cs_in & 31) || (a.mode == 0 && a.pool) || a.KH > 3 || a.KW > 3 ||
+      a.KS != a.KH * a.KW * (a.Cs_in >> 5))
+    return false;
+  const int d = a.in_dil > 1 ? a.in_dil : 1;
+  if (a.Ho % d || a.Wo % d) return false;
+  for (int cls = 0; cls < d * d; ++cls) {
+    HsGeom q;
+    q.init(a, cls, 32 * nwv);
+    if (q.RB == 0 || (32 * nwv) % q.Wc || q.Hc % q.RB || q.HR * q.HWd > hs_halo_pix(nwv)) return false;
+  }
+  return true;
 }
 
-size_t conv_hs_lds_bytes(int ntc) {
-  const size_t ring = (size_t)HS_NBUF * ntc * 1024 + 2 * HS_HALO_BYTES;
-  const size_t ep = epilogue_bytes(ntc) * 2;          // 8 waves
+size_t conv_hs_lds_bytes(int ntc, int nwv) {
+  const size_t ring = (size_t)HS_NBUF * ntc * 1024 + 2 * hs_halo_bytes(nwv);
+  const size_t ep = epilogue_bytes(ntc) * nwv / 4;
   return ring > ep ? ring : ep;
 }
 
-bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s) {
-  if (!conv_hs_ok(a, ntc)) return false;
-  const dim3 grid(a.B * (a.Ho / (256 / a.W)), (a.NT + ntc - 1) / ntc);
-  const size_t lds = conv_hs_lds_bytes(ntc);
-  if (ntc == 16) {
-    (void)hipFuncSetAttribute((const void*)conv_hs_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(conv_hs_kernel<16>, grid, dim3(512), lds, s, a);
+template <int NTC, int NWV>
+static void launch_hs(const ConvMMArgs& a, hipStream_t s) {
+  HsGeom q;
+  q.init(a, 0, 32 * NWV);
+  const dim3 grid(a.B * (q.Hc / q.RB), (a.NT + NTC - 1) / NTC, q.dil * q.dil);
+  const size_t lds = conv_hs_lds_bytes(NTC, NWV);
+  auto k = conv_hs_kernel<NTC, NWV>;
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k, grid, dim3(64 * NWV), lds, s, a);
+}
+
+bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s, int nwv) {
+  if (!conv_hs_ok(a, ntc, nwv)) return false;
+  if (nwv == 16) {   // (no NTC 16 form: 1024 threads leave 128 VGPRs, and its tile spills)
+    if (ntc == 8) launch_hs<8, 16>(a, s);
+    else launch_hs<4, 16>(a, s);
   } else {
-    (void)hipFuncSetAttribute((const void*)conv_hs_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(conv_hs_kernel<8>, grid, dim3(512), lds, s, a);
+    if (ntc == 16) launch_hs<16, 8>(a, s);
+    else if (ntc == 8) launch_hs<8, 8>(a, s);
+    else launch_hs<4, 8>(a, s);
   }
   return true;
 }

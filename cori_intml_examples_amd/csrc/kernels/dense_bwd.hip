@@ -101,7 +101,9 @@ size_t dense_wgrad_lds_bytes(int kg, int ntt) {
   return std::max(stage, red + 16 * 128 * 4 + (size_t)32 * DW_PKLD * 2);
 }
 
-template <int KG, int NTT, bool OPT>
+// LATE: the optimizer state of the fused update is loaded after the chunk loop instead of
+// before it (fewer registers live across the MFMAs: 4 waves / SIMD instead of 3 for NTT 4)
+template <int KG, int NTT, bool OPT, bool LATE = false>
 __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int bx, const int by, const int bz,
                                                  char* smem) {
   using G = DwGeom<NTT>;
@@ -159,7 +161,7 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
   constexpr int C4 = NTT * 4;                                    // float4 per 16-feature row
   constexpr int NQ = (16 * C4 + 255) / 256;                      // float4 per thread per k-tile
   f32x4 op[OPT ? KG : 1][NQ], om[OPT ? KG : 1][NQ], ov[OPT ? KG : 1][NQ];
-  if constexpr (OPT) {
+  auto load_state = [&]() {
     const OptimArgs& o = a.opt;
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -174,7 +176,8 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
         om[kt][q] = (ok && o.s0) ? *reinterpret_cast<const f32x4*>(o.s0 + x) : z;
         ov[kt][q] = (ok && o.s1) ? *reinterpret_cast<const f32x4*>(o.s1 + x) : z;
       }
-  }
+  };
+  if constexpr (OPT && !LATE) load_state();
 
   // fragment read rows: lane reads rows 8g + (i>>2) (lo) and +4 (hi), 4 columns at 4*(i&3)
   const int rd = 8 * g + (i >> 2);
@@ -205,6 +208,7 @@ __device__ __forceinline__ void dense_wgrad_body(const WgradArgs& a, const int b
     __builtin_amdgcn_wave_barrier();
   }
 
+  if constexpr (OPT && LATE) load_state();
   // fixed-order cross-wave sum (w0 + w1 + w2 + w3), one 16-feature k-tile per pass
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);                   // [4 waves][16][LDR]
@@ -356,11 +360,11 @@ size_t dense_dx_lds_bytes(int ntc) { return (size_t)4 * 16 * (ntc * 16 + 4) * 4;
 // instead of one 16 * NTT * 4-byte strip of every row) and share their x slice; order 2 also
 // hands each XCD (dispatch round-robins workgroup ids over the 8) a contiguous range of tiles,
 // so that x slice is fetched into one L2 (needs a grid that is a multiple of 8)
-template <int KG, int NTT, bool OPT>
-__global__ __launch_bounds__(256) void dense_wgrad_kernel(const WgradArgs a, const int order) {
+template <int KG, int NTT, bool OPT, bool LATE = false>
+__global__ __launch_bounds__(256, LATE ? 4 : 1) void dense_wgrad_kernel(const WgradArgs a, const int order) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (order == 0) {
-    dense_wgrad_body<KG, NTT, OPT>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+    dense_wgrad_body<KG, NTT, OPT, LATE>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
     return;
   }
   const int ny = (a.Ktiles + KG - 1) / KG, nz = (a.NT + NTT - 1) / NTT;
@@ -368,7 +372,7 @@ __global__ __launch_bounds__(256) void dense_wgrad_kernel(const WgradArgs a, con
   if (order == 2) id = (id & 7) * (gridDim.x >> 3) + (id >> 3);
   const int bz = id % nz;
   id /= nz;
-  dense_wgrad_body<KG, NTT, OPT>(a, id / ny, id % ny, bz, smem);
+  dense_wgrad_body<KG, NTT, OPT, LATE>(a, id / ny, id % ny, bz, smem);
 }
 
 template <int NTC>
@@ -423,7 +427,7 @@ static dim3 dense_dx_grid(const DenseFwdArgs& a, int ntc) {
 
 #define DW_CASES(X) X(2, 1) X(2, 2) X(2, 4) X(2, 8)
 
-void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s, int order) {
+void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStream_t s, int order, bool late) {
   dense_wgrad_check(a, kg, ntt, splits);
   dim3 grid = dense_wgrad_grid(a, kg, ntt, splits);
   const unsigned n = grid.x * grid.y * grid.z;
@@ -431,6 +435,10 @@ void launch_dense_wgrad(const WgradArgs& a, int kg, int ntt, int splits, hipStre
   if (order == 2 && n % 8) order = 1;
   if (order) grid = dim3(n);
   const size_t lds = dense_wgrad_lds_bytes(kg, ntt);
+  if (late && a.opt_w >= 0 && kg == 2 && ntt == 4) {
+    hipLaunchKernelGGL((dense_wgrad_kernel<2, 4, true, true>), grid, dim3(256), lds, s, a, order);
+    return;
+  }
 #define X(KG_, NT_)                                                                         \
   if (kg == KG_ && ntt == NT_) {                                                            \
     if (a.opt_w >= 0) hipLaunchKernelGGL((dense_wgrad_kernel<KG_, NT_, true>), grid, dim3(256), lds, s, a, order); \

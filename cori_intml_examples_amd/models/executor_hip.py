@@ -860,18 +860,22 @@ class BatchPlan(GeometryMixin):
                     wa.slab = grad + 4 * sp.offset
                     wa.opt = ex._optim_args(False, defer_pack=True)
                     wa.opt_w = sp.offset
-                    # opt_nograd=1: skip storing the gradient the update consumed (legacy 1.231 ->
-                    # 1.218 ms/step, profiles/r4g_ab_legacy.txt) -- opt-in: the layer's gradient
-                    # is then not readable through the store (store.view(..., grad=True))
-                    wa.opt_nograd = int(tune("opt_nograd", False))
+                    # the gradient the update consumed is not stored (134 MB of writes for the
+                    # legacy Dense(512): 1.107 -> 1.097 ms/step, with dw_order 1.101 -> 1.086,
+                    # profiles/r6_dense_wgrad_ab.txt) -- this layer's gradient is then not
+                    # readable through the store (store.view(..., grad=True)); opt_nograd=0 keeps it
+                    wa.opt_nograd = int(tune("opt_nograd", True))
                     if ex.routes_ok:
                         wa.pk_fwd, wa.pk_NT = g.pack_fwd, g.NT
                         wa.pk_bwd, wa.pk_NTb = (g.pack_bwd, g.NTb) if g.KSb else (-1, 0)
                     if ds.dense.use_bias:
                         wa.bslab = grad + 4 * store.spec(ds.dense, "bias").offset
                         wa.opt_b = store.spec(ds.dense, "bias").offset
-                dw_order = int(tune("dw_order", 0))
-                wl = lambda s, a=wa, c=cfg, o=dw_order: K.dense_wgrad(a, c[0], c[1], c[2], s, o)
+                # grid order 1: the n groups of one feature group consecutive (whole rows of the
+                # weight / optimizer-state arrays per resident wave of workgroups; legacy -5 us)
+                dw_order = int(tune("dw_order", 1))
+                dw_late = bool(tune("dw_late", True))     # 4 waves / SIMD: legacy 1.070 -> 1.059 ms
+                wl = lambda s, a=wa, c=cfg, o=dw_order, l=dw_late: K.dense_wgrad(a, c[0], c[1], c[2], s, o, l)
             else:
                 wa, cfg, slab, bslab = self._wgrad_args(
                     xin, 1, 1, g.src.width, 1, 1, 1, 1, 1, 0, 0, self.dense_dh[g.j], g.Ns, g.N, bs,

@@ -208,13 +208,22 @@ class GeometryMixin:
                         if NT >= nb and K.conv_tile_big_blocks(a, nb) >= tune("conv_big_min", 512):
                             ntc, big = nb, True
                             break
-                # stride-1 3x3 'same' layers with whole-row blocks: the halo-staged kernel (each
-                # input pixel DMA'd once per 32-channel chunk instead of once per tap)
+                # stride-1 layers (and the parity classes of a strided dgrad) with whole-row
+                # blocks: the halo-staged kernel (each input pixel DMA'd once per 32-channel
+                # chunk instead of once per tap)
                 # (8 n-tiles per block: 116 VGPRs and 80 KB of LDS -- two blocks per CU; the
-                # all-256-channel NTC 16 block, one per CU, measured no faster than conv_gl)
+                # all-256-channel NTC 16 block, one per CU, measured no faster than conv_gl;
+                # a 64-channel strided dgrad takes 4-tile blocks)
                 hs = int(tune("conv_hs_ntc", 8))
-                if tune("conv_hs", True) and NT >= hs and K.conv_hs_ok(a, hs):
-                    return lambda s, a=a, n=hs: K.conv_hs(a, n, s)
+                if NT < hs:
+                    hs = 4 if NT >= 4 and a.in_dil > 1 else 0
+                dil_ok = a.in_dil <= 1 or tune("conv_hs_dil", True)
+                if tune("conv_hs", True) and hs and dil_ok:
+                    # 16 waves / 512-row blocks where the shape tiles into them (half the weight
+                    # DMA per MFMA), else 8 waves / 256 rows
+                    for wv in ((16, 8) if tune("conv_hs_wv", 8) == 16 else (8,)):
+                        if K.conv_hs_ok(a, hs, wv):
+                            return lambda s, a=a, n=hs, w=wv: K.conv_hs(a, n, s, w)
             nbuf = int(tune("conv_gl_nbuf", 3))
             return lambda s, a=a, n=ntc, b=big, nb=nbuf: K.conv_tile(a, n, s, b, nb)
         ntc = self._halo_cfg(a, NT, pool)

@@ -88,7 +88,8 @@ def test_dense_fused_optimizer_matches_reduction(monkeypatch):
 
 
 @gpu
-def test_dense_fused_optimizer_writes_packs_legacy(monkeypatch):
+@pytest.mark.parametrize("extra", ["", ",dw_late=1,dw_order=2"])
+def test_dense_fused_optimizer_writes_packs_legacy(monkeypatch, extra):
     """Legacy RPV (Dense(512) on a flattened 16384-wide input: its gradient is written in
     place) with the optimizer fused into the dense wgrad (dense_opt=auto, the default): the kernel
     also writes the layer's forward / backward bf16 packs from its updated-weight tile, and
@@ -104,7 +105,8 @@ def test_dense_fused_optimizer_writes_packs_legacy(monkeypatch):
     w0 = zoo.rpv_legacy_cnn((32, 32, 3), lr=1e-3, device="cuda:0").get_weights()
     out = {}
     for flag in ("auto", "0"):
-        monkeypatch.setenv("INTML_TUNE", "dense_opt=" + flag)
+        # (extra: the late optimizer-state load form at 4 waves / SIMD, the XCD-ranged grid order)
+        monkeypatch.setenv("INTML_TUNE", "dense_opt=" + flag + extra)
         m = zoo.rpv_legacy_cnn((32, 32, 3), lr=1e-3, device="cuda:0")
         m.set_weights(w0)
         for i in range(3):

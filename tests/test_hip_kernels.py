@@ -130,7 +130,10 @@ def test_conv_dgrad_bwd_through(kind, drop, cin, hw, n):
 
 
 @pytest.mark.parametrize("kind,drop,cin,hw,n", ALL)
-def test_dense_and_head(kind, drop, cin, hw, n):
+def test_dense_and_head(kind, drop, cin, hw, n, monkeypatch):
+    # (the legacy Dense(512) applies its update inside its wgrad kernel and by default does not
+    # store the gradient it consumed: keep it here so the gradient can be checked)
+    monkeypatch.setenv("INTML_TUNE", "opt_nograd=0")
     m, ex, bp, wb = _step(kind, drop, cin, hw, n)
     step = int(ex._st_i32[0].item())
 
@@ -195,3 +198,14 @@ def test_wide_convs_on_big_tiles(kind, drop, cin, monkeypatch):
     monkeypatch.setenv("INTML_TUNE", "conv_big_min=1")
     test_conv_forward(kind, drop, cin, 16, 40)
     test_conv_dgrad_bwd_through(kind, drop, cin, 16, 40)
+
+
+@pytest.mark.parametrize("tune_s", ["conv_hs_wv=16", "conv_hs_dil=0,conv_gl_nbuf=4", "conv_hs=0"])
+def test_legacy_conv_variants(tune_s, monkeypatch):
+    """The legacy bench shapes through each conv kernel form the executor can pick: the
+    halo-staged conv in 512-row / 16-wave blocks (conv3, the strided dgrads' parity classes),
+    the per-tap LDS-DMA gather with the 4-slot ring for the strided dgrads, and no halo-staged
+    conv at all -- forward and dgrad against the fp32 reference."""
+    monkeypatch.setenv("INTML_TUNE", tune_s)
+    test_conv_forward("legacy", 0.0, 1, 64, 128)
+    test_conv_dgrad_bwd_through("legacy", 0.0, 1, 64, 128)
