@@ -186,6 +186,15 @@ class GeometryMixin:
         n-tiles than a 128-channel tile needs -> use the tiled whole-batch GEMM kernels."""
         return Cs_in % 32 == 0 and KS * min(NT, 8) > 64
 
+    def _cu_count(self):
+        """Compute units of the executor's device (256 on MI355X; CPU / no device: 256)."""
+        if getattr(self, "_ncu", None) is None:
+            try:
+                self._ncu = int(torch.cuda.get_device_properties(self.ex.device).multi_processor_count)
+            except Exception:          # noqa: BLE001
+                self._ncu = 256
+        return self._ncu
+
     def _zero_buf(self):
         """Zero bytes for the LDS-DMA kernels: padded rows read from here (DMA cannot zero-fill)."""
         if getattr(self, "_zero16", None) is None:
@@ -336,8 +345,15 @@ class GeometryMixin:
         a.P = P
         tiles = cdiv(a.Ktiles * 16, 128) * cdiv(g.NT, ntc)
         per_split_bytes = a.Ktiles * 16 * g.NT * 16 * 4
-        S = max(1, min(cdiv(tune("wgrad_tile_wgs", 1024), tiles), (tune("wgrad_tile_slab_mb", 64) << 20) // per_split_bytes,
-                       cdiv(P, 256)))
+        # split count: as many workgroups as fit the machine AT ONCE (64 KB of LDS each: two per
+        # CU), never one more -- a grid a few workgroups past a whole number of residency
+        # waves runs a second wave for them and nearly doubles the launch (legacy conv3 wgrad
+        # 113 us at 486 workgroups, 185 us at 522; profiles/r6_wgrad_splits_ab.txt).  The
+        # reduction's slab bytes halve with it (end-of-step reduce + Adam 54 -> 35 us).
+        slots = tune("wgrad_tile_fill", 1) * self._cu_count() * 2
+        wgs = tune("wgrad_tile_wgs", 0)
+        S = max(1, min(cdiv(wgs, tiles) if wgs else max(1, slots // tiles),
+                       (tune("wgrad_tile_slab_mb", 64) << 20) // per_split_bytes, cdiv(P, 256)))
         a.px_per_split = cdiv(cdiv(P, S), 64) * 64
         S = cdiv(P, a.px_per_split)
         slab = torch.zeros(S, a.Ktiles * 16, g.NT * 16, dtype=torch.float32, device=dev)
