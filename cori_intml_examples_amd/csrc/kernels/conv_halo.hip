@@ -25,17 +25,22 @@ size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc) {
   const int ntab = cs4 ? a.KS * 8 : a.KS * 4;
   const int W_in = (a.Wo - 1) * a.stride + a.KW;
   const int R_in = (a.R - 1) * a.stride + a.KH;
-  const int TM = ntc >= 8 ? 2 : 4;
+  const int TM = (ntc >= 8 || (ntc == 4 && a.tm == 2)) ? 2 : 4;
   const size_t ep_wave = (size_t)TM * 16 * 2 * ntc * 16;   // bytes
   const int XP = (cs4 || !a.xpix) ? a.Cs_in : a.xpix;
   return (size_t)((ntab * 4 + 15) & ~15) + 32 + (size_t)a.KS * ntc * 64 * 16 +
          (((size_t)R_in * W_in * XP + 7) & ~(size_t)7) * 2 + 4 * ep_wave;
 }
 
+// TM: m-tiles per wave per pass -- 2 for 8 n-tiles; 4 for fewer, or 2 with 4 n-tiles when the
+// host asks (a.tm == 2: half the epilogue staging, 16 KB less LDS per workgroup)
 template <int NTC, int KCH, bool CS4>
 static void launch_h(const ConvMMArgs& a, int gx, int gy, size_t lds, hipStream_t s) {
   constexpr int TM = NTC >= 8 ? 2 : 4;
   auto k = conv_halo_kernel<NTC, TM, KCH, CS4>;
+  if constexpr (NTC == 4) {
+    if (a.tm == 2) k = conv_halo_kernel<NTC, 2, KCH, CS4>;
+  }
   if (lds > 65536) hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, dim3(gx, gy), dim3(256), lds, s, a);
 }

@@ -236,6 +236,8 @@ class GeometryMixin:
             nbuf = int(tune("conv_gl_nbuf", 3))
             return lambda s, a=a, n=ntc, b=big, nb=nbuf: K.conv_tile(a, n, s, b, nb)
         ntc = self._halo_cfg(a, NT, pool)
+        if not a.tm:
+            a.tm = int(tune("halo_tm", 0))      # 2: two m-tiles per wave per pass (4-tile blocks)
         return lambda s, a=a, n=ntc: K.conv_halo(a, n, s)
 
     def _dense_dual(self, wa, cfg, da, s):
