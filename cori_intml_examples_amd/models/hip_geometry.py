@@ -237,7 +237,10 @@ class GeometryMixin:
             return lambda s, a=a, n=ntc, b=big, nb=nbuf: K.conv_tile(a, n, s, b, nb)
         ntc = self._halo_cfg(a, NT, pool)
         if not a.tm:
-            a.tm = int(tune("halo_tm", 0))      # 2: two m-tiles per wave per pass (4-tile blocks)
+            # 4-tile blocks: two m-tiles per wave per pass -- half the epilogue staging LDS, four
+            # workgroups per CU instead of three (legacy first conv 37.7 -> 26.8 us,
+            # profiles/r6_halo_tm_ab.txt); halo_tm=4 restores the four-tile pass
+            a.tm = int(tune("halo_tm", 2))
         return lambda s, a=a, n=ntc: K.conv_halo(a, n, s)
 
     def _dense_dual(self, wa, cfg, da, s):
