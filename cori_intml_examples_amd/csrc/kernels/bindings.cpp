@@ -13,7 +13,7 @@ namespace py = pybind11;
 void launch_conv_halo(const ConvMMArgs& a, int ntc, hipStream_t s);
 size_t conv_halo_lds_bytes(const ConvMMArgs& a, int ntc);
 void launch_conv_tile(const ConvMMArgs& a, int ntc, hipStream_t s, bool big, int nbuf);
-bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s, int nwv);
+bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s, int nwv, int order);
 bool conv_hs_ok(const ConvMMArgs& a, int ntc, int nwv);
 long long conv_tile_big_blocks(const ConvMMArgs& a, int ntc);
 size_t conv_tile_lds_bytes(int ntc);
@@ -360,9 +360,9 @@ PYBIND11_MODULE(_kernels, m) {
     py::arg("big") = false, py::arg("nbuf") = 4);
   m.def("conv_tile_big_blocks", &conv_tile_big_blocks);
   m.def("conv_hs_ok", &conv_hs_ok, py::arg("a"), py::arg("ntc"), py::arg("nwv") = 8);
-  m.def("conv_hs", [](const ConvMMArgs& a, int ntc, uintptr_t s, int nwv) {
-    const bool ok = launch_conv_hs(a, ntc, S(s), nwv); check_last("conv_hs"); return ok; },
-    py::arg("a"), py::arg("ntc"), py::arg("s"), py::arg("nwv") = 8,
+  m.def("conv_hs", [](const ConvMMArgs& a, int ntc, uintptr_t s, int nwv, int order) {
+    const bool ok = launch_conv_hs(a, ntc, S(s), nwv, order); check_last("conv_hs"); return ok; },
+    py::arg("a"), py::arg("ntc"), py::arg("s"), py::arg("nwv") = 8, py::arg("order") = 0,
     "halo-staged wide conv (stride 1 or the parity classes of a strided dgrad, whole-row blocks of "
     "32 * nwv rows); false (nothing launched) for other shapes");
   m.def("wgrad_tile_lds_bytes", &wgrad_tile_lds_bytes);

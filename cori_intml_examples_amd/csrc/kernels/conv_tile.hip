@@ -410,8 +410,10 @@ struct HsGeom {
 }  // namespace
 
 // NWV waves: 8 (256-row blocks, two per CU) or 16 (512-row blocks: half the weight DMA per MFMA)
+// order 1: the n-blocks of one row block get adjacent workgroup ids on ONE XCD (dispatch
+// round-robins ids over the 8 XCDs), so the blocks that stage the same input halo share an L2
 template <int NTC, int NWV>
-__global__ __launch_bounds__(64 * NWV) void conv_hs_kernel(const ConvMMArgs a) {
+__global__ __launch_bounds__(64 * NWV) void conv_hs_kernel(const ConvMMArgs a, const int order) {
   constexpr int WM = NWV / 2, NW = NTC / 2;
   constexpr int B_BYTES = NTC * 1024;
   constexpr int HS_HALO_BYTES = hs_halo_bytes(NWV);
@@ -426,8 +428,16 @@ __global__ __launch_bounds__(64 * NWV) void conv_hs_kernel(const ConvMMArgs a) {
   q.init(a, (int)blockIdx.z, 32 * NWV);
   const int W = a.W, HWd = q.HWd, RB = q.RB, nkx = q.nkx;
   const int nyb = q.Hc / RB;
-  const int b = (int)blockIdx.x / nyb, y0 = ((int)blockIdx.x - b * nyb) * RB;
-  const int nt0 = blockIdx.y * NTC;
+  int bxx = (int)blockIdx.x, byy = (int)blockIdx.y;
+  if (order == 1) {   // (host: gridDim.x * gridDim.y % 8 == 0)
+    const int n = (int)(gridDim.x * gridDim.y);
+    int id = bxx + (int)gridDim.x * byy;
+    id = (id & 7) * (n >> 3) + (id >> 3);
+    byy = id % (int)gridDim.y;
+    bxx = id / (int)gridDim.y;
+  }
+  const int b = bxx / nyb, y0 = (bxx - b * nyb) * RB;
+  const int nt0 = byy * NTC;
   const int cps = a.Cs_in >> 5, ntap = q.nky * nkx, KS = ntap * cps;
   const int npix_h = q.HR * HWd;                       // halo pixels per chunk
   const uint32_t step = a.st ? (uint32_t)a.st->t : 0u;
@@ -750,25 +760,26 @@ size_t conv_hs_lds_bytes(int ntc, int nwv) {
 }
 
 template <int NTC, int NWV>
-static void launch_hs(const ConvMMArgs& a, hipStream_t s) {
+static void launch_hs(const ConvMMArgs& a, hipStream_t s, int order) {
   HsGeom q;
   q.init(a, 0, 32 * NWV);
   const dim3 grid(a.B * (q.Hc / q.RB), (a.NT + NTC - 1) / NTC, q.dil * q.dil);
+  if (order != 1 || grid.y < 2 || (grid.x * grid.y) % 8) order = 0;
   const size_t lds = conv_hs_lds_bytes(NTC, NWV);
   auto k = conv_hs_kernel<NTC, NWV>;
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k, grid, dim3(64 * NWV), lds, s, a);
+  hipLaunchKernelGGL(k, grid, dim3(64 * NWV), lds, s, a, order);
 }
 
-bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s, int nwv) {
+bool launch_conv_hs(const ConvMMArgs& a, int ntc, hipStream_t s, int nwv, int order) {
   if (!conv_hs_ok(a, ntc, nwv)) return false;
   if (nwv == 16) {   // (no NTC 16 form: 1024 threads leave 128 VGPRs, and its tile spills)
-    if (ntc == 8) launch_hs<8, 16>(a, s);
-    else launch_hs<4, 16>(a, s);
+    if (ntc == 8) launch_hs<8, 16>(a, s, order);
+    else launch_hs<4, 16>(a, s, order);
   } else {
-    if (ntc == 16) launch_hs<16, 8>(a, s);
-    else if (ntc == 8) launch_hs<8, 8>(a, s);
-    else launch_hs<4, 8>(a, s);
+    if (ntc == 16) launch_hs<16, 8>(a, s, order);
+    else if (ntc == 8) launch_hs<8, 8>(a, s, order);
+    else launch_hs<4, 8>(a, s, order);
   }
   return true;
 }

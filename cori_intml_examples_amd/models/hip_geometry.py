@@ -232,7 +232,10 @@ class GeometryMixin:
                     # DMA per MFMA), else 8 waves / 256 rows
                     for wv in ((16, 8) if tune("conv_hs_wv", 8) == 16 else (8,)):
                         if K.conv_hs_ok(a, hs, wv):
-                            return lambda s, a=a, n=hs, w=wv: K.conv_hs(a, n, s, w)
+                            # (1: the n-blocks of a row block adjacent on one XCD -- legacy conv3
+                            # forward 103.0 -> 101.6 us, profiles/r6_conv_hs_order_ab.txt)
+                            o = int(tune("conv_hs_order", 1))
+                            return lambda s, a=a, n=hs, w=wv, o=o: K.conv_hs(a, n, s, w, o)
             nbuf = int(tune("conv_gl_nbuf", 3))
             return lambda s, a=a, n=ntc, b=big, nb=nbuf: K.conv_tile(a, n, s, b, nb)
         ntc = self._halo_cfg(a, NT, pool)

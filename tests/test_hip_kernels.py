@@ -200,7 +200,7 @@ def test_wide_convs_on_big_tiles(kind, drop, cin, monkeypatch):
     test_conv_dgrad_bwd_through(kind, drop, cin, 16, 40)
 
 
-@pytest.mark.parametrize("tune_s", ["conv_hs_wv=16,halo_tm=4", "conv_hs_dil=0,conv_gl_nbuf=4", "conv_hs=0"])
+@pytest.mark.parametrize("tune_s", ["conv_hs_wv=16,halo_tm=4", "conv_hs_dil=0,conv_gl_nbuf=4", "conv_hs=0", "conv_hs_order=0"])
 def test_legacy_conv_variants(tune_s, monkeypatch):
     """The legacy bench shapes through each conv kernel form the executor can pick: the
     halo-staged conv in 512-row / 16-wave blocks (conv3, the strided dgrads' parity classes),
