@@ -7,7 +7,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 T="timeout -k 10"
-O=gpurun_out/r6f
+O=gpurun_out/${TAG:-r6f}
 $T 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > ${O}_tests.log 2>&1
 rc=$?; grep -E "passed|failed" ${O}_tests.log | tail -n 2
 if [ $rc -ne 0 ]; then grep -E "FAILED|ERROR" ${O}_tests.log | head -n 20; exit $rc; fi
